@@ -1,0 +1,154 @@
+/*
+ * rtenv.h -- C-ABI of librtenv.so, the MI355X-native vectorised radiotherapy
+ * environment (HIP kernels for gfx950).
+ *
+ * Drop-in boundary for the reference's hot path (rmaguado/ppo-radiotherapy):
+ *
+ *   reference                                   | this ABI
+ *   --------------------------------------------+---------------------------------
+ *   RadiotherapyEnv.__init__  environment.py:34 | rt_env_create (N envs at once)
+ *   RadiotherapyEnv.reset     environment.py:77 | rt_env_reset
+ *   RadiotherapyEnv.step      environment.py:193| rt_env_step (+ gymnasium 1.0
+ *     + SyncVectorEnv.step / NEXT_STEP autoreset|   SyncVectorEnv autoreset and
+ *     + RecordEpisodeStatistics (train.py:32-39)|   RecordEpisodeStatistics)
+ *   beam_voxels               draw_line.py:4    | rt_debug_beam (parity hook)
+ *   apply_rotation/translation transforms.py:7,62| rt_debug_pose (parity hook)
+ *   GAE loop                  train.py:163-181  | rt_gae
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; `*_d` arguments are DEVICE pointers
+ *    (caller-owned, e.g. torch tensors), host pointers are named `*_h`.
+ *  - All device work is enqueued on the caller's stream (a hipStream_t passed
+ *    as `void*`; NULL = the legacy default stream); no call synchronises the
+ *    device, allocates, or frees after rt_env_create -> the step and reset
+ *    calls are hipGraph-capturable.
+ *  - Return 0 on success or a negative RT_E* code; never abort.  The message of
+ *    the last failure on the calling thread is in rt_last_error().
+ *  - One host thread per handle (a handle is not thread-safe); handles are
+ *    independent, typically one per GPU / process.
+ */
+#ifndef RTENV_H
+#define RTENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTENV_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_EINVAL = -1,   /* bad argument / config */
+    RT_ENOMEM = -2,   /* device or host allocation failed */
+    RT_EDEVICE = -3,  /* HIP runtime error (no device, bad device id, ...) */
+    RT_ELAUNCH = -4,  /* kernel launch failed */
+    RT_ELIMIT = -5    /* a compile-time capacity was exceeded (grid, tumour size) */
+};
+
+/* info[N][RT_INFO_W] float layout written by rt_env_step (environment.py:222-241
+ * plus the RecordEpisodeStatistics / autoreset fields of gymnasium 1.0). */
+enum {
+    RT_INFO_TOTAL = 0,        /* reward_components.total                       */
+    RT_INFO_TUMOUR = 1,       /* reward_components.tumour                      */
+    RT_INFO_LUNG = 2,         /* reward_components.lung                        */
+    RT_INFO_DISTANCE = 3,     /* reward_components.distance_to_tumour          */
+    RT_INFO_DOSE_TUMOUR = 4,  /* doses.tumour  = sum(dose * tumour)            */
+    RT_INFO_DOSE_LUNG = 5,    /* doses.lung    = sum(dose * lungs)             */
+    RT_INFO_OVERSHOOT_T = 6,  /* overshoot.translation[3]  (6,7,8)             */
+    RT_INFO_OVERSHOOT_R = 9,  /* overshoot.rotation                            */
+    RT_INFO_POS = 10,         /* beam_position.translation[3] (10,11,12)       */
+    RT_INFO_DIR = 13,         /* beam_position.rotation[3]    (13,14,15)       */
+    RT_INFO_STEPPED = 16,     /* 1: env stepped; 0: this call was its autoreset */
+    RT_INFO_EP_DONE = 17,     /* 1: an episode finished on this step ("_r")    */
+    RT_INFO_EP_RETURN = 18,   /* episode.r (sum of step rewards)               */
+    RT_INFO_EP_LENGTH = 19,   /* episode.l                                     */
+    RT_INFO_W = 20
+};
+
+typedef struct rt_env rt_env; /* opaque */
+
+typedef struct {
+    /* geometry */
+    int32_t grid[3];          /* D, H, W (LUNG_SHAPE, environment.py:30) */
+    int32_t num_envs;         /* envs owned by this handle */
+    int32_t visionless;       /* 1: obs f32[9]; 0: obs f32[4,D,H,W] (environment.py:54-57) */
+    /* constants (environment.py:16-26); rt_env_config_default fills the reference values */
+    int32_t max_time_steps;   /* 100 */
+    float beam_dose;          /* 0.1 */
+    float lung_dose_threshold;   /* 0.2 */
+    float tumour_dose_threshold; /* 0.9 */
+    double min_angle_z;       /* pi/4 */
+    double movement_speed;    /* 0.2 */
+    float rotation_speed;     /* 0.5 (applied in f32, environment.py:141) */
+    double lung_dose_reward;  /* -1.0 */
+    float tumour_dose_reward; /* 10.0 (applied in f32, environment.py:169) */
+    double distance_reward;   /* -1.0 */
+    /* assets (host memory; copied to HBM by rt_env_create) */
+    const uint8_t* lungs_h;          /* u8[D*H*W] in {0,1}, C order */
+    int32_t n_tumours;               /* library size K */
+    const int32_t* tumour_voxels_h;  /* concat of sorted flat C-order indices */
+    const int64_t* tumour_offsets_h; /* [K+1] */
+    /* RNG for tumour sampling on autoreset (np.random.choice, environment.py:90) */
+    uint64_t seed;
+    int64_t env_id_base;      /* global id of env 0 of this handle (rank * N) */
+} rt_env_config;
+
+int rt_env_config_default(rt_env_config* cfg);
+
+int rt_env_create(const rt_env_config* cfg, int device, rt_env** out);
+void rt_env_destroy(rt_env* env);
+
+/* Reset the envs selected by mask_d (u8[N], NULL = all).  tumour_ids_d
+ * (i32[N], NULL = sample) picks library tumours; a negative entry samples.
+ * Writes obs for ALL envs (unselected envs report their current obs). */
+int rt_env_reset(rt_env* env, const uint8_t* mask_d, const int32_t* tumour_ids_d, float* obs_d,
+                 void* stream);
+
+/* One vectorised step with gymnasium-1.0 NEXT_STEP autoreset: an env whose
+ * previous step terminated ignores its action, resets, and returns the reset
+ * obs with reward 0 and terminated 0 (info[RT_INFO_STEPPED] = 0).
+ * actions_d f32[N,6]; obs_d f32[N,9] (visionless) or f32[N,4,D,H,W];
+ * reward_d f32[N]; terminated_d u8[N]; info_d f32[N,RT_INFO_W] (may be NULL). */
+int rt_env_step(rt_env* env, const float* actions_d, float* obs_d, float* reward_d,
+                uint8_t* terminated_d, float* info_d, void* stream);
+
+/* Tumours used by the NEXT autoreset of each env (i32[N]; negative = sample).
+ * Parity mode: replays the reference's np.random.choice draws. */
+int rt_env_set_next_tumours(rt_env* env, const int32_t* tumour_ids_d, void* stream);
+
+/* State access (device pointers into library-owned memory; valid until
+ * rt_env_destroy).  dose is f32[N][dose_stride] with the first D*H*W floats
+ * of each row used. */
+float* rt_env_dose(rt_env* env, int64_t* dose_stride);
+int rt_env_get_state(rt_env* env, double* pose_d /* f64[N,6] pos,dir */, int32_t* t_d,
+                     int32_t* tumour_d, void* stream);
+int rt_env_set_pose(rt_env* env, const double* pose_d /* f64[N,6] */, void* stream);
+int rt_env_num_envs(const rt_env* env);
+
+/* Parity hooks (same device code as the step kernels). */
+/* beam_voxels for M poses: raw splats in march order, idx_d i32[M,cap],
+ * w_d f32[M,cap], count_d i32[M] (-1 = ValueError: direction norm < eps). */
+int rt_debug_beam(const int32_t grid[3], int32_t m, const double* pos_d, const double* dir_d,
+                  int32_t cap, int32_t* idx_d, float* w_d, int32_t* count_d, void* stream);
+/* map_translation/apply_translation/map_rotation/apply_rotation for M
+ * (pos,dir,action) triples: out_d f64[M,10] = new pos[3], new dir[3],
+ * overshoot_t[3], overshoot_r. */
+int rt_debug_pose(const int32_t grid[3], int32_t m, const double* pos_d, const double* dir_d,
+                  const float* action_d, double* out_d, void* stream);
+
+/* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
+ * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */
+int rt_gae(int32_t T, int32_t N, const float* rewards_d, const float* values_d,
+           const float* dones_d, const float* next_value_d, const float* next_done_d,
+           double gamma, double gae_lambda, float* adv_d, float* ret_d, void* stream);
+
+const char* rt_last_error(void);
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTENV_H */

@@ -1,0 +1,125 @@
+"""ctypes binding of librtenv.so (include/rtenv.h).
+
+This is the same binding a maintainer would add to the reference repo (see
+INTEGRATION.md).  Device buffers are passed as raw pointers (torch
+`tensor.data_ptr()`), the stream as the raw hipStream_t of torch's current
+stream.  There is no CPU fallback: if the library is missing or fails to load
+every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import build as _build
+
+LIB_PATH = _build.OUT
+
+INFO_NAMES = {
+    "total": 0, "tumour": 1, "lung": 2, "distance_to_tumour": 3, "dose_tumour": 4, "dose_lung": 5,
+    "overshoot_t": 6, "overshoot_r": 9, "pos": 10, "dir": 13, "stepped": 16, "ep_done": 17,
+    "ep_return": 18, "ep_length": 19,
+}
+INFO_W = 20
+
+RT_ERRORS = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EDEVICE", -4: "RT_ELAUNCH", -5: "RT_ELIMIT"}
+
+# every symbol include/rtenv.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "rt_env_config_default", "rt_env_create", "rt_env_destroy", "rt_env_reset", "rt_env_step",
+    "rt_env_set_next_tumours", "rt_env_dose", "rt_env_get_state", "rt_env_set_pose", "rt_env_num_envs",
+    "rt_debug_beam", "rt_debug_pose", "rt_gae", "rt_last_error", "rt_abi_version",
+]
+
+
+class RtError(RuntimeError):
+    pass
+
+
+class RtEnvConfig(ctypes.Structure):
+    _fields_ = [
+        ("grid", ctypes.c_int32 * 3),
+        ("num_envs", ctypes.c_int32),
+        ("visionless", ctypes.c_int32),
+        ("max_time_steps", ctypes.c_int32),
+        ("beam_dose", ctypes.c_float),
+        ("lung_dose_threshold", ctypes.c_float),
+        ("tumour_dose_threshold", ctypes.c_float),
+        ("min_angle_z", ctypes.c_double),
+        ("movement_speed", ctypes.c_double),
+        ("rotation_speed", ctypes.c_float),
+        ("lung_dose_reward", ctypes.c_double),
+        ("tumour_dose_reward", ctypes.c_float),
+        ("distance_reward", ctypes.c_double),
+        ("lungs_h", ctypes.c_void_p),
+        ("n_tumours", ctypes.c_int32),
+        ("tumour_voxels_h", ctypes.c_void_p),
+        ("tumour_offsets_h", ctypes.c_void_p),
+        ("seed", ctypes.c_uint64),
+        ("env_id_base", ctypes.c_int64),
+    ]
+
+
+_lib = None
+
+
+def load(build_if_missing: bool = True):
+    """Load librtenv.so (building it first when only sources are present)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if build_if_missing and (not os.path.exists(LIB_PATH) or _build.needs_build()):
+        try:
+            _build.build()
+        except Exception as exc:  # pragma: no cover - surfaced to the caller
+            if not os.path.exists(LIB_PATH):
+                raise RtError(f"librtenv.so is missing and could not be built: {exc}") from exc
+    if not os.path.exists(LIB_PATH):
+        raise RtError(f"librtenv.so not found at {LIB_PATH}")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    sig = {
+        "rt_env_config_default": ([ctypes.POINTER(RtEnvConfig)], ctypes.c_int),
+        "rt_env_create": ([ctypes.POINTER(RtEnvConfig), ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
+        "rt_env_destroy": ([vp], None),
+        "rt_env_reset": ([vp, vp, vp, vp, vp], ctypes.c_int),
+        "rt_env_step": ([vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "rt_env_set_next_tumours": ([vp, vp, vp], ctypes.c_int),
+        "rt_env_dose": ([vp, ctypes.POINTER(i64)], vp),
+        "rt_env_get_state": ([vp, vp, vp, vp, vp], ctypes.c_int),
+        "rt_env_set_pose": ([vp, vp, vp], ctypes.c_int),
+        "rt_env_num_envs": ([vp], ctypes.c_int),
+        "rt_debug_beam": ([ctypes.POINTER(i32), i32, vp, vp, i32, vp, vp, vp, vp], ctypes.c_int),
+        "rt_debug_pose": ([ctypes.POINTER(i32), i32, vp, vp, vp, vp, vp], ctypes.c_int),
+        "rt_gae": ([i32, i32, vp, vp, vp, vp, vp, f64, f64, vp, vp, vp], ctypes.c_int),
+        "rt_last_error": ([], ctypes.c_char_p),
+        "rt_abi_version": ([], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().rt_last_error().decode(errors="replace")
+        raise RtError(f"{what} failed: {RT_ERRORS.get(rc, rc)}: {msg}")
+
+
+def ptr(t) -> int | None:
+    """Raw device pointer of a torch tensor (None passes NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(stream=None) -> int | None:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream or None
+
+
+def grid_arg(grid):
+    return (ctypes.c_int32 * 3)(*[int(x) for x in grid])

@@ -1,0 +1,1295 @@
+// rtenv.hip -- MI355X (gfx950) vectorised radiotherapy environment.
+//
+// Hot path of rmaguado/ppo-radiotherapy re-designed for CDNA4:
+//   environment.py:193-243 RadiotherapyEnv.step   -> k_pose + k_step
+//   transforms.py:7-69     apply_rotation/translation -> pose_update (k_pose)
+//   draw_line.py:4-102     beam_voxels            -> beam_setup + march_iter (k_step)
+//   environment.py:107-191 add_beam + rewards     -> k_step dense pass + tumour phase
+//   environment.py:77-105  reset                  -> k_pose/k_step RESET mode
+//   gymnasium 1.0 SyncVectorEnv NEXT_STEP autoreset + RecordEpisodeStatistics
+//   train.py:163-181       GAE                    -> k_gae
+//
+// Numerics: the reference runs numpy 2.x (NEP 50: its beam code is pure f32),
+// scipy's Rotation (f64) and OpenBLAS dot kernels (fused f64 norms).  This file
+// is compiled with -ffp-contract=off and IEEE-correct f32/f64 division and
+// sqrt so every operation rounds exactly where the reference rounds; fma() is
+// written out where OpenBLAS fuses.  See DESIGN.md "Numerics".
+//
+// Data layout in HBM (per handle = one GPU):
+//   dose      f32[N][Vpad]   Vpad = round_up(D*H*W, 1024): rows 4 KiB aligned
+//   pose      f64[N][6]      beam position + direction
+//   lung_bits u32[Vpad/32]   shared lung mask, 1 bit per voxel (L2-resident)
+//   tumour library: sorted C-order voxel lists + per-tumour sum plans
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rtenv.h"
+
+namespace {
+
+constexpr int kStepThreads = 256;
+constexpr int kUnroll = 8;               // float4 loads in flight per thread
+constexpr int kSegVoxels = 256;          // one wave's 64 x float4 footprint
+constexpr int kMaxTumourVoxels = 1024;   // capacity of the per-block tumour phase
+constexpr int kMaxGridDim = 1024;
+constexpr float kEpsF = 1e-6f;           // draw_line.py:4 (f32 under NEP 50)
+
+enum : int32_t { MODE_NOOP = 0, MODE_STEP = 1, MODE_RESET = 2 };
+enum : int32_t { FLAG_NEEDS_RESET = 1 };
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define RT_HIP(call)                                                                          \
+    do {                                                                                      \
+        hipError_t _e = (call);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return fail(RT_EDEVICE, std::string(#call) + ": " + hipGetErrorString(_e));       \
+    } while (0)
+
+#define RT_LAUNCH_CHECK(name)                                                                 \
+    do {                                                                                      \
+        hipError_t _e = hipGetLastError();                                                    \
+        if (_e != hipSuccess)                                                                 \
+            return fail(RT_ELAUNCH, std::string(name) + ": " + hipGetErrorString(_e));        \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// Per-env beam record: written by k_pose, read by k_step.  (64 B)
+// ---------------------------------------------------------------------------
+struct alignas(16) BeamSetup {
+    int32_t mode;      // MODE_*
+    int32_t niter;     // march iterations (0 = empty beam)
+    int32_t start;     // first dominant-axis voxel
+    int32_t stepdir;   // +1 / -1
+    int32_t dom, o0, o1;
+    int32_t tumour;    // tumour id after this call
+    float intery0, interz0, sgy, sgz;
+    float os_t[3];     // overshoot.translation (f32 copy for info)
+    float os_r;        // overshoot.rotation
+};
+
+struct TumourMeta {
+    int32_t vox_base;    // into tumour voxel array
+    int32_t n;           // voxel count
+    int32_t op_base;     // into op array
+    int32_t lvl_base;    // into level-end array
+    int32_t nlev;
+    int32_t result;      // slot of the final sum (-1: empty -> 0)
+    float T;             // np.sum(tumours) (exact integer in f32)
+    float obs_c[3];      // centroid observation (environment.py:261)
+    double lung_total;   // np.sum(lungs * (1 - tumours)) (exact)
+};
+
+struct Geom {
+    int32_t g[3];
+    int32_t V;
+    int32_t Vpad;
+    double S[3];
+    double normS;       // np.linalg.norm(LUNG_SHAPE) (ddot: fused)
+};
+
+struct Consts {
+    int32_t max_t;
+    float beam_dose, lung_thr, tum_thr;
+    double min_angle, cos_min_angle, move_speed;
+    float rot_speed, tum_reward;
+    double lung_reward, dist_reward;
+    float pi_f;
+};
+
+struct EnvState {
+    float* dose;          // [N][Vpad]
+    double* pose;         // [N][6]
+    int32_t* t;
+    int32_t* tumour;
+    int32_t* flags;
+    uint32_t* episode;
+    double* ep_return;
+    int32_t* ep_len;
+    int32_t* next_tumour;
+    BeamSetup* setup;
+};
+
+struct Library {
+    const uint32_t* lung_bits;
+    const int32_t* vox;
+    const uint32_t* ops;     // packed (a | b << 16); dst = n + op index
+    const int32_t* lvl_end;  // per level: op index end (relative to op_base)
+    const TumourMeta* meta;
+    int32_t K;
+};
+
+// ---------------------------------------------------------------------------
+// Device numerics helpers
+// ---------------------------------------------------------------------------
+
+// np.linalg.norm(f64[n]) = sqrt(ddot) with the OpenBLAS tail loop fused.
+__device__ __forceinline__ double ddot_norm3(double a, double b, double c) {
+    return sqrt(fma(c, c, fma(b, b, a * a)));
+}
+
+// np.linalg.norm(f32[3]): OpenBLAS sdot sums fl32 products in a double, then
+// numpy applies sqrtf to the float result.
+__device__ __forceinline__ float sdot_norm3(float a, float b, float c) {
+    float p0 = a * a, p1 = b * b, p2 = c * c;
+    double acc = 0.0;
+    acc += (double)p0;
+    acc += (double)p1;
+    acc += (double)p2;
+    return sqrtf((float)acc);
+}
+
+__device__ __forceinline__ float clip01(float x) {
+    x = x < 0.0f ? 0.0f : x;
+    return x > 1.0f ? 1.0f : x;
+}
+
+// Philox4x32-10 (counter-based RNG for tumour sampling on autoreset).
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
+        uint32_t lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// ---------------------------------------------------------------------------
+// transforms.py / environment.py:112-143 (f64 pose update, one lane)
+// ---------------------------------------------------------------------------
+struct PoseOut {
+    double pos[3], dir[3], os_t[3], os_r;
+};
+
+__device__ void pose_update(const Geom& G, const Consts& C, const double pos[3], const double dir[3],
+                            const float a[6], PoseOut& o) {
+    // map_translation (environment.py:122-126) + apply_translation (transforms.py:62-69)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float c = a[i] < -1.0f ? -1.0f : (a[i] > 1.0f ? 1.0f : a[i]);
+        double tr = ((double)c * G.S[i]) * C.move_speed;
+        double raw = pos[i] + tr;
+        double cl = raw < 0.0 ? 0.0 : raw;
+        cl = cl > G.S[i] ? G.S[i] : cl;
+        o.pos[i] = cl;
+        o.os_t[i] = fabs(raw - cl);
+    }
+    // map_rotation (environment.py:139-143): f32 under NEP 50
+    double r[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float c = a[3 + i] < -1.0f ? -1.0f : (a[3 + i] > 1.0f ? 1.0f : a[3 + i]);
+        r[i] = (double)((c * C.pi_f) * C.rot_speed);
+    }
+    // apply_rotation (transforms.py:7-59); scipy Rotation.from_rotvec().apply()
+    double n0 = ddot_norm3(dir[0], dir[1], dir[2]);
+    double d0 = dir[0] / n0, d1 = dir[1] / n0, d2 = dir[2] / n0;
+    double ang = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    double s;
+    if (ang <= 1e-3) {
+        double a2 = ang * ang;
+        s = 0.5 - a2 / 48.0 + a2 * a2 / 3840.0;
+    } else {
+        s = sin(ang / 2.0) / ang;
+    }
+    double qx = s * r[0], qy = s * r[1], qz = s * r[2], qw = cos(ang / 2.0);
+    double x2 = qx * qx, y2 = qy * qy, z2 = qz * qz, w2 = qw * qw;
+    double xy = qx * qy, zw = qz * qw, xz = qx * qz, yw = qy * qw, yz = qy * qz, xw = qx * qw;
+    double m00 = x2 - y2 - z2 + w2, m01 = 2.0 * (xy - zw), m02 = 2.0 * (xz + yw);
+    double m10 = 2.0 * (xy + zw), m11 = -x2 + y2 - z2 + w2, m12 = 2.0 * (yz - xw);
+    double m20 = 2.0 * (xz - yw), m21 = 2.0 * (yz + xw), m22 = -x2 - y2 + z2 + w2;
+    // einsum row order on the reference host: (m0*v0 + m2*v2) + m1*v1
+    double rd0 = (m00 * d0 + m02 * d2) + m01 * d1;
+    double rd1 = (m10 * d0 + m12 * d2) + m11 * d1;
+    double rd2 = (m20 * d0 + m22 * d2) + m21 * d1;
+    double n1 = ddot_norm3(rd0, rd1, rd2);
+    rd0 = rd0 / n1;
+    rd1 = rd1 / n1;
+    rd2 = rd2 / n1;
+    double zc = rd0 < -1.0 ? -1.0 : (rd0 > 1.0 ? 1.0 : rd0);
+    double sgn = zc > 0.0 ? 1.0 : (zc < 0.0 ? -1.0 : 0.0);
+    double angz = acos(zc);
+    if (sgn < 0.0) angz = M_PI - angz;
+    double nd0, nd1, nd2;
+    if (fabs(angz) < C.min_angle) {
+        double tz = sgn * C.cos_min_angle;
+        double txy = sqrt(1.0 - tz * tz);
+        double x = rd1, y = rd2;
+        double nxy = sqrt(fma(y, y, x * x));
+        if (nxy < 1e-8) {
+            x = 1.0;
+            y = 0.0;
+        } else {
+            x = x / nxy;
+            y = y / nxy;
+        }
+        nd0 = tz;
+        nd1 = x * txy;
+        nd2 = y * txy;
+    } else {
+        nd0 = rd0;
+        nd1 = rd1;
+        nd2 = rd2;
+    }
+    double n2 = ddot_norm3(nd0, nd1, nd2);
+    o.dir[0] = nd0 / n2;
+    o.dir[1] = nd1 / n2;
+    o.dir[2] = nd2 / n2;
+    double os = C.min_angle - angz;
+    o.os_r = os > 0.0 ? os : 0.0;
+}
+
+// ---------------------------------------------------------------------------
+// draw_line.py:17-66 (f32): ray/box clip and march parameters.
+// Returns -1 on the ValueError path (norm < eps), else 0 (niter may be 0).
+// ---------------------------------------------------------------------------
+__device__ int beam_setup(const int32_t g[3], const double pos_d[3], const double dir_d[3],
+                          BeamSetup& s) {
+    float p[3], d[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        p[i] = (float)pos_d[i];
+        d[i] = (float)dir_d[i];
+    }
+    s.niter = 0;
+    float nrm = sdot_norm3(d[0], d[1], d[2]);
+    if (nrm < kEpsF) return -1;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) d[i] = d[i] / nrm;
+    float tmin[3], tmax[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (fabsf(d[i]) > kEpsF) {
+            float t1 = (-p[i]) / d[i];
+            float t2 = ((float)(g[i] - 1) - p[i]) / d[i];
+            tmin[i] = (t2 < t1) ? t2 : t1;
+            tmax[i] = (t2 > t1) ? t2 : t1;
+        } else {
+            if (p[i] < 0.0f || p[i] > (float)(g[i] - 1)) return 0;
+            tmin[i] = -INFINITY;
+            tmax[i] = INFINITY;
+        }
+    }
+    float te = tmin[0], tx = tmax[0];
+#pragma unroll
+    for (int i = 1; i < 3; ++i) {
+        if (tmin[i] > te) te = tmin[i];
+        if (tmax[i] < tx) tx = tmax[i];
+    }
+    if (te > tx) return 0;
+    float a0 = fabsf(d[0]), a1 = fabsf(d[1]), a2 = fabsf(d[2]);
+    int dom = 0;
+    float am = a0;
+    if (a1 > am) { dom = 1; am = a1; }
+    if (a2 > am) { dom = 2; am = a2; }
+    int o0 = dom == 0 ? 1 : 0;
+    int o1 = dom == 2 ? 1 : 2;
+    int step = d[dom] > 0.0f ? 1 : -1;
+    float pd = p[dom], dd = d[dom];
+    float e_pt = pd + te * dd;
+    float x_pt = pd + tx * dd;
+    int start = (int)floorf(e_pt);
+    int end = (int)floorf(x_pt);
+    int niter = (end - start) * step + 1;
+    if (niter < 0) niter = 0;
+    if (niter > kMaxGridDim + 2) niter = kMaxGridDim + 2;  // unreachable guard
+    float po0 = o0 == 0 ? p[0] : p[1];
+    float po1 = o1 == 1 ? p[1] : p[2];
+    float do0 = o0 == 0 ? d[0] : d[1];
+    float do1 = o1 == 1 ? d[1] : d[2];
+    s.intery0 = po0 + te * do0;
+    s.interz0 = po1 + te * do1;
+    float den = dd + kEpsF;
+    float gy = do0 / den, gz = do1 / den;
+    s.sgy = gy * (float)step;
+    s.sgz = gz * (float)step;
+    s.start = start;
+    s.stepdir = step;
+    s.dom = dom;
+    s.o0 = o0;
+    s.o1 = o1;
+    s.niter = niter;
+    return 0;
+}
+
+// Splats of march iteration k given its intery/interz (draw_line.py:69-100).
+// Writes up to 4 in-bounds (flat idx, weight) in reference order; returns count.
+__device__ __forceinline__ int march_splats(const int32_t g[3], const BeamSetup& s, int k, float y,
+                                            float z, int32_t idx[4], float w[4]) {
+    int x = s.start + k * s.stepdir;
+    int yf = (int)floorf(y), zf = (int)floorf(z);
+    float yfr = y - (float)yf;
+    float zfr = z - (float)zf;
+    // idx[dom] = x, idx[o0] = y_floor, idx[o1] = z_floor (draw_line.py:73-82)
+    const int b0 = s.dom == 0 ? x : yf;
+    const int b1 = s.dom == 1 ? x : (s.dom == 0 ? yf : zf);
+    const int b2 = s.dom == 2 ? x : zf;
+    int n = 0;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+#pragma unroll
+        for (int dz = 0; dz < 2; ++dz) {
+            float wy = dy == 0 ? (1.0f - yfr) : yfr;
+            float ww = wy * (dz == 0 ? (1.0f - zfr) : zfr);
+            // draw_line.py:88-90: +dy/+dz always on axes 1/2
+            int ix = b0, iy = b1 + dy, iz = b2 + dz;
+            if (ix >= 0 && ix < g[0] && iy >= 0 && iy < g[1] && iz >= 0 && iz < g[2]) {
+                idx[n] = (ix * g[1] + iy) * g[2] + iz;
+                w[n] = ww;
+                ++n;
+            }
+        }
+    }
+    return n;
+}
+
+// ---------------------------------------------------------------------------
+// LDS hash of the beam (flat idx -> summed weight).  A voxel receives at most
+// two splats; IEEE add is commutative, so ds_add_f32 in any order reproduces
+// the reference's `output[ix,iy,iz] += weight` exactly.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t hslot(int32_t key, uint32_t mask) {
+    return ((uint32_t)key * 2654435761u >> 7) & mask;
+}
+
+__device__ __forceinline__ void hash_insert(int32_t* keys, float* vals, uint32_t mask, int32_t key,
+                                            float w) {
+    uint32_t h = hslot(key, mask);
+    while (true) {
+        int32_t old = atomicCAS(&keys[h], -1, key);
+        if (old == -1 || old == key) {
+            atomicAdd(&vals[h], w);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ bool hash_find(const int32_t* keys, const float* vals, uint32_t mask,
+                                          int32_t key, float& w) {
+    uint32_t h = hslot(key, mask);
+    while (true) {
+        int32_t k = keys[h];
+        if (k == key) {
+            w = vals[h];
+            return true;
+        }
+        if (k == -1) return false;
+        h = (h + 1) & mask;
+    }
+}
+
+struct PoseParams {
+    Geom G;
+    Consts C;
+    EnvState st;
+    Library lib;
+    const float* actions;         // [N][6] (STEP)
+    const uint8_t* reset_mask;    // RESET call: NULL = all
+    const int32_t* reset_ids;     // RESET call: NULL = sample
+    int32_t N;
+    int32_t is_reset_call;
+    uint64_t seed;
+    int64_t env_id_base;
+};
+
+// ---------------------------------------------------------------------------
+// k_pose: one lane per env.  Decides STEP / RESET (NEXT_STEP autoreset),
+// samples the tumour on reset, updates the f64 pose and the f32 beam setup.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pose(PoseParams P) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P.N) return;
+    EnvState& st = P.st;
+    BeamSetup s{};
+    int32_t flags = st.flags[e];
+    int mode;
+    if (P.is_reset_call) {
+        bool sel = P.reset_mask == nullptr || P.reset_mask[e] != 0;
+        mode = sel ? MODE_RESET : MODE_NOOP;
+        if (sel && P.reset_ids) st.next_tumour[e] = P.reset_ids[e];
+    } else {
+        mode = (flags & FLAG_NEEDS_RESET) ? MODE_RESET : MODE_STEP;
+    }
+    s.mode = mode;
+    double* pose = st.pose + (size_t)e * 6;
+    if (mode == MODE_RESET) {
+        int32_t tid = st.next_tumour[e];
+        if (tid < 0 || tid >= P.lib.K) {
+            uint32_t ep = st.episode[e]++;
+            uint64_t gid = (uint64_t)(P.env_id_base + e);
+            uint4 r = philox4x32(make_uint4(ep, (uint32_t)gid, (uint32_t)(gid >> 32), 0x52544e56u),
+                                 make_uint2((uint32_t)P.seed, (uint32_t)(P.seed >> 32)));
+            tid = (int32_t)(((uint64_t)r.x * (uint64_t)P.lib.K) >> 32);
+        }
+        st.next_tumour[e] = -1;
+        st.tumour[e] = tid;
+        s.tumour = tid;
+        pose[0] = P.G.S[0] / 2.0;
+        pose[1] = P.G.S[1] / 2.0;
+        pose[2] = P.G.S[2] / 2.0;
+        pose[3] = 0.0;
+        pose[4] = 1.0;
+        pose[5] = 0.0;
+        st.t[e] = 0;
+        st.flags[e] = flags & ~FLAG_NEEDS_RESET;
+        st.ep_return[e] = 0.0;
+        st.ep_len[e] = 0;
+    } else if (mode == MODE_STEP) {
+        s.tumour = st.tumour[e];
+        float a[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) a[i] = P.actions[(size_t)e * 6 + i];
+        double pos[3] = {pose[0], pose[1], pose[2]};
+        double dir[3] = {pose[3], pose[4], pose[5]};
+        PoseOut o;
+        pose_update(P.G, P.C, pos, dir, a, o);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            pose[i] = o.pos[i];
+            pose[3 + i] = o.dir[i];
+            s.os_t[i] = (float)o.os_t[i];
+        }
+        s.os_r = (float)o.os_r;
+        st.t[e] = st.t[e] + 1;
+        beam_setup(P.G.g, o.pos, o.dir, s);  // a direction is never ~0 after renormalisation
+    } else {
+        s.tumour = st.tumour[e];
+    }
+    st.setup[e] = s;
+}
+
+struct StepParams {
+    Geom G;
+    Consts C;
+    EnvState st;
+    Library lib;
+    float* obs;          // [N][9]
+    float* reward;       // [N]
+    uint8_t* terminated; // [N]
+    float* info;         // [N][RT_INFO_W] or null
+    uint32_t hash_mask;  // hash slots - 1
+    int32_t seg_words;   // u32 words of the segment bitmap
+    int32_t max_tvox;    // tumour LDS capacity
+};
+
+__device__ __forceinline__ void write_obs9(const StepParams& P, int e, const double* pose,
+                                           const TumourMeta& m) {
+    float* o = P.obs + (size_t)e * 9;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        o[i] = (float)(pose[i] / P.G.S[i] * 2.0 - 1.0);
+        o[3 + i] = (float)pose[3 + i];
+        o[6 + i] = m.obs_c[i];
+    }
+}
+
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+#define APPLY_BEAM(comp, vox)                                                       \
+    {                                                                               \
+        float bw;                                                                   \
+        if (hash_find(hkeys, hvals, P.hash_mask, (vox), bw)) {                      \
+            comp = clip01(comp + bw * P.C.beam_dose);                               \
+            hit = true;                                                             \
+        }                                                                           \
+    }
+
+#define REDUCE_VOXEL(comp, bit)                                                     \
+    if ((lb >> (bit)) & 1u) {                                                       \
+        part += comp;                                                               \
+        cnt += comp > P.C.lung_thr ? 1 : 0;                                         \
+    }
+
+// ---------------------------------------------------------------------------
+// k_step: one 256-thread block per env.
+//  phase 1  march: iteration k on thread k, splats -> LDS hash + segment bits
+//  phase 2  tumour voxels: old dose gather, beam applied, lung/threshold
+//           correction, distance argmin (f64)
+//  phase 3  exact np.sum of dose*tumour via the tumour's level plan
+//  phase 4  dense pass over the env's dose row: float4 stream, beam applied
+//           in flagged segments (written back only there), lung-masked
+//           threshold count and dose sum
+//  phase 5  rewards, termination, obs, info, episode statistics
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kStepThreads) void k_step(StepParams P) {
+    const int e = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t hslots = P.hash_mask + 1;
+    int32_t* hkeys = reinterpret_cast<int32_t*>(smem);
+    float* hvals = reinterpret_cast<float*>(hkeys + hslots);
+    uint32_t* segbits = reinterpret_cast<uint32_t*>(hvals + hslots);
+    float* tvals = reinterpret_cast<float*>(segbits + P.seg_words);
+    __shared__ unsigned long long s_minbits;
+    __shared__ int s_minidx, s_cnt_tum, s_red_i[kStepThreads / 64];
+    __shared__ double s_red_d[kStepThreads / 64];
+
+    const BeamSetup s = P.st.setup[e];
+    const TumourMeta m = P.lib.meta[s.tumour];
+    double* pose = P.st.pose + (size_t)e * 6;
+    float* dose = P.st.dose + (size_t)e * P.G.Vpad;
+
+    if (s.mode != MODE_STEP) {
+        if (s.mode == MODE_RESET) {
+            float4* d4 = reinterpret_cast<float4*>(dose);
+            const int nvec = P.G.Vpad >> 2;
+            for (int q = tid; q < nvec; q += kStepThreads) d4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (tid == 0) {
+            write_obs9(P, e, pose, m);
+            if (P.reward) P.reward[e] = 0.0f;
+            if (P.terminated) P.terminated[e] = 0;
+            if (P.info) {
+                float* inf = P.info + (size_t)e * RT_INFO_W;
+                for (int i = 0; i < RT_INFO_W; ++i) inf[i] = 0.0f;
+            }
+        }
+        return;
+    }
+
+    // ---- init LDS ----
+    for (uint32_t i = tid; i < hslots; i += kStepThreads) {
+        hkeys[i] = -1;
+        hvals[i] = 0.0f;
+    }
+    for (int i = tid; i < P.seg_words; i += kStepThreads) segbits[i] = 0u;
+    if (tid == 0) {
+        s_minbits = ~0ull;
+        s_minidx = 0x7fffffff;
+        s_cnt_tum = 0;
+    }
+    __syncthreads();
+
+    // ---- phase 1: beam march (draw_line.py:68-100) ----
+    for (int k = tid; k < s.niter; k += kStepThreads) {
+        float y = s.intery0, z = s.interz0;
+        for (int j = 0; j < k; ++j) {  // sequential f32 accumulation, as the reference
+            y = y + s.sgy;
+            z = z + s.sgz;
+        }
+        int32_t idx[4];
+        float w[4];
+        int n = march_splats(P.G.g, s, k, y, z, idx, w);
+        for (int i = 0; i < n; ++i) {
+            hash_insert(hkeys, hvals, P.hash_mask, idx[i], w[i]);
+            int seg = idx[i] / kSegVoxels;
+            atomicOr(&segbits[seg >> 5], 1u << (seg & 31));
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 2: tumour voxels ----
+    const int nt = m.n;
+    const int32_t* tv = P.lib.vox + m.vox_base;
+    const double px = pose[0], py = pose[1], pz = pose[2];
+    const int HW = P.G.g[1] * P.G.g[2];
+    for (int i = tid; i < nt; i += kStepThreads) {
+        int v = tv[i];
+        float x = dose[v];
+        int seg = v / kSegVoxels;
+        if ((segbits[seg >> 5] >> (seg & 31)) & 1u) {
+            float bw;
+            if (hash_find(hkeys, hvals, P.hash_mask, v, bw)) x = clip01(x + bw * P.C.beam_dose);
+        }
+        tvals[i] = x;
+        bool lung = (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u;
+        if (lung && x > P.C.lung_thr) atomicAdd(&s_cnt_tum, 1);
+        int ix = v / HW, iy = (v / P.G.g[2]) % P.G.g[1], iz = v % P.G.g[2];
+        double d0 = (double)ix - px, d1 = (double)iy - py, d2 = (double)iz - pz;
+        double nn = sqrt((d0 * d0 + d1 * d1) + d2 * d2);  // np.linalg.norm(axis=1) order
+        atomicMin(&s_minbits, (unsigned long long)__double_as_longlong(nn));
+    }
+    __syncthreads();
+    for (int i = tid; i < nt; i += kStepThreads) {  // first index among the minima (np.argmin)
+        int v = tv[i];
+        int ix = v / HW, iy = (v / P.G.g[2]) % P.G.g[1], iz = v % P.G.g[2];
+        double d0 = (double)ix - px, d1 = (double)iy - py, d2 = (double)iz - pz;
+        double nn = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+        if ((unsigned long long)__double_as_longlong(nn) == s_minbits) atomicMin(&s_minidx, i);
+    }
+    // ---- phase 3: exact np.sum(dose * tumours) (8192-chunked pairwise order) ----
+    {
+        const uint32_t* ops = P.lib.ops + m.op_base;
+        const int32_t* lend = P.lib.lvl_end + m.lvl_base;
+        int lo = 0;
+        for (int l = 0; l < m.nlev; ++l) {
+            __syncthreads();
+            int hi = lend[l];
+            for (int o = lo + tid; o < hi; o += kStepThreads) {
+                uint32_t ab = ops[o];
+                tvals[nt + o] = tvals[ab & 0xffffu] + tvals[ab >> 16];
+            }
+            lo = hi;
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 4: dense pass over the dose row ----
+    int cnt = 0;
+    double lsum = 0.0;
+    {
+        float4* d4 = reinterpret_cast<float4*>(dose);
+        const int nvec = P.G.Vpad >> 2;  // multiple of 256
+        const uint32_t* lbits = P.lib.lung_bits;
+        for (int base = 0; base < nvec; base += kStepThreads * kUnroll) {
+            float4 v[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                int q = base + u * kStepThreads + tid;
+                v[u] = q < nvec ? d4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                int q = base + u * kStepThreads + tid;
+                if (base + u * kStepThreads >= nvec) break;  // block-uniform tail
+                uint32_t lb = (lbits[q >> 3] >> ((q & 7) << 2)) & 0xFu;
+                int seg = q >> 6;  // wave-uniform: a wave covers one 256-voxel segment
+                if ((segbits[seg >> 5] >> (seg & 31)) & 1u) {
+                    bool hit = false;
+                    const int v0 = q << 2;
+                    APPLY_BEAM(v[u].x, v0)
+                    APPLY_BEAM(v[u].y, v0 + 1)
+                    APPLY_BEAM(v[u].z, v0 + 2)
+                    APPLY_BEAM(v[u].w, v0 + 3)
+                    if (hit) d4[q] = v[u];
+                }
+                float part = 0.0f;
+                REDUCE_VOXEL(v[u].x, 0)
+                REDUCE_VOXEL(v[u].y, 1)
+                REDUCE_VOXEL(v[u].z, 2)
+                REDUCE_VOXEL(v[u].w, 3)
+                lsum += (double)part;
+            }
+        }
+    }
+    cnt = wave_sum_i(cnt);
+    lsum = wave_sum_d(lsum);
+    if (lane == 0) {
+        s_red_i[wid] = cnt;
+        s_red_d[wid] = lsum;
+    }
+    __syncthreads();
+
+    // ---- phase 5: rewards (environment.py:164-191), obs, info ----
+    if (tid == 0) {
+        long long c = 0;
+        double dl = 0.0;
+        for (int w = 0; w < kStepThreads / 64; ++w) {
+            c += s_red_i[w];
+            dl += s_red_d[w];
+        }
+        c -= s_cnt_tum;  // lungs * (1 - tumours): tumour voxels are not lung voxels
+        float S = m.result >= 0 ? tvals[m.result] : 0.0f;
+        float ratio = S / m.T;
+        float r_tum = ratio * P.C.tum_reward;
+        double r_lung = (double)c / m.lung_total * P.C.lung_reward;
+        int bi = s_minidx;
+        int v = tv[bi];
+        int ix = v / HW, iy = (v / P.G.g[2]) % P.G.g[1], iz = v % P.G.g[2];
+        double dn = ddot_norm3((double)ix - px, (double)iy - py, (double)iz - pz);
+        double r_dist = dn / P.G.normS * P.C.dist_reward;
+        double total = ((double)r_tum + r_lung) + r_dist;
+        int t = P.st.t[e];
+        bool done = (ratio >= P.C.tum_thr) || (t >= P.C.max_t);
+        write_obs9(P, e, pose, m);
+        P.reward[e] = (float)total;
+        P.terminated[e] = done ? 1 : 0;
+        double ret = P.st.ep_return[e] + total;
+        int len = P.st.ep_len[e] + 1;
+        P.st.ep_return[e] = ret;
+        P.st.ep_len[e] = len;
+        if (done) P.st.flags[e] |= FLAG_NEEDS_RESET;
+        if (P.info) {
+            float* inf = P.info + (size_t)e * RT_INFO_W;
+            inf[RT_INFO_TOTAL] = (float)total;
+            inf[RT_INFO_TUMOUR] = r_tum;
+            inf[RT_INFO_LUNG] = (float)r_lung;
+            inf[RT_INFO_DISTANCE] = (float)r_dist;
+            inf[RT_INFO_DOSE_TUMOUR] = S;
+            inf[RT_INFO_DOSE_LUNG] = (float)dl;
+            for (int i = 0; i < 3; ++i) {
+                inf[RT_INFO_OVERSHOOT_T + i] = s.os_t[i];
+                inf[RT_INFO_POS + i] = (float)pose[i];
+                inf[RT_INFO_DIR + i] = (float)pose[3 + i];
+            }
+            inf[RT_INFO_OVERSHOOT_R] = s.os_r;
+            inf[RT_INFO_STEPPED] = 1.0f;
+            inf[RT_INFO_EP_DONE] = done ? 1.0f : 0.0f;
+            inf[RT_INFO_EP_RETURN] = (float)ret;
+            inf[RT_INFO_EP_LENGTH] = (float)len;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Parity hooks
+// ---------------------------------------------------------------------------
+__global__ void k_debug_beam(Geom G, int m, const double* pos, const double* dir, int cap,
+                             int32_t* idx_out, float* w_out, int32_t* count) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= m) return;
+    BeamSetup s{};
+    double p[3] = {pos[c * 3], pos[c * 3 + 1], pos[c * 3 + 2]};
+    double d[3] = {dir[c * 3], dir[c * 3 + 1], dir[c * 3 + 2]};
+    if (beam_setup(G.g, p, d, s) < 0) {
+        count[c] = -1;
+        return;
+    }
+    int n = 0;
+    float y = s.intery0, z = s.interz0;
+    for (int k = 0; k < s.niter; ++k) {
+        int32_t ii[4];
+        float ww[4];
+        int q = march_splats(G.g, s, k, y, z, ii, ww);
+        for (int i = 0; i < q; ++i, ++n) {
+            if (n < cap) {
+                idx_out[(size_t)c * cap + n] = ii[i];
+                w_out[(size_t)c * cap + n] = ww[i];
+            }
+        }
+        y = y + s.sgy;
+        z = z + s.sgz;
+    }
+    count[c] = n;
+}
+
+__global__ void k_debug_pose(Geom G, Consts C, int m, const double* pos, const double* dir,
+                             const float* act, double* out) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= m) return;
+    double p[3] = {pos[c * 3], pos[c * 3 + 1], pos[c * 3 + 2]};
+    double d[3] = {dir[c * 3], dir[c * 3 + 1], dir[c * 3 + 2]};
+    float a[6];
+    for (int i = 0; i < 6; ++i) a[i] = act[c * 6 + i];
+    PoseOut o;
+    pose_update(G, C, p, d, a, o);
+    double* r = out + (size_t)c * 10;
+    for (int i = 0; i < 3; ++i) {
+        r[i] = o.pos[i];
+        r[3 + i] = o.dir[i];
+        r[6 + i] = o.os_t[i];
+    }
+    r[9] = o.os_r;
+}
+
+__global__ void k_set_next(EnvState st, int N, const int32_t* ids) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < N) st.next_tumour[e] = ids[e];
+}
+
+__global__ void k_get_state(EnvState st, int N, double* pose, int32_t* t, int32_t* tum) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    if (pose)
+        for (int i = 0; i < 6; ++i) pose[(size_t)e * 6 + i] = st.pose[(size_t)e * 6 + i];
+    if (t) t[e] = st.t[e];
+    if (tum) tum[e] = st.tumour[e];
+}
+
+__global__ void k_set_pose(EnvState st, int N, const double* pose) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    for (int i = 0; i < 6; ++i) st.pose[(size_t)e * 6 + i] = pose[(size_t)e * 6 + i];
+}
+
+// train.py:163-181, one lane per env; same operation order as the torch loop
+// (gamma and gamma*lambda are applied as f32 scalars, as torch does).
+__global__ void k_gae(int T, int N, const float* __restrict__ rew, const float* __restrict__ val,
+                      const float* __restrict__ dones, const float* __restrict__ next_value,
+                      const float* __restrict__ next_done, float gamma, float gl,
+                      float* __restrict__ adv, float* __restrict__ ret) {
+    int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    float last = 0.0f;
+    float nv = next_value[n];
+    float nnt = 1.0f - next_done[n];
+    for (int t = T - 1; t >= 0; --t) {
+        size_t i = (size_t)t * N + n;
+        float v = val[i];
+        float delta = (rew[i] + (gamma * nv) * nnt) - v;
+        last = delta + ((gl * nnt) * last);
+        adv[i] = last;
+        ret[i] = last + v;
+        nv = v;
+        nnt = 1.0f - dones[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host: exact-sum plan for one tumour.
+// np.sum over the dense f32 volume adds 8192-element buffers, each summed by
+// numpy's pairwise routine (8-way unrolled leaves of <=128 elements), into an
+// accumulator.  Zeros are exact identities, so restricted to the tumour voxels
+// the sum is a fixed binary tree over those voxels; the plan lists its adds in
+// dependency levels (slot = leaf index for i < n, n + op index otherwise).
+// ---------------------------------------------------------------------------
+struct PlanBuilder {
+    const int32_t* idx;
+    int n;
+    int64_t V;
+    int p = 0;
+    std::vector<int> opa, opb, lvl;
+
+    int level(int s) const { return s < n ? 0 : lvl[s - n]; }
+    int add(int x, int y) {
+        if (x < 0) return y;
+        if (y < 0) return x;
+        int s = n + (int)opa.size();
+        opa.push_back(x);
+        opb.push_back(y);
+        lvl.push_back(std::max(level(x), level(y)) + 1);
+        return s;
+    }
+    int pairwise(int64_t start, int64_t len) {
+        const int64_t stop = start + len;
+        if (p >= n || idx[p] >= stop) return -1;
+        if (len < 8) {
+            int r = -1;
+            while (p < n && idx[p] < stop) r = add(r, p++);
+            return r;
+        }
+        if (len <= 128) {
+            const int64_t cut = stop - len % 8;
+            int r[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+            while (p < n && idx[p] < cut) {
+                int j = (int)((idx[p] - start) & 7);
+                r[j] = add(r[j], p++);
+            }
+            int res = add(add(add(r[0], r[1]), add(r[2], r[3])), add(add(r[4], r[5]), add(r[6], r[7])));
+            while (p < n && idx[p] < stop) res = add(res, p++);
+            return res;
+        }
+        int64_t n2 = len / 2;
+        n2 -= n2 % 8;
+        int a = pairwise(start, n2);
+        int b = pairwise(start + n2, len - n2);
+        return add(a, b);
+    }
+    int build() {
+        int acc = -1;
+        while (p < n) {
+            int64_t c = idx[p] / 8192;
+            int64_t len = std::min<int64_t>(8192, V - c * 8192);
+            acc = add(acc, pairwise(c * 8192, len));
+        }
+        return acc;
+    }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+struct rt_env {
+    int device = 0;
+    int N = 0;
+    Geom G{};
+    Consts C{};
+    uint64_t seed = 0;
+    int64_t env_id_base = 0;
+    int visionless = 1;
+    EnvState st{};
+    Library lib{};
+    uint32_t hash_mask = 0;
+    int seg_words = 0;
+    int max_tvox = 0;
+    size_t smem = 0;
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+template <typename T>
+int dev_alloc(rt_env* env, T** p, size_t count) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+    if (e != hipSuccess) return fail(RT_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    env->allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return RT_OK;
+}
+
+uint32_t next_pow2(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+void free_env(rt_env* env) {
+    if (!env) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(env->device);
+    for (void* p : env->allocs) (void)hipFree(p);
+    (void)hipSetDevice(cur);
+    delete env;
+}
+
+int fill_geom(const int32_t grid[3], Geom& G) {
+    for (int i = 0; i < 3; ++i)
+        if (grid[i] < 1 || grid[i] > kMaxGridDim) return fail(RT_ELIMIT, "grid dimension out of range [1,1024]");
+    int64_t V = (int64_t)grid[0] * grid[1] * grid[2];
+    if (V > (int64_t)1 << 30) return fail(RT_ELIMIT, "grid too large");
+    for (int i = 0; i < 3; ++i) {
+        G.g[i] = grid[i];
+        G.S[i] = (double)grid[i];
+    }
+    G.V = (int32_t)V;
+    G.Vpad = (int32_t)((V + 1023) / 1024 * 1024);
+    G.normS = std::sqrt(std::fma(G.S[2], G.S[2], std::fma(G.S[1], G.S[1], G.S[0] * G.S[0])));
+    return RT_OK;
+}
+
+Consts make_consts(const rt_env_config& c) {
+    Consts C{};
+    C.max_t = c.max_time_steps;
+    C.beam_dose = c.beam_dose;
+    C.lung_thr = c.lung_dose_threshold;
+    C.tum_thr = c.tumour_dose_threshold;
+    C.min_angle = c.min_angle_z;
+    C.cos_min_angle = std::cos(c.min_angle_z);
+    C.move_speed = c.movement_speed;
+    C.rot_speed = c.rotation_speed;
+    C.tum_reward = c.tumour_dose_reward;
+    C.lung_reward = c.lung_dose_reward;
+    C.dist_reward = c.distance_reward;
+    C.pi_f = (float)M_PI;
+    return C;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RTENV_ABI_VERSION; }
+
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+int rt_env_config_default(rt_env_config* cfg) {
+    if (!cfg) return fail(RT_EINVAL, "cfg is NULL");
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->grid[0] = 67;
+    cfg->grid[1] = 43;
+    cfg->grid[2] = 70;
+    cfg->num_envs = 1;
+    cfg->visionless = 1;
+    cfg->max_time_steps = 100;
+    cfg->beam_dose = 0.1f;
+    cfg->lung_dose_threshold = 0.2f;
+    cfg->tumour_dose_threshold = 0.9f;
+    cfg->min_angle_z = M_PI / 4.0;
+    cfg->movement_speed = 0.2;
+    cfg->rotation_speed = 0.5f;
+    cfg->lung_dose_reward = -1.0;
+    cfg->tumour_dose_reward = 10.0f;
+    cfg->distance_reward = -1.0;
+    return RT_OK;
+}
+
+int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
+    if (!cfg || !out) return fail(RT_EINVAL, "NULL argument");
+    *out = nullptr;
+    if (cfg->num_envs < 1) return fail(RT_EINVAL, "num_envs must be >= 1");
+    if (!cfg->visionless) return fail(RT_ELIMIT, "vision observations are not built into this library yet");
+    if (!cfg->lungs_h || !cfg->tumour_voxels_h || !cfg->tumour_offsets_h || cfg->n_tumours < 1)
+        return fail(RT_EINVAL, "lungs / tumour library missing");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_EDEVICE, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RT_EDEVICE, "bad device id");
+    RT_HIP(hipSetDevice(device));
+
+    rt_env* env = new rt_env();
+    env->device = device;
+    env->N = cfg->num_envs;
+    env->seed = cfg->seed;
+    env->env_id_base = cfg->env_id_base;
+    env->visionless = cfg->visionless;
+    int rc = fill_geom(cfg->grid, env->G);
+    if (rc) { free_env(env); return rc; }
+    env->C = make_consts(*cfg);
+    const Geom& G = env->G;
+    const int K = cfg->n_tumours;
+
+    // ---- library (host build) ----
+    std::vector<uint32_t> lbits(G.Vpad / 32, 0u);
+    int64_t lung_count = 0;
+    for (int64_t v = 0; v < G.V; ++v) {
+        if (cfg->lungs_h[v]) {
+            lbits[v >> 5] |= 1u << (v & 31);
+            ++lung_count;
+        }
+    }
+    std::vector<TumourMeta> meta(K);
+    std::vector<int32_t> vox;
+    std::vector<uint32_t> ops;
+    std::vector<int32_t> lvl_end;
+    int max_n = 0;
+    for (int k = 0; k < K; ++k) {
+        int64_t a = cfg->tumour_offsets_h[k], b = cfg->tumour_offsets_h[k + 1];
+        int n = (int)(b - a);
+        if (n < 1) { free_env(env); return fail(RT_EINVAL, "empty tumour in library"); }
+        if (n > kMaxTumourVoxels) { free_env(env); return fail(RT_ELIMIT, "tumour larger than 1024 voxels"); }
+        const int32_t* iv = cfg->tumour_voxels_h + a;
+        int64_t in_lung = 0;
+        double csum[3] = {0, 0, 0};
+        for (int i = 0; i < n; ++i) {
+            if (iv[i] < 0 || iv[i] >= G.V || (i && iv[i] <= iv[i - 1])) {
+                free_env(env);
+                return fail(RT_EINVAL, "tumour voxels must be sorted, unique and inside the grid");
+            }
+            if (cfg->lungs_h[iv[i]]) ++in_lung;
+            int64_t v = iv[i];
+            csum[0] += (double)(v / ((int64_t)G.g[1] * G.g[2]));
+            csum[1] += (double)((v / G.g[2]) % G.g[1]);
+            csum[2] += (double)(v % G.g[2]);
+        }
+        max_n = std::max(max_n, n);
+        TumourMeta& m = meta[k];
+        m.vox_base = (int32_t)vox.size();
+        m.n = n;
+        m.T = (float)n;
+        m.lung_total = (double)(lung_count - in_lung);
+        for (int i = 0; i < 3; ++i) {
+            double c = csum[i] / (double)n;  // np.mean of exact integer sums
+            m.obs_c[i] = (float)(c / G.S[i] * 2.0 - 1.0);
+        }
+        vox.insert(vox.end(), iv, iv + n);
+        PlanBuilder pb{iv, n, (int64_t)G.V};
+        int res = pb.build();
+        // order ops by level; op at sorted position o writes slot n + o
+        int nops = (int)pb.opa.size();
+        std::vector<int> order(nops);
+        for (int i = 0; i < nops; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return pb.lvl[x] < pb.lvl[y]; });
+        std::vector<int> remap(nops);
+        for (int o = 0; o < nops; ++o) remap[order[o]] = o;
+        auto slot = [&](int s) { return s < n ? s : n + remap[s - n]; };
+        m.op_base = (int32_t)ops.size();
+        m.lvl_base = (int32_t)lvl_end.size();
+        int nlev = 0;
+        for (int o = 0; o < nops; ++o) {
+            int src = order[o];
+            ops.push_back((uint32_t)slot(pb.opa[src]) | ((uint32_t)slot(pb.opb[src]) << 16));
+            int L = pb.lvl[src];
+            if (o + 1 == nops || pb.lvl[order[o + 1]] != L) {
+                lvl_end.push_back(o + 1);
+                ++nlev;
+            }
+        }
+        m.nlev = nlev;
+        m.result = res < 0 ? -1 : slot(res);
+    }
+    env->lib.K = K;
+    env->max_tvox = max_n;
+    int maxdim = std::max(G.g[0], std::max(G.g[1], G.g[2]));
+    env->hash_mask = next_pow2((uint32_t)(8 * (maxdim + 2))) - 1;  // <= 25 % load
+    env->seg_words = (G.Vpad / kSegVoxels + 31) / 32;
+    env->smem = (size_t)(env->hash_mask + 1) * 8 + (size_t)env->seg_words * 4 + (size_t)2 * max_n * 4;
+    if (env->smem > 64 * 1024) { free_env(env); return fail(RT_ELIMIT, "LDS budget exceeded"); }
+
+    // ---- device allocations ----
+    const int N = env->N;
+    uint32_t* d_lbits;
+    int32_t *d_vox, *d_lvl;
+    uint32_t* d_ops;
+    TumourMeta* d_meta;
+    EnvState& st = env->st;
+    if ((rc = dev_alloc(env, &d_lbits, lbits.size())) || (rc = dev_alloc(env, &d_vox, vox.size())) ||
+        (rc = dev_alloc(env, &d_ops, ops.size())) || (rc = dev_alloc(env, &d_lvl, lvl_end.size())) ||
+        (rc = dev_alloc(env, &d_meta, meta.size())) ||
+        (rc = dev_alloc(env, &st.dose, (size_t)N * G.Vpad)) || (rc = dev_alloc(env, &st.pose, (size_t)N * 6)) ||
+        (rc = dev_alloc(env, &st.t, N)) || (rc = dev_alloc(env, &st.tumour, N)) ||
+        (rc = dev_alloc(env, &st.flags, N)) || (rc = dev_alloc(env, &st.episode, N)) ||
+        (rc = dev_alloc(env, &st.ep_return, N)) || (rc = dev_alloc(env, &st.ep_len, N)) ||
+        (rc = dev_alloc(env, &st.next_tumour, N)) || (rc = dev_alloc(env, &st.setup, N))) {
+        free_env(env);
+        return rc;
+    }
+    auto h2d = [&](void* d, const void* h, size_t bytes) { return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice); };
+    std::vector<int32_t> ones(N, FLAG_NEEDS_RESET), neg(N, -1);
+    std::vector<double> pose0((size_t)N * 6, 0.0);
+    for (int e = 0; e < N; ++e) {
+        for (int i = 0; i < 3; ++i) pose0[(size_t)e * 6 + i] = G.S[i] / 2.0;
+        pose0[(size_t)e * 6 + 4] = 1.0;
+    }
+    if (h2d(d_lbits, lbits.data(), lbits.size() * 4) || h2d(d_vox, vox.data(), vox.size() * 4) ||
+        (ops.size() && h2d(d_ops, ops.data(), ops.size() * 4)) ||
+        (lvl_end.size() && h2d(d_lvl, lvl_end.data(), lvl_end.size() * 4)) ||
+        h2d(d_meta, meta.data(), meta.size() * sizeof(TumourMeta)) ||
+        h2d(st.flags, ones.data(), N * 4) || h2d(st.next_tumour, neg.data(), N * 4) ||
+        h2d(st.pose, pose0.data(), pose0.size() * 8) ||
+        hipMemset(st.dose, 0, (size_t)N * G.Vpad * 4) || hipMemset(st.t, 0, N * 4) ||
+        hipMemset(st.tumour, 0, N * 4) || hipMemset(st.episode, 0, N * 4) ||
+        hipMemset(st.ep_return, 0, N * 8) || hipMemset(st.ep_len, 0, N * 4) ||
+        hipMemset(st.setup, 0, (size_t)N * sizeof(BeamSetup)) || hipDeviceSynchronize()) {
+        free_env(env);
+        return fail(RT_EDEVICE, "initial upload failed");
+    }
+    env->lib.lung_bits = d_lbits;
+    env->lib.vox = d_vox;
+    env->lib.ops = d_ops;
+    env->lib.lvl_end = d_lvl;
+    env->lib.meta = d_meta;
+    *out = env;
+    return RT_OK;
+}
+
+void rt_env_destroy(rt_env* env) { free_env(env); }
+
+int rt_env_num_envs(const rt_env* env) { return env ? env->N : 0; }
+
+float* rt_env_dose(rt_env* env, int64_t* stride) {
+    if (!env) return nullptr;
+    if (stride) *stride = env->G.Vpad;
+    return env->st.dose;
+}
+
+static int launch_pair(rt_env* env, bool reset_call, const float* actions, const uint8_t* mask,
+                       const int32_t* ids, float* obs, float* reward, uint8_t* term, float* info,
+                       hipStream_t stream) {
+    PoseParams pp{};
+    pp.G = env->G;
+    pp.C = env->C;
+    pp.st = env->st;
+    pp.lib = env->lib;
+    pp.actions = actions;
+    pp.reset_mask = mask;
+    pp.reset_ids = ids;
+    pp.N = env->N;
+    pp.is_reset_call = reset_call ? 1 : 0;
+    pp.seed = env->seed;
+    pp.env_id_base = env->env_id_base;
+    hipLaunchKernelGGL(k_pose, dim3((env->N + 255) / 256), dim3(256), 0, stream, pp);
+    RT_LAUNCH_CHECK("k_pose");
+    StepParams sp{};
+    sp.G = env->G;
+    sp.C = env->C;
+    sp.st = env->st;
+    sp.lib = env->lib;
+    sp.obs = obs;
+    sp.reward = reward;
+    sp.terminated = term;
+    sp.info = info;
+    sp.hash_mask = env->hash_mask;
+    sp.seg_words = env->seg_words;
+    sp.max_tvox = env->max_tvox;
+    hipLaunchKernelGGL(k_step, dim3(env->N), dim3(kStepThreads), env->smem, stream, sp);
+    RT_LAUNCH_CHECK("k_step");
+    return RT_OK;
+}
+
+int rt_env_reset(rt_env* env, const uint8_t* mask_d, const int32_t* tumour_ids_d, float* obs_d,
+                 void* stream) {
+    if (!env || !obs_d) return fail(RT_EINVAL, "NULL argument");
+    return launch_pair(env, true, nullptr, mask_d, tumour_ids_d, obs_d, nullptr, nullptr, nullptr,
+                       as_stream(stream));
+}
+
+int rt_env_step(rt_env* env, const float* actions_d, float* obs_d, float* reward_d,
+                uint8_t* terminated_d, float* info_d, void* stream) {
+    if (!env || !actions_d || !obs_d || !reward_d || !terminated_d) return fail(RT_EINVAL, "NULL argument");
+    return launch_pair(env, false, actions_d, nullptr, nullptr, obs_d, reward_d, terminated_d, info_d,
+                       as_stream(stream));
+}
+
+int rt_env_set_next_tumours(rt_env* env, const int32_t* ids_d, void* stream) {
+    if (!env || !ids_d) return fail(RT_EINVAL, "NULL argument");
+    hipLaunchKernelGGL(k_set_next, dim3((env->N + 255) / 256), dim3(256), 0, as_stream(stream), env->st,
+                       env->N, ids_d);
+    RT_LAUNCH_CHECK("k_set_next");
+    return RT_OK;
+}
+
+int rt_env_get_state(rt_env* env, double* pose_d, int32_t* t_d, int32_t* tumour_d, void* stream) {
+    if (!env) return fail(RT_EINVAL, "NULL argument");
+    hipLaunchKernelGGL(k_get_state, dim3((env->N + 255) / 256), dim3(256), 0, as_stream(stream), env->st,
+                       env->N, pose_d, t_d, tumour_d);
+    RT_LAUNCH_CHECK("k_get_state");
+    return RT_OK;
+}
+
+int rt_env_set_pose(rt_env* env, const double* pose_d, void* stream) {
+    if (!env || !pose_d) return fail(RT_EINVAL, "NULL argument");
+    hipLaunchKernelGGL(k_set_pose, dim3((env->N + 255) / 256), dim3(256), 0, as_stream(stream), env->st,
+                       env->N, pose_d);
+    RT_LAUNCH_CHECK("k_set_pose");
+    return RT_OK;
+}
+
+int rt_debug_beam(const int32_t grid[3], int32_t m, const double* pos_d, const double* dir_d,
+                  int32_t cap, int32_t* idx_d, float* w_d, int32_t* count_d, void* stream) {
+    Geom G{};
+    int rc = fill_geom(grid, G);
+    if (rc) return rc;
+    if (m < 0 || cap < 0 || !pos_d || !dir_d || !count_d) return fail(RT_EINVAL, "bad argument");
+    if (m == 0) return RT_OK;
+    hipLaunchKernelGGL(k_debug_beam, dim3((m + 63) / 64), dim3(64), 0, as_stream(stream), G, m, pos_d, dir_d,
+                       cap, idx_d, w_d, count_d);
+    RT_LAUNCH_CHECK("k_debug_beam");
+    return RT_OK;
+}
+
+int rt_debug_pose(const int32_t grid[3], int32_t m, const double* pos_d, const double* dir_d,
+                  const float* action_d, double* out_d, void* stream) {
+    Geom G{};
+    int rc = fill_geom(grid, G);
+    if (rc) return rc;
+    if (m < 0 || !pos_d || !dir_d || !action_d || !out_d) return fail(RT_EINVAL, "bad argument");
+    if (m == 0) return RT_OK;
+    rt_env_config cfg;
+    rt_env_config_default(&cfg);
+    Consts C = make_consts(cfg);
+    hipLaunchKernelGGL(k_debug_pose, dim3((m + 63) / 64), dim3(64), 0, as_stream(stream), G, C, m, pos_d,
+                       dir_d, action_d, out_d);
+    RT_LAUNCH_CHECK("k_debug_pose");
+    return RT_OK;
+}
+
+int rt_gae(int32_t T, int32_t N, const float* rewards_d, const float* values_d, const float* dones_d,
+           const float* next_value_d, const float* next_done_d, double gamma, double gae_lambda, float* adv_d,
+           float* ret_d, void* stream) {
+    if (T < 1 || N < 1 || !rewards_d || !values_d || !dones_d || !next_value_d || !next_done_d || !adv_d || !ret_d)
+        return fail(RT_EINVAL, "bad argument");
+    // torch applies python-float scalars in f32: gamma, and gamma*lambda (a python product)
+    float gl = (float)(gamma * gae_lambda);
+    hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, as_stream(stream), T, N, rewards_d,
+                       values_d, dones_d, next_value_d, next_done_d, (float)gamma, gl, adv_d, ret_d);
+    RT_LAUNCH_CHECK("k_gae");
+    return RT_OK;
+}
+
+}  // extern "C"

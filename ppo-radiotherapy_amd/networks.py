@@ -1,0 +1,136 @@
+"""Policy / value networks (reference: networks.py).
+
+`PPO` (networks.py:107-147) is the visionless MLP actor-critic; `PPO_3DCNN`
+(networks.py:54-104) puts the C3D-style `FeaturesExtractor3D`
+(networks.py:8-45) in front.  Module names and parameter shapes are those of
+the reference, so `saves/*.model` state dicts load unchanged.
+
+The Gaussian policy head is written out in closed form instead of going
+through `torch.distributions.Normal`: the distribution's argument validation
+reduces its inputs to a host bool on every construction (a device->host sync
+per rollout step); the math is identical (log N(a; mu, sigma) summed over the
+6 action dims, entropy 0.5 + 0.5 log 2pi + log sigma).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+from torch import nn
+
+_HALF_LOG_2PI = 0.5 * math.log(2.0 * math.pi)
+
+
+def layer_init(layer: nn.Module, std: float = float(np.sqrt(2)), bias_const: float = 0.0) -> nn.Module:
+    """Orthogonal weights, constant bias (networks.py:48-51)."""
+    nn.init.orthogonal_(layer.weight, std)
+    nn.init.constant_(layer.bias, bias_const)
+    return layer
+
+
+def _tanh_mlp(d_in: int, width: int, d_out: int, head_std: float) -> nn.Sequential:
+    # indices 0/2/4 hold the Linear layers, as in the reference's Sequential
+    return nn.Sequential(
+        layer_init(nn.Linear(d_in, width)), nn.Tanh(),
+        layer_init(nn.Linear(width, width)), nn.Tanh(),
+        layer_init(nn.Linear(width, d_out), std=head_std),
+    )
+
+
+class GaussianHeadMixin:
+    """get_value / get_action_and_value of the reference agents."""
+
+    actor_logstd: nn.Parameter
+
+    def _features(self, x: torch.Tensor) -> torch.Tensor:
+        return x
+
+    def get_value(self, x: torch.Tensor) -> torch.Tensor:
+        return self.critic(self._features(x))
+
+    def get_action_and_value(self, x: torch.Tensor, action: torch.Tensor | None = None,
+                             generator: torch.Generator | None = None):
+        f = self._features(x)
+        mean = self.actor_mean(f)
+        logstd = self.actor_logstd.expand_as(mean)
+        std = torch.exp(logstd)
+        if action is None:
+            noise = torch.randn(mean.shape, dtype=mean.dtype, device=mean.device, generator=generator)
+            action = mean + std * noise
+        z = (action - mean) / std
+        logprob = (-0.5 * z * z - logstd - _HALF_LOG_2PI).sum(1)
+        entropy = (0.5 + _HALF_LOG_2PI + logstd).sum(1)
+        return action, logprob, entropy, self.critic(f)
+
+
+class PPO(GaussianHeadMixin, nn.Module):
+    """Visionless agent: obs [B, 9] -> MLP 64-64 -> mean [B, 6], value [B, 1]."""
+
+    def __init__(self, observation_shape, action_space, feature_dim: int = 64):
+        super().__init__()
+        self.feature_dim = feature_dim
+        self.observation_shape = tuple(observation_shape)
+        self.action_space = tuple(np.atleast_1d(action_space))
+        n_obs = int(np.prod(self.observation_shape))
+        n_act = int(np.prod(self.action_space))
+        self.critic = _tanh_mlp(n_obs, feature_dim, 1, head_std=1.0)
+        self.actor_mean = _tanh_mlp(n_obs, feature_dim, n_act, head_std=0.01)
+        self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
+
+
+class FeaturesExtractor3D(nn.Module):
+    """C3D-lite encoder (networks.py:8-45): three 3x3x3 convs (groups 1/2/4)
+    with ReLU and 2x2x2 max-pools, flatten, Linear -> features_dim, ReLU.
+    The first pool pads each axis by (S_i - 2) % 2 (networks.py:18-20)."""
+
+    def __init__(self, observation_shape, features_dim: int):
+        super().__init__()
+        self.observation_shape = tuple(observation_shape)
+        c_in, *spatial = self.observation_shape
+        pad1 = tuple((s - 2) % 2 for s in spatial)
+        self.cnn = nn.Sequential(
+            nn.Conv3d(c_in, 16, 3), nn.ReLU(), nn.MaxPool3d(2, 2, padding=pad1),
+            nn.Conv3d(16, 16, 3, groups=2), nn.ReLU(), nn.MaxPool3d(2, 2),
+            nn.Conv3d(16, 16, 3, groups=4), nn.ReLU(), nn.MaxPool3d(2, 2),
+            nn.Flatten(),
+        )
+        self.n_flatten = self._flat_size(spatial)
+        self.mlp = nn.Sequential(nn.Linear(self.n_flatten, features_dim), nn.ReLU())
+
+    @staticmethod
+    def _flat_size(spatial) -> int:
+        # closed form of the reference's dry run (networks.py:35-37)
+        s = [x - 2 for x in spatial]                           # conv1
+        s = [(x + 2 * ((sp - 2) % 2) - 2) // 2 + 1 for x, sp in zip(s, spatial)]  # pool1
+        s = [(x - 2 - 2) // 2 + 1 for x in s]                  # conv2 + pool2
+        s = [(x - 2 - 2) // 2 + 1 for x in s]                  # conv3 + pool3
+        return 16 * int(np.prod(s))
+
+    def forward(self, observations: torch.Tensor) -> torch.Tensor:
+        return self.mlp(self.cnn(observations))
+
+
+class PPO_3DCNN(GaussianHeadMixin, nn.Module):
+    """Vision agent (networks.py:54-104)."""
+
+    def __init__(self, observation_shape, action_space, feature_dim: int = 64):
+        super().__init__()
+        self.feature_dim = feature_dim
+        self.observation_shape = tuple(observation_shape)
+        self.action_space = tuple(np.atleast_1d(action_space))
+        n_act = int(np.prod(self.action_space))
+        self.features_extractor = FeaturesExtractor3D(self.observation_shape, feature_dim)
+        self.critic = _tanh_mlp(feature_dim, feature_dim, 1, head_std=1.0)
+        self.actor_mean = _tanh_mlp(feature_dim, feature_dim, n_act, head_std=0.01)
+        self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
+
+    def _features(self, x):
+        return self.features_extractor(x)
+
+    def summary(self):
+        print("Observation shape: ", self.observation_shape)
+        print("Action space: ", self.action_space)
+        print("Feature dim: ", self.feature_dim)
+        n = sum(p.numel() for p in self.features_extractor.parameters())
+        print(f"Features extractor: {self.features_extractor}\n  flatten={self.features_extractor.n_flatten} params={n}")

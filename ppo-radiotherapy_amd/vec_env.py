@@ -1,0 +1,202 @@
+"""Device-resident vectorised environment (the drop-in for the reference's
+`gym.vector.SyncVectorEnv([make_env(visionless)] * num_envs)`, train.py:32-39,93-95).
+
+All N envs live in HBM; `step()` is two HIP kernels (include/rtenv.h
+rt_env_step) on torch's current stream and never synchronises with the host.
+Semantics follow gymnasium 1.0.0:
+
+* NEXT_STEP autoreset: the step after an env terminates ignores its action,
+  resets it, and returns the reset observation with reward 0 / terminated
+  False; `infos["_reward_components"]` is False for that env (the reference
+  env's reset info is `{}`).
+* RecordEpisodeStatistics: when an episode ends, `infos["episode"]` holds
+  r (sum of step rewards), l (steps), t and the masks `_r/_l/_t`;
+  `infos["_episode"]` marks the finishing envs.
+
+`infos` always carries every key (as device tensors with masks) so that no
+host sync is needed to build it; `has_episode(infos)` is the sync-on-demand
+equivalent of `"episode" in infos` (train.py:160).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from . import _lib, assets, spaces
+from .assets import TumourLibrary
+
+# RadiotherapyEnv class constants (environment.py:16-26)
+ACTION_SIZE = 6
+MAX_TIME_STEPS = 100
+
+
+class RadiotherapyVecEnv:
+    metadata = {"render_modes": ["human"], "render_fps": 30, "autoreset_mode": "NextStep"}
+
+    def __init__(self, num_envs: int, visionless: bool = True, grid=None, device=None, seed: int = 0,
+                 library: TumourLibrary | None = None, env_id_base: int = 0):
+        if not visionless:
+            raise NotImplementedError("vision observations (4-channel volumes) are not built yet")
+        if not torch.cuda.is_available():
+            raise _lib.RtError("RadiotherapyVecEnv needs a HIP device (MI355X); no CPU fallback")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise ValueError("device must be a HIP device")
+        self.num_envs = int(num_envs)
+        self.visionless = bool(visionless)
+        self.library = library if library is not None else assets.library_for(grid or (67, 43, 70))
+        self.grid = tuple(self.library.shape)
+        self.lung_shape = np.array(self.grid)
+        self._seed = int(seed)
+        self.single_observation_space = spaces.Box(0.0, 1.0, (9,) if visionless else (4, *self.grid), np.float32)
+        self.single_action_space = spaces.Box(-1.0, 1.0, (ACTION_SIZE,), np.float32)
+        self.observation_space = spaces.Box(0.0, 1.0, (self.num_envs, *self.single_observation_space.shape), np.float32)
+        self.action_space = spaces.Box(-1.0, 1.0, (self.num_envs, ACTION_SIZE), np.float32)
+
+        L = _lib.load()
+        cfg = _lib.RtEnvConfig()
+        _lib.check(L.rt_env_config_default(cfg), "rt_env_config_default")
+        for i in range(3):
+            cfg.grid[i] = self.grid[i]
+        cfg.num_envs = self.num_envs
+        cfg.visionless = 1 if visionless else 0
+        self._lungs = np.ascontiguousarray(self.library.lungs.ravel(), dtype=np.uint8)
+        self._vox = np.ascontiguousarray(self.library.voxels, dtype=np.int32)
+        self._off = np.ascontiguousarray(self.library.offsets, dtype=np.int64)
+        cfg.lungs_h = self._lungs.ctypes.data
+        cfg.n_tumours = self.library.n_tumours
+        cfg.tumour_voxels_h = self._vox.ctypes.data
+        cfg.tumour_offsets_h = self._off.ctypes.data
+        cfg.seed = self._seed & 0xFFFFFFFFFFFFFFFF
+        cfg.env_id_base = int(env_id_base)
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        handle = ctypes_void_p()
+        with torch.cuda.device(dev_index):
+            _lib.check(L.rt_env_create(cfg, dev_index, handle), "rt_env_create")
+        self._h = handle.value
+        self._L = L
+
+        N = self.num_envs
+        kw = dict(device=self.device)
+        self.obs = torch.zeros((N, *self.single_observation_space.shape), dtype=torch.float32, **kw)
+        self.reward = torch.zeros(N, dtype=torch.float32, **kw)
+        self.terminated = torch.zeros(N, dtype=torch.uint8, **kw)
+        self.truncated = torch.zeros(N, dtype=torch.bool, **kw)
+        self.info = torch.zeros((N, _lib.INFO_W), dtype=torch.float32, **kw)
+        self._episode_start = torch.zeros(N, dtype=torch.float64, **kw)
+        self.closed = False
+
+    # ------------------------------------------------------------------ API
+    def reset(self, seed: int | None = None, options: dict | None = None):
+        """Reset every env (gymnasium VectorEnv.reset).  `options` may hold
+        `tumour_ids` (int[N], -1 = sample) and `mask` (bool[N])."""
+        options = options or {}
+        ids = options.get("tumour_ids")
+        mask = options.get("mask")
+        ids_t = None if ids is None else torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
+        mask_t = None if mask is None else torch.as_tensor(np.asarray(mask), dtype=torch.uint8, device=self.device)
+        _lib.check(self._L.rt_env_reset(self._h, _lib.ptr(mask_t), _lib.ptr(ids_t), _lib.ptr(self.obs),
+                                        _lib.stream_handle()), "rt_env_reset")
+        self._episode_start.fill_(time.perf_counter())
+        return self.obs, {}
+
+    def step(self, actions: torch.Tensor):
+        a = actions
+        if a.dtype != torch.float32 or a.device != self.device or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        if a.shape != (self.num_envs, ACTION_SIZE):
+            raise ValueError(f"actions must be [{self.num_envs}, {ACTION_SIZE}], got {tuple(a.shape)}")
+        _lib.check(self._L.rt_env_step(self._h, _lib.ptr(a), _lib.ptr(self.obs), _lib.ptr(self.reward),
+                                       _lib.ptr(self.terminated), _lib.ptr(self.info), _lib.stream_handle()),
+                   "rt_env_step")
+        return self.obs, self.reward, self.terminated.bool(), self.truncated, self._infos()
+
+    def set_next_tumours(self, ids):
+        t = torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
+        _lib.check(self._L.rt_env_set_next_tumours(self._h, _lib.ptr(t), _lib.stream_handle()),
+                   "rt_env_set_next_tumours")
+
+    def get_state(self):
+        N = self.num_envs
+        pose = torch.empty((N, 6), dtype=torch.float64, device=self.device)
+        t = torch.empty(N, dtype=torch.int32, device=self.device)
+        tum = torch.empty(N, dtype=torch.int32, device=self.device)
+        _lib.check(self._L.rt_env_get_state(self._h, _lib.ptr(pose), _lib.ptr(t), _lib.ptr(tum),
+                                            _lib.stream_handle()), "rt_env_get_state")
+        return pose, t, tum
+
+    def set_pose(self, pose: torch.Tensor):
+        p = pose.to(device=self.device, dtype=torch.float64).contiguous()
+        _lib.check(self._L.rt_env_set_pose(self._h, _lib.ptr(p), _lib.stream_handle()), "rt_env_set_pose")
+
+    def dose(self) -> torch.Tensor:
+        """View [N, D, H, W] of the library-owned dose volumes."""
+        stride = ctypes_int64()
+        p = self._L.rt_env_dose(self._h, stride)
+        V = int(np.prod(self.grid))
+        flat = _tensor_from_ptr(p, (self.num_envs, stride.value), torch.float32, self.device)
+        return flat[:, :V].reshape(self.num_envs, *self.grid)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rt_env_destroy(self._h)
+            self._h = None
+        self.closed = True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ infos
+    def _infos(self):
+        I = self.info
+        stepped = I[:, 16] > 0.5
+        ep_done = I[:, 17] > 0.5
+        rc = {
+            "total": I[:, 0], "tumour": I[:, 1], "lung": I[:, 2], "distance_to_tumour": I[:, 3],
+            "_total": stepped, "_tumour": stepped, "_lung": stepped, "_distance_to_tumour": stepped,
+        }
+        ep = {"r": I[:, 18], "l": I[:, 19], "_r": ep_done, "_l": ep_done, "_t": ep_done}
+        return {
+            "reward_components": rc, "_reward_components": stepped,
+            "beam_position": {"translation": I[:, 10:13], "rotation": I[:, 13:16]}, "_beam_position": stepped,
+            "doses": {"tumour": I[:, 4], "lung": I[:, 5]}, "_doses": stepped,
+            "overshoot": {"translation": I[:, 6:9], "rotation": I[:, 9]}, "_overshoot": stepped,
+            "episode": ep, "_episode": ep_done,
+        }
+
+
+def has_episode(infos) -> bool:
+    """`"episode" in infos` of gymnasium (one device->host sync)."""
+    return bool(infos["_episode"].any().item())
+
+
+# --------------------------------------------------------------------- helpers
+def ctypes_void_p():
+    import ctypes
+
+    return ctypes.c_void_p()
+
+
+def ctypes_int64():
+    import ctypes
+
+    return ctypes.c_int64()
+
+
+def _tensor_from_ptr(ptr: int, shape, dtype, device):
+    """Non-owning torch view of library-owned device memory."""
+
+    class _Holder:
+        def __init__(self, p, nbytes):
+            self.__cuda_array_interface__ = {
+                "shape": (nbytes // 4,), "typestr": "<f4", "data": (p, False), "version": 3, "strides": None,
+            }
+
+    n = int(np.prod(shape))
+    t = torch.as_tensor(_Holder(ptr, n * 4), device=device)
+    return t.view(dtype).reshape(shape)
