@@ -30,7 +30,7 @@ def test_param_counts():
 
 
 @pytest.mark.parametrize("spatial,flat", [((67, 43, 70), 2016), ((64, 64, 64), 3456), ((128, 128, 128), 43904),
-                                          ((20, 21, 23), None)])
+                                          ((30, 33, 41), None)])
 def test_flatten_closed_form(spatial, flat):
     fe = FeaturesExtractor3D((4, *spatial), 64)
     with torch.no_grad():
