@@ -138,6 +138,10 @@ int rt_debug_beam(const int32_t grid[3], int32_t m, const double* pos_d, const d
 int rt_debug_pose(const int32_t grid[3], int32_t m, const double* pos_d, const double* dir_d,
                   const float* action_d, double* out_d, void* stream);
 
+/* Host-side evaluation of the correctly rounded sin/cos the pose kernel uses
+ * for scipy's from_rotvec half angle (no device needed; parity hook). */
+int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h);
+
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */
 int rt_gae(int32_t T, int32_t N, const float* rewards_d, const float* values_d,

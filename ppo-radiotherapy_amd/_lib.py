@@ -28,7 +28,7 @@ RT_ERRORS = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EDEVICE", -4:
 EXPORTS = [
     "rt_env_config_default", "rt_env_create", "rt_env_destroy", "rt_env_reset", "rt_env_step",
     "rt_env_set_next_tumours", "rt_env_dose", "rt_env_get_state", "rt_env_set_pose", "rt_env_num_envs",
-    "rt_debug_beam", "rt_debug_pose", "rt_gae", "rt_last_error", "rt_abi_version",
+    "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_gae", "rt_last_error", "rt_abi_version",
 ]
 
 
@@ -68,6 +68,10 @@ def load(build_if_missing: bool = True):
     global _lib
     if _lib is not None:
         return _lib
+    # torch ships its own libamdhip64.so.7; importing it first makes the
+    # process use that one runtime (loading ours first would pair the system
+    # HIP runtime with torch's HSA runtime and find no device).
+    import torch  # noqa: F401
     if build_if_missing and (not os.path.exists(LIB_PATH) or _build.needs_build()):
         try:
             _build.build()
@@ -91,6 +95,7 @@ def load(build_if_missing: bool = True):
         "rt_env_num_envs": ([vp], ctypes.c_int),
         "rt_debug_beam": ([ctypes.POINTER(i32), i32, vp, vp, i32, vp, vp, vp, vp], ctypes.c_int),
         "rt_debug_pose": ([ctypes.POINTER(i32), i32, vp, vp, vp, vp, vp], ctypes.c_int),
+        "rt_host_sincos": ([i32, vp, vp, vp], ctypes.c_int),
         "rt_gae": ([i32, i32, vp, vp, vp, vp, vp, f64, f64, vp, vp, vp], ctypes.c_int),
         "rt_last_error": ([], ctypes.c_char_p),
         "rt_abi_version": ([], ctypes.c_int),

@@ -36,7 +36,8 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+    deps = (SRC, HDR, os.path.join(PKG, "csrc", "rt_ddmath.h"), __file__)
+    return any(os.path.getmtime(p) > t for p in deps)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "rtenv.h"
+#include "rt_ddmath.h"
 
 namespace {
 
@@ -172,6 +173,11 @@ __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
 // ---------------------------------------------------------------------------
 // transforms.py / environment.py:112-143 (f64 pose update, one lane)
 // ---------------------------------------------------------------------------
+// libm sin/cos of the rotation half-angle (scipy from_rotvec): correctly
+// rounded in double-double on the range the env produces (<= 1.361).
+__device__ __forceinline__ double half_sin(double x) { return x <= 1.6 ? rtdd::sin_cr(x) : sin(x); }
+__device__ __forceinline__ double half_cos(double x) { return x <= 1.6 ? rtdd::cos_cr(x) : cos(x); }
+
 struct PoseOut {
     double pos[3], dir[3], os_t[3], os_r;
 };
@@ -205,9 +211,9 @@ __device__ void pose_update(const Geom& G, const Consts& C, const double pos[3],
         double a2 = ang * ang;
         s = 0.5 - a2 / 48.0 + a2 * a2 / 3840.0;
     } else {
-        s = sin(ang / 2.0) / ang;
+        s = half_sin(ang / 2.0) / ang;
     }
-    double qx = s * r[0], qy = s * r[1], qz = s * r[2], qw = cos(ang / 2.0);
+    double qx = s * r[0], qy = s * r[1], qz = s * r[2], qw = half_cos(ang / 2.0);
     double x2 = qx * qx, y2 = qy * qy, z2 = qz * qz, w2 = qw * qw;
     double xy = qx * qy, zw = qz * qw, xz = qx * qz, yw = qy * qw, yz = qy * qz, xw = qx * qw;
     double m00 = x2 - y2 - z2 + w2, m01 = 2.0 * (xy - zw), m02 = 2.0 * (xz + yw);
@@ -996,6 +1002,15 @@ Consts make_consts(const rt_env_config& c) {
 extern "C" {
 
 int rt_abi_version(void) { return RTENV_ABI_VERSION; }
+
+int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h) {
+    if (n < 0 || (n && (!x_h || !sin_h || !cos_h))) return fail(RT_EINVAL, "bad argument");
+    for (int32_t i = 0; i < n; ++i) {
+        sin_h[i] = x_h[i] <= 1.6 ? rtdd::sin_cr(x_h[i]) : std::sin(x_h[i]);
+        cos_h[i] = x_h[i] <= 1.6 ? rtdd::cos_cr(x_h[i]) : std::cos(x_h[i]);
+    }
+    return RT_OK;
+}
 
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
