@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark: env steps/s (whole node) + PPO updates/s, visionless, 64^3.
+
+Workload (BASELINE.json configs[1]; configs[2] at --gpus 8): 4096 envs per
+GPU on a 64^3 voxel grid (reference lung mask nearest-resampled, 1000
+synthetic spherical tumours), the reference's visionless MLP policy, PPO with
+num_steps=64, num_minibatches=8, update_epochs=10 and the
+remaining keys of configs/default.yaml.
+
+A bench "step" = one vectorised rollout step of every env on every GPU:
+policy forward + Gaussian sample + the HIP env step (k_pose + k_step), i.e.
+train.py:143-158.  `value` = envs x steps / max-over-ranks wall time.
+Also reported:
+  ppo_updates_per_s      optimizer steps/s of the PPO update phase
+                         (80 minibatch steps of 32768 samples per rank, flat
+                         gradient all-reduce per step when n_gpus > 1)
+  train_env_steps_per_s  env steps/s of a full PPO iteration
+                         (64 rollout steps + GAE + 80 updates)
+  roofline               k_step dense pass vs HBM (HIP events on the env
+                         stream over the timed region)
+  cpu_baseline           op-for-op NumPy port of the reference step on one
+                         host core, same 64^3 workload (bounded sample)
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      (N > 1 under torch.distributed.run, one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from types import SimpleNamespace
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "env steps/sec (whole node) + PPO updates/sec, visionless 64³ voxel, 1/2/4/8 GPU"
+HBM_PEAK = 8.0e12  # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--grid", type=int, default=64)
+    ap.add_argument("--num-steps", type=int, default=64)
+    ap.add_argument("--num-minibatches", type=int, default=8)
+    ap.add_argument("--update-epochs", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-update", action="store_true")
+    ap.add_argument("--env-only", action="store_true", help="time rt_env_step alone (profiling)")
+    ap.add_argument("--seed", type=int, default=1)
+    return ap.parse_args()
+
+
+def trainer_cfg(a):
+    # configs/default.yaml keys; C2 rollout/update shape
+    return SimpleNamespace(num_steps=a.num_steps, num_minibatches=a.num_minibatches, update_epochs=a.update_epochs,
+                           learning_rate=3e-4, anneal_lr=False, gamma=0.99, gae_lambda=0.95, norm_adv=True,
+                           clip_coef=0.1, clip_vloss=True, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5)
+
+
+def cpu_baseline(lib, seconds: float):
+    """One-core NumPy port of the reference step on the same 64^3 workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from numpy_env import NumpyEnv
+
+    rng = np.random.default_rng(0)
+    env = NumpyEnv(lib.lungs, lib.tumour_dense(0))
+    env.reset()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        a = rng.uniform(-1, 1, 6).astype(np.float32)
+        _, _, done = env.step(a)
+        n += 1
+        if done:
+            env.reset(lib.tumour_dense(int(rng.integers(lib.n_tumours))))
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return {"value": n / dt, "unit": "env steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} visionless steps of one env at {lib.shape[0]}x{lib.shape[1]}x{lib.shape[2]} "
+                      f"(oracle/numpy_env.py, U(-1,1) actions, autoreset), {dt:.1f} s on 1 host core"}
+
+
+def load_pmc(grid, envs):
+    """Per-launch HBM traffic of k_step from the committed rocprofv3 PMC run."""
+    p = os.path.join(REPO, "profiles", "k_step_pmc.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if tuple(d.get("grid", ())) == tuple(grid) and int(d.get("envs", -1)) == envs:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world == 1 and a.gpus > 1:
+        print(f"bench.py: --gpus {a.gpus} must be launched with torch.distributed.run "
+              f"--nproc-per-node {a.gpus}", file=sys.stderr)
+        sys.exit(2)
+
+    import torch
+    import torch.distributed as dist
+
+    import _rtpkg  # noqa: F401
+    from ppo_radiotherapy_amd import assets
+    from ppo_radiotherapy_amd.networks import PPO
+    from ppo_radiotherapy_amd.ppo import PPOTrainer, broadcast_parameters
+    from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    grid = (a.grid,) * 3
+    lib = assets.synthetic_library(grid, 1000, 0)
+    env = RadiotherapyVecEnv(a.envs, visionless=True, library=lib, device=dev, seed=a.seed + rank,
+                             env_id_base=rank * a.envs)
+    torch.manual_seed(a.seed)
+    agent = PPO((9,), (6,), 64).to(dev)
+    broadcast_parameters(agent)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(a.seed * 1000 + rank)
+    cfg = trainer_cfg(a)
+    tr = PPOTrainer(cfg, env, agent, dev, rank, world, gen)
+    tr.reset()
+    T = tr.T
+
+    # ---------------- warmup
+    for i in range(a.warmup):
+        tr.rollout_step(i % T)
+    if not a.no_update and not a.env_only:
+        tr.compute_gae()
+        tr.update()
+    torch.cuda.synchronize()
+
+    # ---------------- timed rollout (or env-only)
+    K = a.steps
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    actions = torch.rand((a.envs, 6), device=dev, generator=gen) * 2 - 1
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if a.env_only:
+        for i in range(K):
+            evs[i][0].record()
+            env.step(actions, info_out=tr.infos[i % T])
+            evs[i][1].record()
+    else:
+        for i in range(K):
+            tr.rollout_step(i % T, evs[i])
+    torch.cuda.synchronize()
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    env_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    env_ms = max_over_ranks(env_ms)
+    total_envs = a.envs * world
+    steps_per_s = total_envs * K / dt
+
+    # ---------------- PPO update phase + one full iteration
+    upd = {}
+    if not a.no_update and not a.env_only:
+        tr.compute_gae()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        n_upd = tr.update()
+        torch.cuda.synchronize()
+        barrier()
+        du = max_over_ranks(time.perf_counter() - t0)
+        barrier()
+        t0 = time.perf_counter()
+        tr.rollout()
+        tr.compute_gae()
+        tr.update()
+        torch.cuda.synchronize()
+        barrier()
+        di = max_over_ranks(time.perf_counter() - t0)
+        upd = {"ppo_updates_per_s": n_upd / du, "ppo_update_ms": 1000 * du / n_upd,
+               "minibatch_size_per_gpu": tr.minibatch_size,
+               "train_env_steps_per_s": total_envs * T / di, "train_iteration_s": di}
+
+    # ---------------- roofline of the env kernel pair (k_pose + k_step)
+    V = int(np.prod(grid))
+    bytes_step = 4 * V  # the dense pass reads each env's f32 dose row once
+    achieved = a.envs * bytes_step / (env_ms * 1e-3)
+    traffic = load_pmc(grid, a.envs)
+    roof = {"bound": "hbm", "kernel": "k_pose+k_step (rt_env_step)", "achieved": achieved / 1e9,
+            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+            "traffic": traffic, "bytes_per_env_step": bytes_step, "env_step_ms": env_ms,
+            "survey_model_bytes_per_env_step": 8 * V,
+            "survey_model_frac": a.envs * 8 * V / (env_ms * 1e-3) / HBM_PEAK}
+
+    out = {"metric": METRIC, "value": steps_per_s, "unit": "env steps/s", "n_gpus": world, "steps": K,
+           "warmup": a.warmup, "ms_per_step": 1000 * dt / K, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "config": {"workload": f"visionless MLP, {a.envs} envs/GPU, {a.grid}^3 voxel grid "
+                                  f"(BASELINE configs[{1 if world == 1 else 2}])" + (" env-only" if a.env_only else ""),
+                      "envs_per_gpu": a.envs, "global_envs": total_envs, "grid": list(grid),
+                      "num_steps": T, "num_minibatches": a.num_minibatches, "update_epochs": a.update_epochs,
+                      "parallelism": f"dp{world}"},
+           "env_only_kernel_steps_per_s": total_envs / (env_ms * 1e-3)}
+    out.update(upd)
+    out["roofline"] = roof
+    if rank == 0 and world == 1 and not a.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(lib, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -102,16 +102,21 @@ class RadiotherapyVecEnv:
         self._episode_start.fill_(time.perf_counter())
         return self.obs, {}
 
-    def step(self, actions: torch.Tensor):
+    def step(self, actions: torch.Tensor, info_out: torch.Tensor | None = None):
+        """`info_out` (f32 [N, INFO_W], contiguous) receives the info rows
+        instead of the env's own buffer (rollout storage writes in place)."""
         a = actions
         if a.dtype != torch.float32 or a.device != self.device or not a.is_contiguous():
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
         if a.shape != (self.num_envs, ACTION_SIZE):
             raise ValueError(f"actions must be [{self.num_envs}, {ACTION_SIZE}], got {tuple(a.shape)}")
+        info = self.info if info_out is None else info_out
+        if info_out is not None and (info_out.shape != self.info.shape or not info_out.is_contiguous()):
+            raise ValueError("info_out must be a contiguous f32 [N, INFO_W] tensor")
         _lib.check(self._L.rt_env_step(self._h, _lib.ptr(a), _lib.ptr(self.obs), _lib.ptr(self.reward),
-                                       _lib.ptr(self.terminated), _lib.ptr(self.info), _lib.stream_handle()),
+                                       _lib.ptr(self.terminated), _lib.ptr(info), _lib.stream_handle()),
                    "rt_env_step")
-        return self.obs, self.reward, self.terminated.bool(), self.truncated, self._infos()
+        return self.obs, self.reward, self.terminated.bool(), self.truncated, self._infos(info)
 
     def set_next_tumours(self, ids):
         t = torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
@@ -152,8 +157,8 @@ class RadiotherapyVecEnv:
             pass
 
     # ------------------------------------------------------------------ infos
-    def _infos(self):
-        I = self.info
+    def _infos(self, I=None):
+        I = self.info if I is None else I
         stepped = I[:, 16] > 0.5
         ep_done = I[:, 17] > 0.5
         rc = {
