@@ -1,11 +1,12 @@
 // rtenv.hip -- MI355X (gfx950) vectorised radiotherapy environment.
 //
 // Hot path of rmaguado/ppo-radiotherapy re-designed for CDNA4:
-//   environment.py:193-243 RadiotherapyEnv.step   -> k_pose + k_step
-//   transforms.py:7-69     apply_rotation/translation -> pose_update (k_pose)
-//   draw_line.py:4-102     beam_voxels            -> beam_setup + march_iter (k_step)
-//   environment.py:107-191 add_beam + rewards     -> k_step dense pass + tumour phase
-//   environment.py:77-105  reset                  -> k_pose/k_step RESET mode
+//   environment.py:193-243 RadiotherapyEnv.step   -> k_beam + k_dense + k_finish
+//   transforms.py:7-69     apply_rotation/translation -> pose_update (k_beam lane 0)
+//   draw_line.py:4-102     beam_voxels            -> beam_setup + march_splats (k_beam)
+//   environment.py:107-110 add_beam               -> k_beam in-place dose update
+//   environment.py:164-191 rewards / termination  -> k_dense (lung reductions) + k_finish
+//   environment.py:77-105  reset                  -> RESET mode of the same kernels
 //   gymnasium 1.0 SyncVectorEnv NEXT_STEP autoreset + RecordEpisodeStatistics
 //   train.py:163-181       GAE                    -> k_gae
 //
@@ -37,7 +38,7 @@ namespace {
 
 constexpr int kStepThreads = 256;
 constexpr int kUnroll = 8;               // float4 loads in flight per thread
-constexpr int kSegVoxels = 256;          // one wave's 64 x float4 footprint
+constexpr int kSliceVec = 8192;          // k_dense slice: 8192 float4 = 128 KiB of dose
 constexpr int kMaxTumourVoxels = 1024;   // capacity of the per-block tumour phase
 constexpr int kMaxGridDim = 1024;
 constexpr float kEpsF = 1e-6f;           // draw_line.py:4 (f32 under NEP 50)
@@ -67,7 +68,7 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 // ---------------------------------------------------------------------------
-// Per-env beam record: written by k_pose, read by k_step.  (64 B)
+// Per-env beam record: written by k_beam, read by k_dense / k_finish.  (64 B)
 // ---------------------------------------------------------------------------
 struct alignas(16) BeamSetup {
     int32_t mode;      // MODE_*
@@ -364,43 +365,7 @@ __device__ __forceinline__ int march_splats(const int32_t g[3], const BeamSetup&
     return n;
 }
 
-// ---------------------------------------------------------------------------
-// LDS hash of the beam (flat idx -> summed weight).  A voxel receives at most
-// two splats; IEEE add is commutative, so ds_add_f32 in any order reproduces
-// the reference's `output[ix,iy,iz] += weight` exactly.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t hslot(int32_t key, uint32_t mask) {
-    return ((uint32_t)key * 2654435761u >> 7) & mask;
-}
-
-__device__ __forceinline__ void hash_insert(int32_t* keys, float* vals, uint32_t mask, int32_t key,
-                                            float w) {
-    uint32_t h = hslot(key, mask);
-    while (true) {
-        int32_t old = atomicCAS(&keys[h], -1, key);
-        if (old == -1 || old == key) {
-            atomicAdd(&vals[h], w);
-            return;
-        }
-        h = (h + 1) & mask;
-    }
-}
-
-__device__ __forceinline__ bool hash_find(const int32_t* keys, const float* vals, uint32_t mask,
-                                          int32_t key, float& w) {
-    uint32_t h = hslot(key, mask);
-    while (true) {
-        int32_t k = keys[h];
-        if (k == key) {
-            w = vals[h];
-            return true;
-        }
-        if (k == -1) return false;
-        h = (h + 1) & mask;
-    }
-}
-
-struct PoseParams {
+struct BeamParams {
     Geom G;
     Consts C;
     EnvState st;
@@ -415,13 +380,12 @@ struct PoseParams {
 };
 
 // ---------------------------------------------------------------------------
-// k_pose: one lane per env.  Decides STEP / RESET (NEXT_STEP autoreset),
-// samples the tumour on reset, updates the f64 pose and the f32 beam setup.
+// One env's control step (a single lane): NEXT_STEP autoreset decision,
+// tumour sampling on reset (environment.py:86-105), f64 pose update
+// (environment.py:196-210) and the f32 beam setup (draw_line.py:17-66).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pose(PoseParams P) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= P.N) return;
-    EnvState& st = P.st;
+__device__ BeamSetup pose_step(const BeamParams& P, int e) {
+    const EnvState& st = P.st;
     BeamSetup s{};
     int32_t flags = st.flags[e];
     int mode;
@@ -473,35 +437,91 @@ __global__ __launch_bounds__(256) void k_pose(PoseParams P) {
         }
         s.os_r = (float)o.os_r;
         st.t[e] = st.t[e] + 1;
-        beam_setup(P.G.g, o.pos, o.dir, s);  // a direction is never ~0 after renormalisation
+        beam_setup(P.G.g, o.pos, o.dir, s);  // a renormalised direction never takes the ValueError path
     } else {
         s.tumour = st.tumour[e];
     }
-    st.setup[e] = s;
+    return s;
 }
 
-struct StepParams {
-    Geom G;
-    Consts C;
-    EnvState st;
-    Library lib;
-    float* obs;          // [N][9]
-    float* reward;       // [N]
-    uint8_t* terminated; // [N]
-    float* info;         // [N][RT_INFO_W] or null
-    uint32_t hash_mask;  // hash slots - 1
-    int32_t seg_words;   // u32 words of the segment bitmap
-    int32_t max_tvox;    // tumour LDS capacity
-};
+__device__ __forceinline__ int rfl_i(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float rfl_f(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
 
-__device__ __forceinline__ void write_obs9(const StepParams& P, int e, const double* pose,
-                                           const TumourMeta& m) {
-    float* o = P.obs + (size_t)e * 9;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        o[i] = (float)(pose[i] / P.G.S[i] * 2.0 - 1.0);
-        o[3 + i] = (float)pose[3 + i];
-        o[6 + i] = m.obs_c[i];
+// ---------------------------------------------------------------------------
+// k_beam: one wave per env (4 envs per 256-thread block).
+// Lane 0 runs pose_step; then lane k marches iteration k (k, k+64, ...) and
+// applies add_beam (environment.py:107-109) to the voxels it owns:
+//   dose[v] = clip(dose[v] + fl32(b[v] * 0.1f), 0, 1),  b[v] = sum of splats.
+// Only voxels the beam touches change, so the update is done in place on
+// those <= 4*(D+1) voxels.  A voxel receives at most two splats, and only from
+// consecutive iterations (draw_line.py:88-90 puts the +1 offsets on axes 1/2,
+// which is the march axis when dom != 0), so the lane of the lower iteration
+// owns the voxel and adds its neighbour's weight: fl32(w_k + w_k+1) is exactly
+// the reference's `output[...] += weight` sequence (IEEE add commutes).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_beam(BeamParams P) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (e >= P.N) return;  // wave-uniform
+    BeamSetup s{};
+    if (lane == 0) {
+        s = pose_step(P, e);
+        P.st.setup[e] = s;
+    }
+    if (rfl_i(s.mode) != MODE_STEP) return;
+    BeamSetup b;
+    b.niter = rfl_i(s.niter);
+    b.start = rfl_i(s.start);
+    b.stepdir = rfl_i(s.stepdir);
+    b.dom = rfl_i(s.dom);
+    b.o0 = rfl_i(s.o0);
+    b.o1 = rfl_i(s.o1);
+    b.intery0 = rfl_f(s.intery0);
+    b.interz0 = rfl_f(s.interz0);
+    b.sgy = rfl_f(s.sgy);
+    b.sgz = rfl_f(s.sgz);
+    const int niter = b.niter;
+    if (niter <= 0) return;
+    float* dose = P.st.dose + (size_t)e * P.G.Vpad;
+    const float bd = P.C.beam_dose;
+    const bool pairs = b.dom != 0;
+    // running march state: (ya, za) = iteration max(k-1, 0)
+    float ya = b.intery0, za = b.interz0;
+    int k = lane;
+    for (int j = 0; j < k - 1; ++j) {
+        ya = ya + b.sgy;
+        za = za + b.sgz;
+    }
+    for (; k < niter; k += 64) {
+        float yk = ya, zk = za;
+        if (k > 0) {
+            yk = ya + b.sgy;
+            zk = za + b.sgz;
+        }
+        int32_t ci[4], pi[4], ni[4];
+        float cw[4], pw[4], nw[4];
+        int nc = march_splats(P.G.g, b, k, yk, zk, ci, cw);
+        int np = 0, nn = 0;
+        if (pairs && k > 0) np = march_splats(P.G.g, b, k - 1, ya, za, pi, pw);
+        if (pairs && k + 1 < niter) nn = march_splats(P.G.g, b, k + 1, yk + b.sgy, zk + b.sgz, ni, nw);
+        for (int i = 0; i < nc; ++i) {
+            const int32_t v = ci[i];
+            bool owned = true;
+            for (int j = 0; j < np; ++j) owned = owned && (pi[j] != v);
+            if (!owned) continue;
+            float w = cw[i];
+            for (int j = 0; j < nn; ++j)
+                if (ni[j] == v) w = w + nw[j];
+            dose[v] = clip01(dose[v] + w * bd);
+        }
+        // advance (ya, za) to iteration k + 63
+        const int adds = k == 0 ? 63 : 64;
+        for (int j = 0; j < adds; ++j) {
+            ya = ya + b.sgy;
+            za = za + b.sgz;
+        }
     }
 }
 
@@ -521,59 +541,142 @@ __device__ __forceinline__ int wave_sum_i(int v) {
     return v;
 }
 
-#define APPLY_BEAM(comp, vox)                                                       \
-    {                                                                               \
-        float bw;                                                                   \
-        if (hash_find(hkeys, hvals, P.hash_mask, (vox), bw)) {                      \
-            comp = clip01(comp + bw * P.C.beam_dose);                               \
-            hit = true;                                                             \
-        }                                                                           \
-    }
+struct DenseParams {
+    Geom G;
+    float lung_thr;
+    EnvState st;
+    const uint32_t* lung_bits;
+    int32_t* part_cnt;     // [N][slices]
+    double* part_sum;      // [N][slices]
+    int32_t slices;
+    int32_t vec_per_slice; // float4 per slice, multiple of 256
+};
 
-#define REDUCE_VOXEL(comp, bit)                                                     \
-    if ((lb >> (bit)) & 1u) {                                                       \
-        part += comp;                                                               \
-        cnt += comp > P.C.lung_thr ? 1 : 0;                                         \
+#define LUNG_VOXEL(comp, bit)                                                      \
+    if ((lb >> (bit)) & 1u) {                                                      \
+        part += comp;                                                              \
+        cnt += comp > thr ? 1 : 0;                                                 \
     }
 
 // ---------------------------------------------------------------------------
-// k_step: one 256-thread block per env.
-//  phase 1  march: iteration k on thread k, splats -> LDS hash + segment bits
-//  phase 2  tumour voxels: old dose gather, beam applied, lung/threshold
-//           correction, distance argmin (f64)
-//  phase 3  exact np.sum of dose*tumour via the tumour's level plan
-//  phase 4  dense pass over the env's dose row: float4 stream, beam applied
-//           in flagged segments (written back only there), lung-masked
-//           threshold count and dose sum
-//  phase 5  rewards, termination, obs, info, episode statistics
+// k_dense: the full-volume reductions of lungs_dose_reward
+// (environment.py:173-182) and info doses.lung (environment.py:235):
+// count(dose > 0.2 over lung voxels) and sum(dose over lung voxels) for every
+// env, as a read-only float4 stream of each env's dose row split in 128 KiB
+// slices (grid = slices x N).  Tumour voxels are corrected in k_finish.
+// A RESET env's slices are zeroed instead (reset_dose, environment.py:104).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kStepThreads) void k_step(StepParams P) {
-    const int e = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wid = tid >> 6;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t hslots = P.hash_mask + 1;
-    int32_t* hkeys = reinterpret_cast<int32_t*>(smem);
-    float* hvals = reinterpret_cast<float*>(hkeys + hslots);
-    uint32_t* segbits = reinterpret_cast<uint32_t*>(hvals + hslots);
-    float* tvals = reinterpret_cast<float*>(segbits + P.seg_words);
-    __shared__ unsigned long long s_minbits;
-    __shared__ int s_minidx, s_cnt_tum, s_red_i[kStepThreads / 64];
-    __shared__ double s_red_d[kStepThreads / 64];
+__global__ __launch_bounds__(256) void k_dense(DenseParams P) {
+    const int sl = blockIdx.x, e = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int mode = P.st.setup[e].mode;
+    if (mode == MODE_NOOP) return;
+    float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
+    const int nvec = P.G.Vpad >> 2;
+    const int q0 = sl * P.vec_per_slice;
+    const int q1 = min(q0 + P.vec_per_slice, nvec);  // (q1 - q0) % 256 == 0
+    if (mode == MODE_RESET) {
+        for (int q = q0 + tid; q < q1; q += kStepThreads) d4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    const uint32_t* lbits = P.lung_bits;
+    const float thr = P.lung_thr;
+    int cnt = 0;
+    double lsum = 0.0;
+    for (int base = q0; base < q1; base += kStepThreads * kUnroll) {
+        float4 v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            int q = base + u * kStepThreads + tid;
+            v[u] = q < q1 ? d4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            int q = base + u * kStepThreads + tid;
+            if (base + u * kStepThreads >= q1) break;  // block-uniform tail
+            uint32_t lb = (lbits[q >> 3] >> ((q & 7) << 2)) & 0xFu;
+            float part = 0.0f;
+            LUNG_VOXEL(v[u].x, 0)
+            LUNG_VOXEL(v[u].y, 1)
+            LUNG_VOXEL(v[u].z, 2)
+            LUNG_VOXEL(v[u].w, 3)
+            lsum += (double)part;
+        }
+    }
+    __shared__ int s_cnt[kStepThreads / 64];
+    __shared__ double s_sum[kStepThreads / 64];
+    cnt = wave_sum_i(cnt);
+    lsum = wave_sum_d(lsum);
+    if (lane == 0) {
+        s_cnt[wid] = cnt;
+        s_sum[wid] = lsum;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int c = 0;
+        double t = 0.0;
+        for (int w = 0; w < kStepThreads / 64; ++w) {
+            c += s_cnt[w];
+            t += s_sum[w];
+        }
+        P.part_cnt[(size_t)e * P.slices + sl] = c;
+        P.part_sum[(size_t)e * P.slices + sl] = t;
+    }
+}
 
+struct FinishParams {
+    Geom G;
+    Consts C;
+    EnvState st;
+    Library lib;
+    float* obs;          // [N][9]
+    float* reward;       // [N]
+    uint8_t* terminated; // [N]
+    float* info;         // [N][RT_INFO_W] or null
+    const int32_t* part_cnt;
+    const double* part_sum;
+    int32_t slices;
+    int32_t max_tvox;    // per-wave LDS holds 2 * max_tvox floats
+    int32_t N;
+};
+
+__device__ __forceinline__ void write_obs9(float* obs, const Geom& G, int e, const double* pose,
+                                           const TumourMeta& m) {
+    float* o = obs + (size_t)e * 9;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        o[i] = (float)(pose[i] / G.S[i] * 2.0 - 1.0);
+        o[3 + i] = (float)pose[3 + i];
+        o[6 + i] = m.obs_c[i];
+    }
+}
+
+__device__ __forceinline__ void lds_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ---------------------------------------------------------------------------
+// k_finish: one wave per env (4 per block).
+//  - tumour voxels: gather the updated dose, lung-voxel threshold correction
+//    (lungs * (1 - tumours)), distance argmin (environment.py:150-162, f64,
+//    np.argmin first-index tie rule)
+//  - np.sum(dose * tumours) in numpy's exact order via the tumour's level plan
+//  - combine k_dense slices; rewards (environment.py:164-191), termination,
+//    obs (environment.py:259-268), info, episode statistics
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_finish(FinishParams P) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int e = blockIdx.x * 4 + w;
+    if (e >= P.N) return;
+    extern __shared__ __attribute__((aligned(16))) float fsm[];
+    float* tvals = fsm + (size_t)w * 2 * P.max_tvox;
     const BeamSetup s = P.st.setup[e];
     const TumourMeta m = P.lib.meta[s.tumour];
-    double* pose = P.st.pose + (size_t)e * 6;
-    float* dose = P.st.dose + (size_t)e * P.G.Vpad;
-
+    const double* pose = P.st.pose + (size_t)e * 6;
     if (s.mode != MODE_STEP) {
-        if (s.mode == MODE_RESET) {
-            float4* d4 = reinterpret_cast<float4*>(dose);
-            const int nvec = P.G.Vpad >> 2;
-            for (int q = tid; q < nvec; q += kStepThreads) d4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        if (tid == 0) {
-            write_obs9(P, e, pose, m);
+        if (lane == 0) {
+            write_obs9(P.obs, P.G, e, pose, m);
             if (P.reward) P.reward[e] = 0.0f;
             if (P.terminated) P.terminated[e] = 0;
             if (P.info) {
@@ -583,156 +686,80 @@ __global__ __launch_bounds__(kStepThreads) void k_step(StepParams P) {
         }
         return;
     }
-
-    // ---- init LDS ----
-    for (uint32_t i = tid; i < hslots; i += kStepThreads) {
-        hkeys[i] = -1;
-        hvals[i] = 0.0f;
-    }
-    for (int i = tid; i < P.seg_words; i += kStepThreads) segbits[i] = 0u;
-    if (tid == 0) {
-        s_minbits = ~0ull;
-        s_minidx = 0x7fffffff;
-        s_cnt_tum = 0;
-    }
-    __syncthreads();
-
-    // ---- phase 1: beam march (draw_line.py:68-100) ----
-    for (int k = tid; k < s.niter; k += kStepThreads) {
-        float y = s.intery0, z = s.interz0;
-        for (int j = 0; j < k; ++j) {  // sequential f32 accumulation, as the reference
-            y = y + s.sgy;
-            z = z + s.sgz;
-        }
-        int32_t idx[4];
-        float w[4];
-        int n = march_splats(P.G.g, s, k, y, z, idx, w);
-        for (int i = 0; i < n; ++i) {
-            hash_insert(hkeys, hvals, P.hash_mask, idx[i], w[i]);
-            int seg = idx[i] / kSegVoxels;
-            atomicOr(&segbits[seg >> 5], 1u << (seg & 31));
-        }
-    }
-    __syncthreads();
-
-    // ---- phase 2: tumour voxels ----
+    const float* dose = P.st.dose + (size_t)e * P.G.Vpad;
     const int nt = m.n;
     const int32_t* tv = P.lib.vox + m.vox_base;
     const double px = pose[0], py = pose[1], pz = pose[2];
-    const int HW = P.G.g[1] * P.G.g[2];
-    for (int i = tid; i < nt; i += kStepThreads) {
-        int v = tv[i];
-        float x = dose[v];
-        int seg = v / kSegVoxels;
-        if ((segbits[seg >> 5] >> (seg & 31)) & 1u) {
-            float bw;
-            if (hash_find(hkeys, hvals, P.hash_mask, v, bw)) x = clip01(x + bw * P.C.beam_dose);
-        }
+    const int W = P.G.g[2], H = P.G.g[1], HW = H * W;
+    int ctum = 0;
+    double best = INFINITY;
+    int bidx = 0x7fffffff;
+    for (int i = lane; i < nt; i += 64) {
+        const int v = tv[i];
+        const float x = dose[v];
         tvals[i] = x;
-        bool lung = (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u;
-        if (lung && x > P.C.lung_thr) atomicAdd(&s_cnt_tum, 1);
-        int ix = v / HW, iy = (v / P.G.g[2]) % P.G.g[1], iz = v % P.G.g[2];
-        double d0 = (double)ix - px, d1 = (double)iy - py, d2 = (double)iz - pz;
-        double nn = sqrt((d0 * d0 + d1 * d1) + d2 * d2);  // np.linalg.norm(axis=1) order
-        atomicMin(&s_minbits, (unsigned long long)__double_as_longlong(nn));
+        const bool lung = (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u;
+        ctum += (lung && x > P.C.lung_thr) ? 1 : 0;
+        const int ix = v / HW, iy = (v / W) % H, iz = v % W;
+        const double d0 = (double)ix - px, d1 = (double)iy - py, d2 = (double)iz - pz;
+        const double nn = sqrt((d0 * d0 + d1 * d1) + d2 * d2);  // np.linalg.norm(axis=1) order
+        if (nn < best) {
+            best = nn;
+            bidx = i;
+        }
     }
-    __syncthreads();
-    for (int i = tid; i < nt; i += kStepThreads) {  // first index among the minima (np.argmin)
-        int v = tv[i];
-        int ix = v / HW, iy = (v / P.G.g[2]) % P.G.g[1], iz = v % P.G.g[2];
-        double d0 = (double)ix - px, d1 = (double)iy - py, d2 = (double)iz - pz;
-        double nn = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
-        if ((unsigned long long)__double_as_longlong(nn) == s_minbits) atomicMin(&s_minidx, i);
+    ctum = wave_sum_i(ctum);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ob = __shfl_xor(best, off, 64);
+        const int oi = __shfl_xor(bidx, off, 64);
+        if (ob < best || (ob == best && oi < bidx)) {
+            best = ob;
+            bidx = oi;
+        }
     }
-    // ---- phase 3: exact np.sum(dose * tumours) (8192-chunked pairwise order) ----
+    // exact np.sum(dose * tumours): level plan (slots: leaves 0..n-1, op o -> n+o)
     {
         const uint32_t* ops = P.lib.ops + m.op_base;
         const int32_t* lend = P.lib.lvl_end + m.lvl_base;
         int lo = 0;
         for (int l = 0; l < m.nlev; ++l) {
-            __syncthreads();
-            int hi = lend[l];
-            for (int o = lo + tid; o < hi; o += kStepThreads) {
-                uint32_t ab = ops[o];
+            lds_wave_sync();
+            const int hi = lend[l];
+            for (int o = lo + lane; o < hi; o += 64) {
+                const uint32_t ab = ops[o];
                 tvals[nt + o] = tvals[ab & 0xffffu] + tvals[ab >> 16];
             }
             lo = hi;
         }
+        lds_wave_sync();
     }
-    __syncthreads();
-
-    // ---- phase 4: dense pass over the dose row ----
     int cnt = 0;
-    double lsum = 0.0;
-    {
-        float4* d4 = reinterpret_cast<float4*>(dose);
-        const int nvec = P.G.Vpad >> 2;  // multiple of 256
-        const uint32_t* lbits = P.lib.lung_bits;
-        for (int base = 0; base < nvec; base += kStepThreads * kUnroll) {
-            float4 v[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                int q = base + u * kStepThreads + tid;
-                v[u] = q < nvec ? d4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                int q = base + u * kStepThreads + tid;
-                if (base + u * kStepThreads >= nvec) break;  // block-uniform tail
-                uint32_t lb = (lbits[q >> 3] >> ((q & 7) << 2)) & 0xFu;
-                int seg = q >> 6;  // wave-uniform: a wave covers one 256-voxel segment
-                if ((segbits[seg >> 5] >> (seg & 31)) & 1u) {
-                    bool hit = false;
-                    const int v0 = q << 2;
-                    APPLY_BEAM(v[u].x, v0)
-                    APPLY_BEAM(v[u].y, v0 + 1)
-                    APPLY_BEAM(v[u].z, v0 + 2)
-                    APPLY_BEAM(v[u].w, v0 + 3)
-                    if (hit) d4[q] = v[u];
-                }
-                float part = 0.0f;
-                REDUCE_VOXEL(v[u].x, 0)
-                REDUCE_VOXEL(v[u].y, 1)
-                REDUCE_VOXEL(v[u].z, 2)
-                REDUCE_VOXEL(v[u].w, 3)
-                lsum += (double)part;
-            }
-        }
+    double dl = 0.0;
+    for (int j = lane; j < P.slices; j += 64) {
+        cnt += P.part_cnt[(size_t)e * P.slices + j];
+        dl += P.part_sum[(size_t)e * P.slices + j];
     }
     cnt = wave_sum_i(cnt);
-    lsum = wave_sum_d(lsum);
+    dl = wave_sum_d(dl);
     if (lane == 0) {
-        s_red_i[wid] = cnt;
-        s_red_d[wid] = lsum;
-    }
-    __syncthreads();
-
-    // ---- phase 5: rewards (environment.py:164-191), obs, info ----
-    if (tid == 0) {
-        long long c = 0;
-        double dl = 0.0;
-        for (int w = 0; w < kStepThreads / 64; ++w) {
-            c += s_red_i[w];
-            dl += s_red_d[w];
-        }
-        c -= s_cnt_tum;  // lungs * (1 - tumours): tumour voxels are not lung voxels
-        float S = m.result >= 0 ? tvals[m.result] : 0.0f;
-        float ratio = S / m.T;
-        float r_tum = ratio * P.C.tum_reward;
-        double r_lung = (double)c / m.lung_total * P.C.lung_reward;
-        int bi = s_minidx;
-        int v = tv[bi];
-        int ix = v / HW, iy = (v / P.G.g[2]) % P.G.g[1], iz = v % P.G.g[2];
-        double dn = ddot_norm3((double)ix - px, (double)iy - py, (double)iz - pz);
-        double r_dist = dn / P.G.normS * P.C.dist_reward;
-        double total = ((double)r_tum + r_lung) + r_dist;
-        int t = P.st.t[e];
-        bool done = (ratio >= P.C.tum_thr) || (t >= P.C.max_t);
-        write_obs9(P, e, pose, m);
+        const long long c = (long long)cnt - ctum;  // lungs * (1 - tumours)
+        const float S = m.result >= 0 ? tvals[m.result] : 0.0f;
+        const float ratio = S / m.T;
+        const float r_tum = ratio * P.C.tum_reward;
+        const double r_lung = (double)c / m.lung_total * P.C.lung_reward;
+        const int v = tv[bidx];
+        const int ix = v / HW, iy = (v / W) % H, iz = v % W;
+        const double dn = ddot_norm3((double)ix - px, (double)iy - py, (double)iz - pz);
+        const double r_dist = dn / P.G.normS * P.C.dist_reward;
+        const double total = ((double)r_tum + r_lung) + r_dist;
+        const int t = P.st.t[e];
+        const bool done = (ratio >= P.C.tum_thr) || (t >= P.C.max_t);
+        write_obs9(P.obs, P.G, e, pose, m);
         P.reward[e] = (float)total;
         P.terminated[e] = done ? 1 : 0;
-        double ret = P.st.ep_return[e] + total;
-        int len = P.st.ep_len[e] + 1;
+        const double ret = P.st.ep_return[e] + total;
+        const int len = P.st.ep_len[e] + 1;
         P.st.ep_return[e] = ret;
         P.st.ep_len[e] = len;
         if (done) P.st.flags[e] |= FLAG_NEEDS_RESET;
@@ -928,10 +955,12 @@ struct rt_env {
     int visionless = 1;
     EnvState st{};
     Library lib{};
-    uint32_t hash_mask = 0;
-    int seg_words = 0;
     int max_tvox = 0;
-    size_t smem = 0;
+    int slices = 0;          // k_dense slices per env
+    int vec_per_slice = 0;   // float4 per slice
+    size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
+    int32_t* part_cnt = nullptr;
+    double* part_sum = nullptr;
     std::vector<void*> allocs;
 };
 
@@ -1130,11 +1159,10 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     }
     env->lib.K = K;
     env->max_tvox = max_n;
-    int maxdim = std::max(G.g[0], std::max(G.g[1], G.g[2]));
-    env->hash_mask = next_pow2((uint32_t)(8 * (maxdim + 2))) - 1;  // <= 25 % load
-    env->seg_words = (G.Vpad / kSegVoxels + 31) / 32;
-    env->smem = (size_t)(env->hash_mask + 1) * 8 + (size_t)env->seg_words * 4 + (size_t)2 * max_n * 4;
-    if (env->smem > 64 * 1024) { free_env(env); return fail(RT_ELIMIT, "LDS budget exceeded"); }
+    const int nvec = G.Vpad / 4;
+    env->vec_per_slice = std::min(nvec, kSliceVec);
+    env->slices = (nvec + env->vec_per_slice - 1) / env->vec_per_slice;
+    env->finish_smem = (size_t)4 * 2 * max_n * sizeof(float);
 
     // ---- device allocations ----
     const int N = env->N;
@@ -1150,7 +1178,9 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         (rc = dev_alloc(env, &st.t, N)) || (rc = dev_alloc(env, &st.tumour, N)) ||
         (rc = dev_alloc(env, &st.flags, N)) || (rc = dev_alloc(env, &st.episode, N)) ||
         (rc = dev_alloc(env, &st.ep_return, N)) || (rc = dev_alloc(env, &st.ep_len, N)) ||
-        (rc = dev_alloc(env, &st.next_tumour, N)) || (rc = dev_alloc(env, &st.setup, N))) {
+        (rc = dev_alloc(env, &st.next_tumour, N)) || (rc = dev_alloc(env, &st.setup, N)) ||
+        (rc = dev_alloc(env, &env->part_cnt, (size_t)N * env->slices)) ||
+        (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices))) {
         free_env(env);
         return rc;
     }
@@ -1193,51 +1223,65 @@ float* rt_env_dose(rt_env* env, int64_t* stride) {
     return env->st.dose;
 }
 
-static int launch_pair(rt_env* env, bool reset_call, const float* actions, const uint8_t* mask,
+static int launch_step(rt_env* env, bool reset_call, const float* actions, const uint8_t* mask,
                        const int32_t* ids, float* obs, float* reward, uint8_t* term, float* info,
                        hipStream_t stream) {
-    PoseParams pp{};
-    pp.G = env->G;
-    pp.C = env->C;
-    pp.st = env->st;
-    pp.lib = env->lib;
-    pp.actions = actions;
-    pp.reset_mask = mask;
-    pp.reset_ids = ids;
-    pp.N = env->N;
-    pp.is_reset_call = reset_call ? 1 : 0;
-    pp.seed = env->seed;
-    pp.env_id_base = env->env_id_base;
-    hipLaunchKernelGGL(k_pose, dim3((env->N + 255) / 256), dim3(256), 0, stream, pp);
-    RT_LAUNCH_CHECK("k_pose");
-    StepParams sp{};
-    sp.G = env->G;
-    sp.C = env->C;
-    sp.st = env->st;
-    sp.lib = env->lib;
-    sp.obs = obs;
-    sp.reward = reward;
-    sp.terminated = term;
-    sp.info = info;
-    sp.hash_mask = env->hash_mask;
-    sp.seg_words = env->seg_words;
-    sp.max_tvox = env->max_tvox;
-    hipLaunchKernelGGL(k_step, dim3(env->N), dim3(kStepThreads), env->smem, stream, sp);
-    RT_LAUNCH_CHECK("k_step");
+    const int N = env->N;
+    BeamParams bp{};
+    bp.G = env->G;
+    bp.C = env->C;
+    bp.st = env->st;
+    bp.lib = env->lib;
+    bp.actions = actions;
+    bp.reset_mask = mask;
+    bp.reset_ids = ids;
+    bp.N = N;
+    bp.is_reset_call = reset_call ? 1 : 0;
+    bp.seed = env->seed;
+    bp.env_id_base = env->env_id_base;
+    hipLaunchKernelGGL(k_beam, dim3((N + 3) / 4), dim3(256), 0, stream, bp);
+    RT_LAUNCH_CHECK("k_beam");
+    DenseParams dp{};
+    dp.G = env->G;
+    dp.lung_thr = env->C.lung_thr;
+    dp.st = env->st;
+    dp.lung_bits = env->lib.lung_bits;
+    dp.part_cnt = env->part_cnt;
+    dp.part_sum = env->part_sum;
+    dp.slices = env->slices;
+    dp.vec_per_slice = env->vec_per_slice;
+    hipLaunchKernelGGL(k_dense, dim3(env->slices, N), dim3(kStepThreads), 0, stream, dp);
+    RT_LAUNCH_CHECK("k_dense");
+    FinishParams fp{};
+    fp.G = env->G;
+    fp.C = env->C;
+    fp.st = env->st;
+    fp.lib = env->lib;
+    fp.obs = obs;
+    fp.reward = reward;
+    fp.terminated = term;
+    fp.info = info;
+    fp.part_cnt = env->part_cnt;
+    fp.part_sum = env->part_sum;
+    fp.slices = env->slices;
+    fp.max_tvox = env->max_tvox;
+    fp.N = N;
+    hipLaunchKernelGGL(k_finish, dim3((N + 3) / 4), dim3(256), env->finish_smem, stream, fp);
+    RT_LAUNCH_CHECK("k_finish");
     return RT_OK;
 }
 
 int rt_env_reset(rt_env* env, const uint8_t* mask_d, const int32_t* tumour_ids_d, float* obs_d,
                  void* stream) {
     if (!env || !obs_d) return fail(RT_EINVAL, "NULL argument");
-    return launch_pair(env, true, nullptr, mask_d, tumour_ids_d, obs_d, nullptr, nullptr, nullptr,
+    return launch_step(env, true, nullptr, mask_d, tumour_ids_d, obs_d, nullptr, nullptr, nullptr,
                        as_stream(stream));
 }
 
 int rt_env_step(rt_env* env, const float* actions_d, float* obs_d, float* reward_d,
                 uint8_t* terminated_d, float* info_d, void* stream) {
     if (!env || !actions_d || !obs_d || !reward_d || !terminated_d) return fail(RT_EINVAL, "NULL argument");
-    return launch_pair(env, false, actions_d, nullptr, nullptr, obs_d, reward_d, terminated_d, info_d,
+    return launch_step(env, false, actions_d, nullptr, nullptr, obs_d, reward_d, terminated_d, info_d,
                        as_stream(stream));
 }
 
