@@ -8,16 +8,17 @@ num_steps=64, num_minibatches=8, update_epochs=10 and the
 remaining keys of configs/default.yaml.
 
 A bench "step" = one vectorised rollout step of every env on every GPU:
-policy forward + Gaussian sample + the HIP env step (k_pose + k_step), i.e.
-train.py:143-158.  `value` = envs x steps / max-over-ranks wall time.
+policy forward + Gaussian sample + the HIP env step (k_beam + k_dense +
+k_finish), i.e. train.py:143-158.  `value` = envs x steps / max-over-ranks wall time.
 Also reported:
   ppo_updates_per_s      optimizer steps/s of the PPO update phase
                          (80 minibatch steps of 32768 samples per rank, flat
                          gradient all-reduce per step when n_gpus > 1)
   train_env_steps_per_s  env steps/s of a full PPO iteration
                          (64 rollout steps + GAE + 80 updates)
-  roofline               k_step dense pass vs HBM (HIP events on the env
-                         stream over the timed region)
+  roofline               k_dense (the dominant kernel) vs HBM: HIP events the
+                         library records around it on the env stream over
+                         the timed region; traffic from profiles/k_dense_pmc.json
   cpu_baseline           op-for-op NumPy port of the reference step on one
                          host core, same 64^3 workload (bounded sample)
 
@@ -91,8 +92,9 @@ def cpu_baseline(lib, seconds: float):
 
 
 def load_pmc(grid, envs):
-    """Per-launch HBM traffic of k_step from the committed rocprofv3 PMC run."""
-    p = os.path.join(REPO, "profiles", "k_step_pmc.json")
+    """Per-launch HBM traffic of k_dense from the committed rocprofv3 PMC run
+    (tools/parse_pmc.py; gfx950 FETCH_SIZE x2 correction applied there)."""
+    p = os.path.join(REPO, "profiles", "k_dense_pmc.json")
     try:
         with open(p) as f:
             d = json.load(f)
@@ -164,6 +166,7 @@ def main():
     K = a.steps
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     actions = torch.rand((a.envs, 6), device=dev, generator=gen) * 2 - 1
+    env.kernel_timing(K)  # HIP events around k_beam / k_dense / k_finish on the env stream
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -178,8 +181,10 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
-    env_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
-    env_ms = max_over_ranks(env_ms)
+    env_ms = max_over_ranks(float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs])))
+    kms, kcalls = env.kernel_timing_read()
+    env.kernel_timing(0)
+    kms = {k: max_over_ranks(v) for k, v in kms.items()}
     total_envs = a.envs * world
     steps_per_s = total_envs * K / dt
 
@@ -206,14 +211,17 @@ def main():
                "minibatch_size_per_gpu": tr.minibatch_size,
                "train_env_steps_per_s": total_envs * T / di, "train_iteration_s": di}
 
-    # ---------------- roofline of the env kernel pair (k_pose + k_step)
+    # ---------------- roofline of the dominant kernel, k_dense
     V = int(np.prod(grid))
-    bytes_step = 4 * V  # the dense pass reads each env's f32 dose row once
-    achieved = a.envs * bytes_step / (env_ms * 1e-3)
+    bytes_launch = a.envs * 4 * V  # k_dense reads each env's f32 dose row once
+    dense_ms = kms["k_dense"]
+    achieved = bytes_launch / (dense_ms * 1e-3)
     traffic = load_pmc(grid, a.envs)
-    roof = {"bound": "hbm", "kernel": "k_pose+k_step (rt_env_step)", "achieved": achieved / 1e9,
+    roof = {"bound": "hbm", "kernel": "k_dense", "achieved": achieved / 1e9,
             "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
-            "traffic": traffic, "bytes_per_env_step": bytes_step, "env_step_ms": env_ms,
+            "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch, "kernel_ms": dense_ms,
+            "kernel_calls_timed": kcalls, "kernel_ms_all": kms, "env_step_ms": env_ms,
+            "env_step_frac_of_hbm": a.envs * 4 * V / (env_ms * 1e-3) / HBM_PEAK,
             "survey_model_bytes_per_env_step": 8 * V,
             "survey_model_frac": a.envs * 8 * V / (env_ms * 1e-3) / HBM_PEAK}
 

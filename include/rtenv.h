@@ -127,6 +127,15 @@ int rt_env_get_state(rt_env* env, double* pose_d /* f64[N,6] pos,dir */, int32_t
 int rt_env_set_pose(rt_env* env, const double* pose_d /* f64[N,6] */, void* stream);
 int rt_env_num_envs(const rt_env* env);
 
+/* Live kernel timing.  rt_env_kernel_timing(env, K) creates HIP events for
+ * the next K step/reset calls (0 disables; not graph-capturable while on):
+ * each call records events on the caller's stream around its three kernels.
+ * rt_env_kernel_timing_read waits for them and returns the summed
+ * milliseconds of k_beam, k_dense and k_finish (ms_out[3]) over `steps`
+ * calls, then clears the ring. */
+int rt_env_kernel_timing(rt_env* env, int32_t capacity);
+int rt_env_kernel_timing_read(rt_env* env, double* ms_out /* [3] */, int32_t* steps);
+
 /* Parity hooks (same device code as the step kernels). */
 /* beam_voxels for M poses: raw splats in march order, idx_d i32[M,cap],
  * w_d f32[M,cap], count_d i32[M] (-1 = ValueError: direction norm < eps). */

@@ -28,6 +28,7 @@ RT_ERRORS = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EDEVICE", -4:
 EXPORTS = [
     "rt_env_config_default", "rt_env_create", "rt_env_destroy", "rt_env_reset", "rt_env_step",
     "rt_env_set_next_tumours", "rt_env_dose", "rt_env_get_state", "rt_env_set_pose", "rt_env_num_envs",
+    "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_gae", "rt_last_error", "rt_abi_version",
 ]
 
@@ -93,6 +94,8 @@ def load(build_if_missing: bool = True):
         "rt_env_get_state": ([vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_env_set_pose": ([vp, vp, vp], ctypes.c_int),
         "rt_env_num_envs": ([vp], ctypes.c_int),
+        "rt_env_kernel_timing": ([vp, i32], ctypes.c_int),
+        "rt_env_kernel_timing_read": ([vp, ctypes.POINTER(f64), ctypes.POINTER(i32)], ctypes.c_int),
         "rt_debug_beam": ([ctypes.POINTER(i32), i32, vp, vp, i32, vp, vp, vp, vp], ctypes.c_int),
         "rt_debug_pose": ([ctypes.POINTER(i32), i32, vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_host_sincos": ([i32, vp, vp, vp], ctypes.c_int),

@@ -961,6 +961,11 @@ struct rt_env {
     size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
     int32_t* part_cnt = nullptr;
     double* part_sum = nullptr;
+    // optional live kernel timing: 4 events per step (before k_beam, k_dense,
+    // k_finish, after k_finish) in a ring of `timing_cap` steps
+    std::vector<hipEvent_t> tev;
+    int timing_cap = 0;
+    int timing_n = 0;
     std::vector<void*> allocs;
 };
 
@@ -989,6 +994,7 @@ void free_env(rt_env* env) {
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(env->device);
+    for (hipEvent_t e : env->tev) (void)hipEventDestroy(e);
     for (void* p : env->allocs) (void)hipFree(p);
     (void)hipSetDevice(cur);
     delete env;
@@ -1227,6 +1233,9 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
                        const int32_t* ids, float* obs, float* reward, uint8_t* term, float* info,
                        hipStream_t stream) {
     const int N = env->N;
+    hipEvent_t* ev = nullptr;
+    if (env->timing_cap > 0 && env->timing_n < env->timing_cap) ev = &env->tev[(size_t)4 * env->timing_n++];
+    if (ev) (void)hipEventRecord(ev[0], stream);
     BeamParams bp{};
     bp.G = env->G;
     bp.C = env->C;
@@ -1250,8 +1259,10 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     dp.part_sum = env->part_sum;
     dp.slices = env->slices;
     dp.vec_per_slice = env->vec_per_slice;
+    if (ev) (void)hipEventRecord(ev[1], stream);
     hipLaunchKernelGGL(k_dense, dim3(env->slices, N), dim3(kStepThreads), 0, stream, dp);
     RT_LAUNCH_CHECK("k_dense");
+    if (ev) (void)hipEventRecord(ev[2], stream);
     FinishParams fp{};
     fp.G = env->G;
     fp.C = env->C;
@@ -1268,6 +1279,7 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     fp.N = N;
     hipLaunchKernelGGL(k_finish, dim3((N + 3) / 4), dim3(256), env->finish_smem, stream, fp);
     RT_LAUNCH_CHECK("k_finish");
+    if (ev) (void)hipEventRecord(ev[3], stream);
     return RT_OK;
 }
 
@@ -1283,6 +1295,37 @@ int rt_env_step(rt_env* env, const float* actions_d, float* obs_d, float* reward
     if (!env || !actions_d || !obs_d || !reward_d || !terminated_d) return fail(RT_EINVAL, "NULL argument");
     return launch_step(env, false, actions_d, nullptr, nullptr, obs_d, reward_d, terminated_d, info_d,
                        as_stream(stream));
+}
+
+int rt_env_kernel_timing(rt_env* env, int32_t capacity) {
+    if (!env || capacity < 0) return fail(RT_EINVAL, "bad argument");
+    for (hipEvent_t e : env->tev) (void)hipEventDestroy(e);
+    env->tev.clear();
+    env->timing_cap = 0;
+    env->timing_n = 0;
+    if (capacity == 0) return RT_OK;
+    env->tev.resize((size_t)4 * capacity);
+    for (auto& e : env->tev) RT_HIP(hipEventCreate(&e));
+    env->timing_cap = capacity;
+    return RT_OK;
+}
+
+int rt_env_kernel_timing_read(rt_env* env, double* ms_out, int32_t* steps) {
+    if (!env || !ms_out || !steps) return fail(RT_EINVAL, "bad argument");
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (int i = 0; i < env->timing_n; ++i) {
+        hipEvent_t* ev = &env->tev[(size_t)4 * i];
+        RT_HIP(hipEventSynchronize(ev[3]));
+        for (int k = 0; k < 3; ++k) {
+            float ms = 0.0f;
+            RT_HIP(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+            acc[k] += ms;
+        }
+    }
+    for (int k = 0; k < 3; ++k) ms_out[k] = acc[k];
+    *steps = env->timing_n;
+    env->timing_n = 0;
+    return RT_OK;
 }
 
 int rt_env_set_next_tumours(rt_env* env, const int32_t* ids_d, void* stream) {

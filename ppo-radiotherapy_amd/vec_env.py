@@ -144,6 +144,21 @@ class RadiotherapyVecEnv:
         flat = _tensor_from_ptr(p, (self.num_envs, stride.value), torch.float32, self.device)
         return flat[:, :V].reshape(self.num_envs, *self.grid)
 
+    def kernel_timing(self, capacity: int):
+        """Record HIP events around k_beam/k_dense/k_finish for the next
+        `capacity` step/reset calls (0 disables)."""
+        _lib.check(self._L.rt_env_kernel_timing(self._h, int(capacity)), "rt_env_kernel_timing")
+
+    def kernel_timing_read(self):
+        """-> ({'k_beam': ms, 'k_dense': ms, 'k_finish': ms} averaged per call, calls)."""
+        import ctypes
+
+        ms = (ctypes.c_double * 3)()
+        n = ctypes.c_int32()
+        _lib.check(self._L.rt_env_kernel_timing_read(self._h, ms, ctypes.byref(n)), "rt_env_kernel_timing_read")
+        k = max(n.value, 1)
+        return {"k_beam": ms[0] / k, "k_dense": ms[1] / k, "k_finish": ms[2] / k}, n.value
+
     def close(self):
         if getattr(self, "_h", None):
             self._L.rt_env_destroy(self._h)
