@@ -151,6 +151,11 @@ int rt_debug_pose(const int32_t grid[3], int32_t m, const double* pos_d, const d
  * for scipy's from_rotvec half angle (no device needed; parity hook). */
 int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h);
 
+/* Host-side evaluation of the exact-order plan k_finish uses for
+ * np.sum(dose * tumours) over a V-voxel volume whose nonzeros are vals_h at
+ * the sorted flat indices idx_h (no device needed; parity hook). */
+int rt_host_tumour_sum(int64_t V, int32_t n, const int32_t* idx_h, const float* vals_h, float* out_h);
+
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */
 int rt_gae(int32_t T, int32_t N, const float* rewards_d, const float* values_d,

@@ -1038,6 +1038,28 @@ extern "C" {
 
 int rt_abi_version(void) { return RTENV_ABI_VERSION; }
 
+int rt_host_tumour_sum(int64_t V, int32_t n, const int32_t* idx_h, const float* vals_h, float* out_h) {
+    if (V < 1 || n < 0 || !out_h || (n && (!idx_h || !vals_h))) return fail(RT_EINVAL, "bad argument");
+    for (int32_t i = 0; i < n; ++i)
+        if (idx_h[i] < 0 || idx_h[i] >= V || (i && idx_h[i] <= idx_h[i - 1]))
+            return fail(RT_EINVAL, "indices must be sorted, unique and < V");
+    PlanBuilder pb{idx_h, n, V};
+    int res = pb.build();
+    // evaluate in level order exactly as k_finish does
+    int nops = (int)pb.opa.size();
+    std::vector<int> order(nops);
+    for (int i = 0; i < nops; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return pb.lvl[x] < pb.lvl[y]; });
+    std::vector<float> slot((size_t)n + nops);
+    for (int i = 0; i < n; ++i) slot[i] = vals_h[i];
+    for (int o = 0; o < nops; ++o) {
+        int src = order[o];
+        slot[(size_t)n + src] = slot[pb.opa[src]] + slot[pb.opb[src]];
+    }
+    *out_h = res < 0 ? 0.0f : slot[res];
+    return RT_OK;
+}
+
 int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h) {
     if (n < 0 || (n && (!x_h || !sin_h || !cos_h))) return fail(RT_EINVAL, "bad argument");
     for (int32_t i = 0; i < n; ++i) {

@@ -1,0 +1,119 @@
+"""The C-ABI library (include/rtenv.h -> librtenv.so) on a host without a GPU:
+it loads, exports every declared symbol, its config struct layout matches the
+header, and its host-side parity hooks agree with the reference numerics."""
+import ctypes
+import math
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from ppo_radiotherapy_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "rtenv.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    L = _lib.load()
+    decl = declared_functions()
+    assert len(decl) >= 15
+    for name in decl:
+        assert hasattr(L, name), name
+    assert sorted(_lib.EXPORTS) == decl
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (rt_\w+)", out))
+    assert set(decl) <= exported
+
+
+def test_library_has_gfx950_code_object():
+    # the fat binary embeds the offload bundle for gfx950 (and nothing else)
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"amdgcn-amd-amdhsa--gfx942" not in data
+
+
+def test_config_struct_layout_matches_header(tmp_path):
+    fields = [f[0] for f in _lib.RtEnvConfig._fields_]
+    probe = tmp_path / "probe.c"
+    body = "\n".join(f'    printf("{f} %zu\\n", offsetof(rt_env_config, {f}));' for f in fields)
+    probe.write_text(f'#include <stddef.h>\n#include <stdio.h>\n#include "rtenv.h"\nint main(void) {{\n'
+                     f'    printf("sizeof %zu\\n", sizeof(rt_env_config));\n{body}\n    return 0;\n}}\n')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(probe), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                       check=True).stdout.splitlines())
+    assert int(got["sizeof"]) == ctypes.sizeof(_lib.RtEnvConfig)
+    for f in fields:
+        assert int(got[f]) == getattr(_lib.RtEnvConfig, f).offset, f
+
+
+def test_config_defaults_are_reference_constants():
+    L = _lib.load()
+    c = _lib.RtEnvConfig()
+    assert L.rt_env_config_default(c) == 0
+    assert list(c.grid) == [67, 43, 70] and c.max_time_steps == 100
+    assert c.beam_dose == np.float32(0.1) and c.lung_dose_threshold == np.float32(0.2)
+    assert c.tumour_dose_threshold == np.float32(0.9) and c.min_angle_z == math.pi / 4
+    assert c.movement_speed == 0.2 and c.rotation_speed == 0.5
+    assert (c.lung_dose_reward, c.tumour_dose_reward, c.distance_reward) == (-1.0, 10.0, -1.0)
+    assert L.rt_abi_version() == 1
+
+
+def test_error_paths_do_not_abort():
+    L = _lib.load()
+    h = ctypes.c_void_p()
+    rc = L.rt_env_create(None, 0, h)
+    assert rc == -1 and b"NULL" in L.rt_last_error()
+    c = _lib.RtEnvConfig()
+    L.rt_env_config_default(c)
+    c.num_envs = 0
+    assert L.rt_env_create(c, 0, h) == -1
+    assert L.rt_gae(0, 1, None, None, None, None, None, 0.99, 0.95, None, None, None) == -1
+    with pytest.raises(_lib.RtError):
+        _lib.check(-1, "probe")
+
+
+def test_host_sincos_matches_libm():
+    L = _lib.load()
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.uniform(0, 1.3614, 200000), [0.0, 1e-300, 5e-4, 1.3614]])
+    s = np.zeros_like(x)
+    c = np.zeros_like(x)
+    assert L.rt_host_sincos(len(x), x.ctypes.data, s.ctypes.data, c.ctypes.data) == 0
+    gs = np.array([math.sin(v) for v in x])
+    gc = np.array([math.cos(v) for v in x])
+    # glibc is correctly rounded except near rounding midpoints (~0.15 %)
+    assert np.mean(s == gs) > 0.995 and np.mean(c == gc) > 0.995
+    assert np.all(np.abs(s.view(np.int64) - gs.view(np.int64)) <= 1)
+    assert np.all(np.abs(c.view(np.int64) - gc.view(np.int64)) <= 1)
+
+
+@pytest.mark.parametrize("V", [201670, 262144, 2097152, 1000, 8192 * 3 + 5])
+def test_exact_tumour_sum_plan(V):
+    """k_finish's plan reproduces np.sum over the dense f32 volume bit-exactly."""
+    L = _lib.load()
+    rng = np.random.default_rng(V)
+    for trial in range(40):
+        n = int(rng.integers(1, min(V, 1024)))
+        if trial % 3 == 0:  # a compact blob like a tumour
+            start = int(rng.integers(0, max(V - 4 * n, 1)))
+            idx = np.unique(start + rng.integers(0, 4 * n, n)).astype(np.int32)
+            idx = idx[idx < V]
+        else:
+            idx = np.sort(rng.choice(V, size=n, replace=False)).astype(np.int32)
+        vals = (rng.random(idx.size) * rng.choice([1.0, 1e-3, 1e3])).astype(np.float32)
+        dense = np.zeros(V, np.float32)
+        dense[idx] = vals
+        out = np.zeros(1, np.float32)
+        assert L.rt_host_tumour_sum(V, idx.size, idx.ctypes.data, vals.ctypes.data, out.ctypes.data) == 0
+        assert out[0] == np.sum(dense.reshape(-1)), (V, trial)
