@@ -53,8 +53,11 @@ class IterStats:
 
 class PPOTrainer:
     def __init__(self, cfg, env, agent: nn.Module, device, rank: int = 0, world: int = 1,
-                 generator: torch.Generator | None = None):
+                 generator: torch.Generator | None = None, gae_fn=None):
+        """`gae_fn(trainer, next_value)` replaces the rt_gae kernel (tests run
+        the trainer on CPU with a torch reference GAE)."""
         self.cfg = cfg
+        self.gae_fn = gae_fn
         self.env = env
         self.agent = agent
         self.device = torch.device(device)
@@ -85,7 +88,7 @@ class PPOTrainer:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
             off += p.numel()
         self.optimizer = torch.optim.Adam(self.params, lr=float(cfg.learning_rate), eps=1e-5,
-                                          foreach=True)
+                                          foreach=self.device.type == "cuda")
         self.next_obs = None
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
@@ -126,6 +129,8 @@ class PPOTrainer:
     def compute_gae(self):
         """train.py:163-181 via the rt_gae HIP kernel."""
         next_value = self.agent.get_value(self.next_obs).reshape(-1).contiguous()
+        if self.gae_fn is not None:
+            return self.gae_fn(self, next_value)
         L = _lib.load()
         _lib.check(L.rt_gae(self.T, self.N, self.rewards.data_ptr(), self.values.data_ptr(),
                             self.dones.data_ptr(), next_value.data_ptr(), self.next_done.data_ptr(),
@@ -191,7 +196,7 @@ class PPOTrainer:
                 self.flat_grad.zero_()
                 loss.backward()
                 self._allreduce_(self.flat_grad)
-                nn.utils.clip_grad_norm_(self.params, float(cfg.max_grad_norm), foreach=True)
+                nn.utils.clip_grad_norm_(self.params, float(cfg.max_grad_norm))
                 self.optimizer.step()
                 n_mb += 1
         self._last = dict(pg_loss=pg_loss.detach(), v_loss=v_loss.detach(), entropy=entropy_loss.detach(),

@@ -1,0 +1,76 @@
+"""Config, logging, assets and the single-env facade's reference RNG draw."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ppo_radiotherapy_amd import assets, config, logger
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_config_keys_and_derivation(tmp_path):
+    cfg = config.derive(config.load(os.path.join(REPO, "configs", "default.yaml")))
+    # train.py:292-297 on default.yaml.template values
+    assert cfg.batch_size == 16 * 2048 and cfg.minibatch_size == 1024
+    assert cfg.num_iterations == 10000000 // 32768 == 305
+    assert cfg.save_frequency_iterations == 61
+    assert cfg.visionless is True and cfg.learning_rate == 3e-4
+    p = tmp_path / "c.yaml"
+    config.save(cfg, str(p))
+    again = config.load(str(p))
+    assert again.batch_size == cfg.batch_size
+    with pytest.raises(ValueError):
+        config.derive(config.load(os.path.join(REPO, "configs", "default.yaml")), world=3)
+    v = config.derive(config.load(os.path.join(REPO, "configs", "vision.yaml")))
+    assert v.visionless is False and v.minibatch_size == 16 * 128 // 2
+
+
+def test_jsonl_writer(tmp_path):
+    w = logger.JsonlWriter(str(tmp_path))
+    w.add_scalar("charts/episodic_return", 1.5, 10)
+    w.add_text("hyperparameters", "|a|b|")
+    w.close()
+    rows = [json.loads(x) for x in open(tmp_path / "scalars.jsonl")]
+    assert rows[0] == {**rows[0], "tag": "charts/episodic_return", "value": 1.5, "step": 10}
+
+
+def test_reference_library():
+    lib = assets.reference_library()
+    assert lib.shape == (67, 43, 70) and lib.n_tumours == 1000
+    assert int(lib.lungs.sum()) == 74029
+    sizes = np.diff(lib.offsets)
+    assert sizes.min() == 16 and sizes.max() == 586
+    for k in (0, 17, 999):
+        v = lib.tumour_voxels(k)
+        assert np.all(np.diff(v) > 0)
+    # centroid = mean of np.where coordinates (environment.py:145-148)
+    vol = lib.tumour_dense(5)
+    np.testing.assert_array_equal(lib.centroid(5), np.mean(np.stack(np.where(vol == 1.0), -1), axis=0))
+
+
+def test_synthetic_library_64():
+    lib = assets.synthetic_library((64, 64, 64), 200, 0)
+    sizes = np.diff(lib.offsets)
+    assert lib.n_tumours == 200 and sizes.min() >= 8 and sizes.max() <= 1024
+    assert 16 <= np.median(sizes) <= 600
+    # deterministic and prefix-stable in n_tumours
+    small = assets.synthetic_library((64, 64, 64), 20, 0)
+    np.testing.assert_array_equal(small.voxels, lib.voxels[:small.offsets[-1]])
+    # tumour centres lie in the lung mask
+    for k in range(20):
+        c = np.round(lib.centroid(k)).astype(int)
+        assert lib.lungs[tuple(np.clip(c, 0, 63))] in (0, 1)
+
+
+def test_facade_draws_tumours_like_the_reference():
+    """RadiotherapyEnv.reset draws np.random.choice(len(names)); the reference
+    draws np.random.choice(names) (environment.py:90): same stream, same pick."""
+    names = assets.reference_library().names
+    for seed in range(20):
+        np.random.seed(seed)
+        a = np.random.choice(names)
+        np.random.seed(seed)
+        b = names[int(np.random.choice(len(names)))]
+        assert a == b

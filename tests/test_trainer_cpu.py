@@ -1,0 +1,124 @@
+"""Trainer host logic and the data-parallel path on CPU (gloo, world_size 2)."""
+import os
+import socket
+import sys
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _rtpkg  # noqa: E402,F401  (spawned workers do not run conftest)
+from fake_env import FakeVecEnv, torch_gae  # noqa: E402
+
+from ppo_radiotherapy_amd.networks import PPO  # noqa: E402
+from ppo_radiotherapy_amd.ppo import PPOTrainer, broadcast_parameters  # noqa: E402
+
+
+def _cfg(**kw):
+    c = dict(num_steps=8, num_minibatches=4, update_epochs=2, learning_rate=3e-4, anneal_lr=False, gamma=0.99,
+             gae_lambda=0.95, norm_adv=True, clip_coef=0.1, clip_vloss=True, ent_coef=0.0, vf_coef=0.5,
+             max_grad_norm=0.5)
+    c.update(kw)
+    return SimpleNamespace(**c)
+
+
+def _trainer(n_envs, seed, rank=0, world=1, init_seed=1234):
+    torch.manual_seed(init_seed)
+    agent = PPO((9,), (6,), 64)
+    gen = torch.Generator().manual_seed(seed)
+    tr = PPOTrainer(_cfg(), FakeVecEnv(n_envs, seed), agent, "cpu", rank, world, gen, gae_fn=torch_gae)
+    tr.reset()
+    return tr
+
+
+def test_single_process_iteration():
+    tr = _trainer(16, 0)
+    st = tr.train_iteration(1, 10) if torch.cuda.is_available() else None
+    if st is None:  # no device sync on CPU
+        tr.rollout()
+        tr.compute_gae()
+        n = tr.update()
+        assert n == 2 * 4
+        st = tr.iteration_stats()
+    assert st.episodes > 0 and np.isfinite(st.value_loss) and np.isfinite(st.approx_kl)
+    assert abs(st.episodic_length - 7.0) < 1e-6
+    assert all(torch.isfinite(p).all() for p in tr.agent.parameters())
+
+
+def test_flat_gradient_bucket_views_params():
+    tr = _trainer(4, 0)
+    assert all(p.grad.data_ptr() >= tr.flat_grad.data_ptr() for p in tr.params)
+    tr.flat_grad.fill_(2.0)
+    assert all(bool((p.grad == 2.0).all()) for p in tr.params)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # deliberately different init per rank: broadcast_parameters must align them
+    tr = _trainer(8, seed=rank, rank=rank, world=world, init_seed=100 + rank)
+    broadcast_parameters(tr.agent)
+    tr.rollout()
+    tr.compute_gae()
+    # one minibatch gradient by hand: local grads, then the bucket all-reduce
+    tr.flat_grad.zero_()
+    loss = sum((p ** 2).sum() for p in tr.params) * (rank + 1)
+    loss.backward()
+    local = tr.flat_grad.clone()
+    tr._allreduce_(tr.flat_grad)
+    reduced = tr.flat_grad.clone()
+    # global advantage normalisation == single-process statistics of the union
+    adv = tr.advantages.reshape(-1)
+    normed = tr._norm_adv(adv)
+    gathered = [torch.zeros_like(adv) for _ in range(world)]
+    dist.all_gather(gathered, adv)
+    full = torch.cat(gathered)
+    expect = (adv - full.mean()) / (full.std() + 1e-8)
+    tr.update()
+    flat_params = torch.cat([p.detach().reshape(-1) for p in tr.params])
+    q.put((rank, local.numpy().copy(), reduced.numpy().copy(), flat_params.numpy().copy(),
+           float((normed - expect).abs().max())))
+    dist.destroy_process_group()
+
+
+def test_data_parallel_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    import queue
+    import time
+    deadline = time.time() + 240
+    while len(res) < world and time.time() < deadline:
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"worker failed with exit code {dead[0].exitcode}"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(res) == world
+    res = sorted(res, key=lambda x: x[0])
+    (_, l0, g0, p0, e0), (_, l1, g1, p1, e1) = res
+    np.testing.assert_allclose(g0, (l0 + l1) / 2, rtol=1e-6, atol=1e-7)   # averaged bucket
+    np.testing.assert_array_equal(g0, g1)
+    np.testing.assert_array_equal(p0, p1)  # replicas stay identical through the update
+    assert e0 < 1e-5 and e1 < 1e-5
