@@ -33,7 +33,9 @@ def test_facade_replays_reference_trajectory(golden):
         for t in range(int(z["ep_len"][e])):
             obs, r, done, trunc, info = env.step(z["actions"][e][t])
             k = off + t
-            np.testing.assert_array_equal(obs, z["step_obs"][k])
+            # f64 obs: position and centroid exact; direction within an ulp (libm sin/cos)
+            np.testing.assert_array_equal(obs[[0, 1, 2, 6, 7, 8]], z["step_obs"][k][[0, 1, 2, 6, 7, 8]])
+            assert np.abs(obs[3:6] - z["step_obs"][k][3:6]).max() <= 1e-15
             np.testing.assert_array_equal(np.array(info["beam_position"]["translation"]), z["step_pos"][k])
             assert abs(r - z["step_reward"][k]) <= 1e-5 and trunc is False
             assert abs(info["reward_components"]["tumour"] - z["step_tumour"][k]) <= 1e-5
