@@ -22,6 +22,47 @@ from torch import nn
 _HALF_LOG_2PI = 0.5 * math.log(2.0 * math.pi)
 
 
+class _SplitKLinearFn(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient W' = dY^T X (a K = batch reduction:
+    32768 in the PPO update) is computed as a batched GEMM over `chunks` slices
+    of the batch plus one sum, so the reduction runs on many workgroups; the
+    GEMM libraries give a K = 32768, 64 x 64 product only a handful."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, chunks):
+        ctx.save_for_backward(x, weight)
+        ctx.chunks = chunks
+        return torch.addmm(bias, x, weight.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gx = gy.mm(weight) if ctx.needs_input_grad[0] else None
+        c = ctx.chunks
+        B = x.shape[0]
+        if c > 1 and B % c == 0:
+            gw = torch.bmm(gy.reshape(c, B // c, -1).transpose(1, 2), x.reshape(c, B // c, -1)).sum(0)
+        else:
+            gw = gy.t().mm(x)
+        return gx, gw, gy.sum(0), None
+
+
+SPLITK_MIN_BATCH = 4096
+SPLITK_CHUNK = 512  # rows per slice of the weight-gradient reduction
+
+
+class Linear(nn.Linear):
+    """nn.Linear (same parameters and state-dict keys) with the split-K
+    weight gradient for large batches (2-D inputs)."""
+
+    def forward(self, x):
+        B = x.shape[0] if x.dim() == 2 else 0
+        if x.requires_grad or self.weight.requires_grad:
+            if B >= SPLITK_MIN_BATCH and B % SPLITK_CHUNK == 0 and torch.is_grad_enabled():
+                return _SplitKLinearFn.apply(x, self.weight, self.bias, B // SPLITK_CHUNK)
+        return super().forward(x)
+
+
 def layer_init(layer: nn.Module, std: float = float(np.sqrt(2)), bias_const: float = 0.0) -> nn.Module:
     """Orthogonal weights, constant bias (networks.py:48-51)."""
     nn.init.orthogonal_(layer.weight, std)
@@ -32,9 +73,9 @@ def layer_init(layer: nn.Module, std: float = float(np.sqrt(2)), bias_const: flo
 def _tanh_mlp(d_in: int, width: int, d_out: int, head_std: float) -> nn.Sequential:
     # indices 0/2/4 hold the Linear layers, as in the reference's Sequential
     return nn.Sequential(
-        layer_init(nn.Linear(d_in, width)), nn.Tanh(),
-        layer_init(nn.Linear(width, width)), nn.Tanh(),
-        layer_init(nn.Linear(width, d_out), std=head_std),
+        layer_init(Linear(d_in, width)), nn.Tanh(),
+        layer_init(Linear(width, width)), nn.Tanh(),
+        layer_init(Linear(width, d_out), std=head_std),
     )
 
 

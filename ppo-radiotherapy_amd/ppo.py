@@ -82,13 +82,24 @@ class PPOTrainer:
         self.params = [p for p in agent.parameters()]
         # one flat gradient bucket; every param.grad is a view of it
         n = sum(p.numel() for p in self.params)
-        self.flat_grad = torch.zeros(n, **kw)
+        self.flat_grad = torch.zeros(n, dtype=self.params[0].dtype, **kw)
         off = 0
         for p in self.params:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
             off += p.numel()
-        self.optimizer = torch.optim.Adam(self.params, lr=float(cfg.learning_rate), eps=1e-5,
-                                          foreach=self.device.type == "cuda")
+        # hipGraph capture of the minibatch step.  OFF by default: on the torch
+        # 2.10/ROCm 7.0 runtime the graph captured from autograd's backward
+        # replays with a missing ordering edge (results depend on timing; exact
+        # under AMD_SERIALIZE_KERNEL=3) -- see DESIGN.md §9, tests/test_gpu_trainer.py
+        self.use_graphs = (bool(getattr(cfg, "cuda_graphs", False)) and self.device.type == "cuda"
+                           and self.batch_size % self.minibatch_size == 0)
+        self._graph_fb = None
+        self._graph_opt = None
+        self._last_stats = None
+        # a device-tensor lr lets anneal_lr update a captured optimizer step in place
+        lr = torch.tensor(float(cfg.learning_rate), device=self.device) if self.use_graphs else float(cfg.learning_rate)
+        self.optimizer = torch.optim.Adam(self.params, lr=lr, eps=1e-5,
+                                          foreach=self.device.type == "cuda", capturable=self.use_graphs)
         self.next_obs = None
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
@@ -156,52 +167,174 @@ class PPOTrainer:
         var = (s[1] - s[2] * mean * mean) / (s[2] - 1.0)
         return (adv - mean.float()) / (var.clamp_min(0).sqrt().float() + 1e-8)
 
-    def update(self):
-        """train.py:183-248."""
+    def _epoch_adv_stats(self, b_adv: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+        """[n_mb, 2] (mean, std) of every minibatch of this epoch: the
+        reference's per-minibatch normalisation (train.py:215-218), global over
+        ranks with ONE all-reduce per epoch."""
+        n_mb = self.batch_size // self.minibatch_size
+        a = b_adv[perm[:n_mb * self.minibatch_size]].view(n_mb, self.minibatch_size)
+        if self.world == 1:
+            return torch.stack([a.mean(1), a.std(1)], 1)
+        d = a.double()
+        s = torch.stack([d.sum(1), (d * d).sum(1), torch.full((n_mb,), float(self.minibatch_size),
+                                                              dtype=torch.float64, device=d.device)], 1)
+        self._allreduce_(s, average=False)
+        mean = s[:, 0] / s[:, 2]
+        var = (s[:, 1] - s[:, 2] * mean * mean) / (s[:, 2] - 1.0)
+        return torch.stack([mean, var.clamp_min(0).sqrt()], 1).float()
+
+    def _minibatch_loss_backward(self, mb, adv_mean=None, adv_std=None):
+        """train.py:200-246 for one minibatch: losses, then backward into the
+        flat gradient bucket.  Returns the logged statistics."""
         cfg = self.cfg
-        b_obs = self.obs.reshape((-1,) + self.obs.shape[2:])
-        b_logprobs = self.logprobs.reshape(-1)
-        b_actions = self.actions.reshape((-1,) + self.actions.shape[2:])
-        b_adv = self.advantages.reshape(-1)
-        b_ret = self.returns.reshape(-1)
-        b_val = self.values.reshape(-1)
         clip = float(cfg.clip_coef)
+        _, newlogprob, entropy, newvalue = self.agent.get_action_and_value(self._b_obs[mb], self._b_actions[mb])
+        logratio = newlogprob - self._b_logprobs[mb]
+        ratio = logratio.exp()
+        with torch.no_grad():
+            old_approx_kl = (-logratio).mean()
+            approx_kl = ((ratio - 1) - logratio).mean()
+            clipfrac = ((ratio - 1.0).abs() > clip).float().mean()
+        mb_adv = self._b_adv[mb]
+        if cfg.norm_adv:
+            if adv_mean is None:
+                mb_adv = self._norm_adv(mb_adv)
+            else:
+                mb_adv = (mb_adv - adv_mean) / (adv_std + 1e-8)
+        pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+        newvalue = newvalue.view(-1)
+        b_ret, b_val = self._b_ret[mb], self._b_val[mb]
+        if cfg.clip_vloss:
+            v_unclipped = (newvalue - b_ret) ** 2
+            v_clipped = b_val + torch.clamp(newvalue - b_val, -clip, clip)
+            v_loss = 0.5 * torch.max(v_unclipped, (v_clipped - b_ret) ** 2).mean()
+        else:
+            v_loss = 0.5 * ((newvalue - b_ret) ** 2).mean()
+        entropy_loss = entropy.mean()
+        loss = pg_loss - float(cfg.ent_coef) * entropy_loss + v_loss * float(cfg.vf_coef)
+        self.flat_grad.zero_()
+        loss.backward()
+        return torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,
+                            approx_kl, clipfrac])
+
+    def _optimizer_step(self):
+        nn.utils.clip_grad_norm_(self.params, float(self.cfg.max_grad_norm))
+        self.optimizer.step()
+
+    def _bind_batch(self):
+        self._b_obs = self.obs.reshape((-1,) + self.obs.shape[2:])
+        self._b_logprobs = self.logprobs.reshape(-1)
+        self._b_actions = self.actions.reshape((-1,) + self.actions.shape[2:])
+        self._b_adv = self.advantages.reshape(-1)
+        self._b_ret = self.returns.reshape(-1)
+        self._b_val = self.values.reshape(-1)
+
+    def update(self):
+        """train.py:183-248: update_epochs x num_minibatches optimizer steps."""
+        if self.use_graphs:
+            return self._update_graphed()
+        self._bind_batch()
         dev = self.device
-        clipfrac_sum = torch.zeros((), device=dev)
+        stats_sum = torch.zeros(6, device=dev)
         n_mb = 0
-        for _ in range(int(cfg.update_epochs)):
+        for _ in range(int(self.cfg.update_epochs)):
             perm = torch.randperm(self.batch_size, device=dev, generator=self.gen)
             for start in range(0, self.batch_size, self.minibatch_size):
                 mb = perm[start:start + self.minibatch_size]
-                _, newlogprob, entropy, newvalue = self.agent.get_action_and_value(b_obs[mb], b_actions[mb])
-                logratio = newlogprob - b_logprobs[mb]
-                ratio = logratio.exp()
-                with torch.no_grad():
-                    old_approx_kl = (-logratio).mean()
-                    approx_kl = ((ratio - 1) - logratio).mean()
-                    clipfrac_sum += ((ratio - 1.0).abs() > clip).float().mean()
-                mb_adv = b_adv[mb]
-                if cfg.norm_adv:
-                    mb_adv = self._norm_adv(mb_adv)
-                pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
-                newvalue = newvalue.view(-1)
-                if cfg.clip_vloss:
-                    v_unclipped = (newvalue - b_ret[mb]) ** 2
-                    v_clipped = b_val[mb] + torch.clamp(newvalue - b_val[mb], -clip, clip)
-                    v_loss = 0.5 * torch.max(v_unclipped, (v_clipped - b_ret[mb]) ** 2).mean()
-                else:
-                    v_loss = 0.5 * ((newvalue - b_ret[mb]) ** 2).mean()
-                entropy_loss = entropy.mean()
-                loss = pg_loss - float(cfg.ent_coef) * entropy_loss + v_loss * float(cfg.vf_coef)
-                self.flat_grad.zero_()
-                loss.backward()
+                st = self._minibatch_loss_backward(mb)
+                stats_sum[5] += st[5]
                 self._allreduce_(self.flat_grad)
-                nn.utils.clip_grad_norm_(self.params, float(cfg.max_grad_norm))
-                self.optimizer.step()
+                self._optimizer_step()
                 n_mb += 1
-        self._last = dict(pg_loss=pg_loss.detach(), v_loss=v_loss.detach(), entropy=entropy_loss.detach(),
-                          old_approx_kl=old_approx_kl, approx_kl=approx_kl, clipfrac=clipfrac_sum / max(n_mb, 1))
+        self._last_stats = torch.cat([st[:5], (stats_sum[5] / max(n_mb, 1)).reshape(1)])
         return n_mb
+
+    # ---- hipGraph-captured update -------------------------------------------------
+    def _capture(self):
+        """Capture one minibatch step into HIP graph(s).  world == 1: one graph
+        (loss, backward, clip, Adam); world > 1: two graphs with the RCCL
+        bucket all-reduce between them.  The minibatch indices and advantage
+        statistics are static input buffers refreshed before each replay."""
+        dev = self.device
+        mbs = self.minibatch_size
+        self._bind_batch()
+        self._g_idx = torch.zeros(mbs, dtype=torch.long, device=dev)
+        self._g_adv = torch.zeros(2, device=dev)
+        self._g_adv[1] = 1.0
+        # warm up on a side stream, then restore parameters and optimizer state
+        saved_p = [p.detach().clone() for p in self.params]
+        saved_o = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in
+                   ((i, t) for i, t in enumerate(self._opt_state_tensors()))}
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self._minibatch_loss_backward(self._g_idx, self._g_adv[0], self._g_adv[1])
+                self._optimizer_step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        with torch.no_grad():
+            for p, q in zip(self.params, saved_p):
+                p.copy_(q)
+            for i, t in enumerate(self._opt_state_tensors()):
+                t.copy_(saved_o[i])
+        self._graph_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph_fb):
+            self._g_stats = self._minibatch_loss_backward(self._g_idx, self._g_adv[0], self._g_adv[1])
+            if self.world == 1:
+                self._optimizer_step()
+        self._graph_opt = None
+        if self.world > 1:
+            self._graph_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph_opt):
+                self._optimizer_step()
+        torch.cuda.synchronize(dev)
+
+    def _opt_state_tensors(self):
+        out = []
+        for p in self.params:
+            st = self.optimizer.state.get(p, {})
+            for k in sorted(st):
+                if torch.is_tensor(st[k]):
+                    out.append(st[k])
+        return out
+
+    def _update_graphed(self):
+        if self._graph_fb is None:
+            # the optimizer state must exist (with device step counters) before capture
+            self._init_capturable_state()
+            self._capture()
+        dev = self.device
+        clip_sum = torch.zeros((), device=dev)
+        n_mb = 0
+        mbs = self.minibatch_size
+        for _ in range(int(self.cfg.update_epochs)):
+            perm = torch.randperm(self.batch_size, device=dev, generator=self.gen)
+            adv_stats = self._epoch_adv_stats(self._b_adv, perm) if self.cfg.norm_adv else None
+            for i, start in enumerate(range(0, self.batch_size - mbs + 1, mbs)):
+                self._g_idx.copy_(perm[start:start + mbs])
+                if adv_stats is not None:
+                    self._g_adv.copy_(adv_stats[i])
+                self._graph_fb.replay()
+                if self._graph_opt is not None:
+                    self._allreduce_(self.flat_grad)
+                    self._graph_opt.replay()
+                clip_sum += self._g_stats[5]
+                n_mb += 1
+        self._last_stats = torch.cat([self._g_stats[:5], (clip_sum / max(n_mb, 1)).reshape(1)])
+        return n_mb
+
+    def _init_capturable_state(self):
+        """Adam(capturable=True) keeps its step counters on the device; run a
+        zero-gradient step once so every state tensor exists (params restored)."""
+        saved = [p.detach().clone() for p in self.params]
+        self.flat_grad.zero_()
+        self.optimizer.step()
+        with torch.no_grad():
+            for p, q in zip(self.params, saved):
+                p.copy_(q)
+            for t in self._opt_state_tensors():
+                t.zero_()
 
     # ------------------------------------------------------------------ stats
     @torch.no_grad()
@@ -220,10 +353,10 @@ class PPOTrainer:
         var_y = y_true.var(unbiased=False)
         ev = torch.where(var_y == 0, torch.tensor(float("nan"), device=y_true.device),
                          1 - (y_true - y_pred).var(unbiased=False) / var_y)
-        last = self._last if hasattr(self, "_last") else {}
-        host = torch.cat([vals, ev.double().reshape(1)] +
-                         [last[k].double().reshape(1) for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl",
-                                                                "approx_kl", "clipfrac") if k in last]).cpu().numpy()
+        parts = [vals, ev.double().reshape(1)]
+        if getattr(self, "_last_stats", None) is not None:
+            parts.append(self._last_stats.double())
+        host = torch.cat(parts).cpu().numpy()
         st = IterStats()
         n = int(host[0])
         st.episodes = n
@@ -234,14 +367,18 @@ class PPOTrainer:
         if len(host) > 8:
             (st.policy_loss, st.value_loss, st.entropy, st.old_approx_kl, st.approx_kl,
              st.clipfrac) = host[8:14].tolist()
-        st.learning_rate = self.optimizer.param_groups[0]["lr"]
+        st.learning_rate = float(self.optimizer.param_groups[0]["lr"])
         return st
 
     # ------------------------------------------------------------------ loop
     def anneal(self, iteration: int, num_iterations: int):
         if self.cfg.anneal_lr:
             frac = 1.0 - (iteration - 1.0) / num_iterations
-            self.optimizer.param_groups[0]["lr"] = frac * float(self.cfg.learning_rate)
+            lr = self.optimizer.param_groups[0]["lr"]
+            if torch.is_tensor(lr):
+                lr.fill_(frac * float(self.cfg.learning_rate))
+            else:
+                self.optimizer.param_groups[0]["lr"] = frac * float(self.cfg.learning_rate)
 
     def train_iteration(self, iteration: int, num_iterations: int) -> IterStats:
         self.anneal(iteration, num_iterations)

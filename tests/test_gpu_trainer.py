@@ -1,0 +1,94 @@
+"""The hipGraph-captured PPO update equals the eager update."""
+import os
+import sys
+from types import SimpleNamespace
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+sys.path.insert(0, os.path.dirname(__file__))
+
+
+def _cfg(**kw):
+    c = dict(num_steps=32, num_minibatches=4, update_epochs=3, learning_rate=3e-4, anneal_lr=True, gamma=0.99,
+             gae_lambda=0.95, norm_adv=True, clip_coef=0.1, clip_vloss=True, ent_coef=0.01, vf_coef=0.5,
+             max_grad_norm=0.5)
+    c.update(kw)
+    return SimpleNamespace(**c)
+
+
+def _make(graphs):
+    from fake_env import FakeVecEnv, torch_gae
+
+    from ppo_radiotherapy_amd.networks import PPO
+    from ppo_radiotherapy_amd.ppo import PPOTrainer
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    agent = PPO((9,), (6,), 64).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(5)
+    tr = PPOTrainer(_cfg(cuda_graphs=graphs), FakeVecEnv(256), agent, dev, generator=gen, gae_fn=torch_gae)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    for t in (tr.obs, tr.actions, tr.logprobs, tr.advantages, tr.returns, tr.values):
+        t.copy_(torch.randn(t.shape, generator=g))
+    return tr
+
+
+@pytest.mark.skipif(os.environ.get("AMD_SERIALIZE_KERNEL") != "3",
+                    reason="the autograd-captured hipGraph replays with a missing ordering edge on torch "
+                           "2.10/ROCm 7.0 (exact only with AMD_SERIALIZE_KERNEL=3); graphs are off by default")
+def test_graphed_update_matches_eager():
+    eager, graphed = _make(False), _make(True)
+    assert graphed.use_graphs and not eager.use_graphs
+    for it in (1, 2):
+        eager.anneal(it, 5)
+        graphed.anneal(it, 5)
+        n0, n1 = eager.update(), graphed.update()
+        assert n0 == n1 == 12
+    torch.cuda.synchronize()
+    for p, q in zip(eager.params, graphed.params):
+        torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(eager._last_stats, graphed._last_stats, rtol=1e-3, atol=1e-5)
+    assert float(graphed.optimizer.param_groups[0]["lr"]) == pytest.approx(3e-4 * 0.8)
+
+
+def test_eager_update_matches_float64_reference():
+    """The (default, eager) update vs a CPU float64 run of the same minibatches."""
+    from fake_env import FakeVecEnv, torch_gae
+
+    from ppo_radiotherapy_amd.networks import PPO
+    from ppo_radiotherapy_amd.ppo import PPOTrainer
+
+    e = _make(False)
+    rec = []
+    orig = torch.randperm
+
+    def rp(*a, **k):
+        out = orig(*a, **k)
+        rec.append(out.cpu())
+        return out
+
+    torch.randperm = rp
+    try:
+        e.update()
+        e.update()
+    finally:
+        torch.randperm = orig
+    torch.manual_seed(0)
+    c = PPOTrainer(_cfg(cuda_graphs=False), FakeVecEnv(256), PPO((9,), (6,), 64).double(), "cpu", gae_fn=torch_gae)
+    for tc, te in zip((c.obs, c.actions, c.logprobs, c.advantages, c.returns, c.values),
+                      (e.obs, e.actions, e.logprobs, e.advantages, e.returns, e.values)):
+        tc.data = te.detach().cpu().double()
+    c.optimizer = torch.optim.Adam(c.params, lr=3e-4, eps=1e-5)
+    it = iter(rec)
+    torch.randperm = lambda *a, **k: next(it)
+    try:
+        c.update()
+        c.update()
+    finally:
+        torch.randperm = orig
+    for p, q in zip(e.params, c.params):
+        torch.testing.assert_close(p.detach().cpu().double(), q.detach(), rtol=1e-4, atol=2e-6)

@@ -51,3 +51,19 @@ def test_sampling_statistics():
     ref = torch.distributions.Normal(mean, torch.ones_like(mean))
     torch.testing.assert_close(logp, ref.log_prob(a).sum(1), rtol=1e-6, atol=1e-5)
     torch.testing.assert_close(ent, ref.entropy().sum(1), rtol=1e-6, atol=1e-6)
+
+
+def test_splitk_linear_gradients_match_autograd():
+    from ppo_radiotherapy_amd import networks as N
+
+    torch.manual_seed(0)
+    lin = N.Linear(64, 64)
+    ref = torch.nn.Linear(64, 64)
+    ref.load_state_dict(lin.state_dict())
+    x = torch.randn(8192, 64, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    (lin(x) ** 2).sum().backward()
+    (ref(x2) ** 2).sum().backward()
+    torch.testing.assert_close(lin.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(lin.bias.grad, ref.bias.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-5, atol=1e-5)
