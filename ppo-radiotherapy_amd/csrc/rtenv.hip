@@ -624,6 +624,116 @@ __global__ __launch_bounds__(256) void k_dense(DenseParams P) {
     }
 }
 
+// Store 4 consecutive voxels [v0, v0+4) of one obs channel row.
+__device__ __forceinline__ void store4(float* row, int v0, int V, bool aligned4, float a, float b, float c,
+                                       float d) {
+    if (aligned4) {
+        *reinterpret_cast<float4*>(row + v0) = make_float4(a, b, c, d);
+    } else {
+        if (v0 < V) row[v0] = a;
+        if (v0 + 1 < V) row[v0 + 1] = b;
+        if (v0 + 2 < V) row[v0 + 2] = c;
+        if (v0 + 3 < V) row[v0 + 3] = d;
+    }
+}
+
+struct DenseVisParams {
+    DenseParams d;
+    float* obs;   // [N][4][V]
+};
+
+// ---------------------------------------------------------------------------
+// k_dense_vis: k_dense plus the dense channels of the vision observation
+// (environment.py:252-257, get_volumes): channel 0 = clip(lungs), channel 2 =
+// clip(dose) (dose is already in [0,1]); channels 1 (tumour) and 3 (beam view)
+// are zeroed here and scattered by k_finish.  Runs for every mode: STEP also
+// reduces, RESET zeroes the dose, NOOP (a reset call's unselected envs) only
+// re-emits the observation.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dense_vis(DenseVisParams PV) {
+    const DenseParams& P = PV.d;
+    const int sl = blockIdx.x, e = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int mode = P.st.setup[e].mode;
+    float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
+    const int nvec = P.G.Vpad >> 2;
+    const int V = P.G.V;
+    const bool al4 = (V & 3) == 0;
+    float* o0 = PV.obs + (size_t)e * 4 * V;
+    float* o1 = o0 + V;
+    float* o2 = o1 + V;
+    float* o3 = o2 + V;
+    const int q0 = sl * P.vec_per_slice;
+    const int q1 = min(q0 + P.vec_per_slice, nvec);
+    const uint32_t* lbits = P.lung_bits;
+    const float thr = P.lung_thr;
+    int cnt = 0;
+    double lsum = 0.0;
+    for (int q = q0 + tid; q < q1; q += kStepThreads) {
+        const int v0 = q << 2;
+        float4 v;
+        if (mode == MODE_RESET) {
+            v = make_float4(0.f, 0.f, 0.f, 0.f);
+            d4[q] = v;
+        } else {
+            v = d4[q];
+        }
+        const uint32_t lb = (lbits[q >> 3] >> ((q & 7) << 2)) & 0xFu;
+        if (v0 < V) {
+            store4(o0, v0, V, al4, (float)(lb & 1u), (float)((lb >> 1) & 1u), (float)((lb >> 2) & 1u),
+                   (float)((lb >> 3) & 1u));
+            store4(o1, v0, V, al4, 0.f, 0.f, 0.f, 0.f);
+            store4(o2, v0, V, al4, v.x, v.y, v.z, v.w);
+            store4(o3, v0, V, al4, 0.f, 0.f, 0.f, 0.f);
+        }
+        if (mode == MODE_STEP) {
+            float part = 0.0f;
+            LUNG_VOXEL(v.x, 0)
+            LUNG_VOXEL(v.y, 1)
+            LUNG_VOXEL(v.z, 2)
+            LUNG_VOXEL(v.w, 3)
+            lsum += (double)part;
+        }
+    }
+    if (mode != MODE_STEP) return;  // block-uniform
+    __shared__ int s_cnt[kStepThreads / 64];
+    __shared__ double s_sum[kStepThreads / 64];
+    cnt = wave_sum_i(cnt);
+    lsum = wave_sum_d(lsum);
+    if (lane == 0) {
+        s_cnt[wid] = cnt;
+        s_sum[wid] = lsum;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int c = 0;
+        double t = 0.0;
+        for (int w = 0; w < kStepThreads / 64; ++w) {
+            c += s_cnt[w];
+            t += s_sum[w];
+        }
+        P.part_cnt[(size_t)e * P.slices + sl] = c;
+        P.part_sum[(size_t)e * P.slices + sl] = t;
+    }
+}
+
+// LDS hash (flat voxel -> summed weight) for the beam-view channel.
+__device__ __forceinline__ uint32_t hslot(int32_t key, uint32_t mask) {
+    return ((uint32_t)key * 2654435761u >> 7) & mask;
+}
+
+__device__ __forceinline__ void hash_add(int32_t* keys, float* vals, uint32_t mask, int32_t key, float w) {
+    uint32_t h = hslot(key, mask);
+    while (true) {
+        const int32_t old = atomicCAS(&keys[h], -1, key);
+        if (old == -1 || old == key) {
+            atomicAdd(&vals[h], w);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
 struct FinishParams {
     Geom G;
     Consts C;
@@ -638,6 +748,9 @@ struct FinishParams {
     int32_t slices;
     int32_t max_tvox;    // per-wave LDS holds 2 * max_tvox floats
     int32_t N;
+    int32_t vision;      // obs is f32 [N][4][V]
+    uint32_t hash_mask;  // vision: beam-view hash slots - 1
+    int32_t wave_lds;    // bytes of LDS per wave
 };
 
 __device__ __forceinline__ void write_obs9(float* obs, const Geom& G, int e, const double* pose,
@@ -656,6 +769,73 @@ __device__ __forceinline__ void lds_wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Splats of one beam into the wave's LDS hash (lane k: iterations k, k+64, ...).
+__device__ void hash_beam(const Geom& G, const BeamSetup& b, int lane, int32_t* keys, float* vals,
+                          uint32_t mask) {
+    for (int k = lane; k < b.niter; k += 64) {
+        float y = b.intery0, z = b.interz0;
+        for (int j = 0; j < k; ++j) {  // the reference's sequential f32 accumulation
+            y = y + b.sgy;
+            z = z + b.sgz;
+        }
+        int32_t idx[4];
+        float w[4];
+        const int n = march_splats(G.g, b, k, y, z, idx, w);
+        for (int i = 0; i < n; ++i) hash_add(keys, vals, mask, idx[i], w[i]);
+    }
+}
+
+__device__ BeamSetup wave_beam_setup(const Geom& G, const double pos[3], const double dir[3], int lane) {
+    BeamSetup s{};
+    if (lane == 0) beam_setup(G.g, pos, dir, s);
+    BeamSetup b;
+    b.niter = rfl_i(s.niter);
+    b.start = rfl_i(s.start);
+    b.stepdir = rfl_i(s.stepdir);
+    b.dom = rfl_i(s.dom);
+    b.o0 = rfl_i(s.o0);
+    b.o1 = rfl_i(s.o1);
+    b.intery0 = rfl_f(s.intery0);
+    b.interz0 = rfl_f(s.interz0);
+    b.sgy = rfl_f(s.sgy);
+    b.sgz = rfl_f(s.sgz);
+    return b;
+}
+
+// Vision observation, sparse channels (environment.py:245-257): channel 1 =
+// clip(tumours) = 1 on the tumour voxels; channel 3 = clip(beam(pos, dir) +
+// beam(pos, [1,0,0])), built as the reference adds the two dense beams: the
+// first beam's splats are summed (pairs), THEN the horizontal beam is added.
+__device__ void vision_scatter(const FinishParams& P, int e, int lane, const double* pose, const TumourMeta& m,
+                               unsigned char* wave_lds) {
+    const int V = P.G.V;
+    float* row = P.obs + (size_t)e * 4 * V;
+    const int32_t* tv = P.lib.vox + m.vox_base;
+    for (int i = lane; i < m.n; i += 64) row[V + tv[i]] = 1.0f;
+    const uint32_t slots = P.hash_mask + 1;
+    int32_t* keys = reinterpret_cast<int32_t*>(wave_lds + (size_t)P.max_tvox * 2 * sizeof(float));
+    float* vals = reinterpret_cast<float*>(keys + slots);
+    for (uint32_t i = lane; i < slots; i += 64) {
+        keys[i] = -1;
+        vals[i] = 0.0f;
+    }
+    const double pos[3] = {pose[0], pose[1], pose[2]};
+    const double dir[3] = {pose[3], pose[4], pose[5]};
+    const double hdir[3] = {1.0, 0.0, 0.0};
+    const BeamSetup b1 = wave_beam_setup(P.G, pos, dir, lane);
+    const BeamSetup b2 = wave_beam_setup(P.G, pos, hdir, lane);
+    lds_wave_sync();
+    hash_beam(P.G, b1, lane, keys, vals, P.hash_mask);
+    lds_wave_sync();
+    hash_beam(P.G, b2, lane, keys, vals, P.hash_mask);
+    lds_wave_sync();
+    float* view = row + 3 * (size_t)V;
+    for (uint32_t i = lane; i < slots; i += 64) {
+        const int32_t k = keys[i];
+        if (k >= 0) view[k] = clip01(vals[i]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_finish: one wave per env (4 per block).
 //  - tumour voxels: gather the updated dose, lung-voxel threshold correction
@@ -669,14 +849,15 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int e = blockIdx.x * 4 + w;
     if (e >= P.N) return;
-    extern __shared__ __attribute__((aligned(16))) float fsm[];
-    float* tvals = fsm + (size_t)w * 2 * P.max_tvox;
+    extern __shared__ __attribute__((aligned(16))) unsigned char fsm_raw[];
+    unsigned char* wave_lds = fsm_raw + (size_t)w * P.wave_lds;
+    float* tvals = reinterpret_cast<float*>(wave_lds);
     const BeamSetup s = P.st.setup[e];
     const TumourMeta m = P.lib.meta[s.tumour];
     const double* pose = P.st.pose + (size_t)e * 6;
     if (s.mode != MODE_STEP) {
         if (lane == 0) {
-            write_obs9(P.obs, P.G, e, pose, m);
+            if (!P.vision) write_obs9(P.obs, P.G, e, pose, m);
             if (P.reward) P.reward[e] = 0.0f;
             if (P.terminated) P.terminated[e] = 0;
             if (P.info) {
@@ -684,6 +865,7 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
                 for (int i = 0; i < RT_INFO_W; ++i) inf[i] = 0.0f;
             }
         }
+        if (P.vision) vision_scatter(P, e, lane, pose, m, wave_lds);
         return;
     }
     const float* dose = P.st.dose + (size_t)e * P.G.Vpad;
@@ -755,7 +937,7 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
         const double total = ((double)r_tum + r_lung) + r_dist;
         const int t = P.st.t[e];
         const bool done = (ratio >= P.C.tum_thr) || (t >= P.C.max_t);
-        write_obs9(P.obs, P.G, e, pose, m);
+        if (!P.vision) write_obs9(P.obs, P.G, e, pose, m);
         P.reward[e] = (float)total;
         P.terminated[e] = done ? 1 : 0;
         const double ret = P.st.ep_return[e] + total;
@@ -783,6 +965,7 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
             inf[RT_INFO_EP_LENGTH] = (float)len;
         }
     }
+    if (P.vision) vision_scatter(P, e, lane, pose, m, wave_lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -959,6 +1142,8 @@ struct rt_env {
     int slices = 0;          // k_dense slices per env
     int vec_per_slice = 0;   // float4 per slice
     size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
+    int finish_wave_lds = 0; // bytes per wave
+    uint32_t view_hash_mask = 0;
     int32_t* part_cnt = nullptr;
     double* part_sum = nullptr;
     // optional live kernel timing: 4 events per step (before k_beam, k_dense,
@@ -1096,7 +1281,6 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     if (!cfg || !out) return fail(RT_EINVAL, "NULL argument");
     *out = nullptr;
     if (cfg->num_envs < 1) return fail(RT_EINVAL, "num_envs must be >= 1");
-    if (!cfg->visionless) return fail(RT_ELIMIT, "vision observations are not built into this library yet");
     if (!cfg->lungs_h || !cfg->tumour_voxels_h || !cfg->tumour_offsets_h || cfg->n_tumours < 1)
         return fail(RT_EINVAL, "lungs / tumour library missing");
     int ndev = 0;
@@ -1190,7 +1374,14 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     const int nvec = G.Vpad / 4;
     env->vec_per_slice = std::min(nvec, kSliceVec);
     env->slices = (nvec + env->vec_per_slice - 1) / env->vec_per_slice;
-    env->finish_smem = (size_t)4 * 2 * max_n * sizeof(float);
+    const int maxdim = std::max(G.g[0], std::max(G.g[1], G.g[2]));
+    env->view_hash_mask = env->visionless ? 0u : next_pow2((uint32_t)(8 * (maxdim + 2))) - 1;
+    size_t wave_bytes = (size_t)2 * max_n * sizeof(float);
+    if (!env->visionless) wave_bytes += (size_t)(env->view_hash_mask + 1) * 8;
+    wave_bytes = (wave_bytes + 15) / 16 * 16;
+    env->finish_wave_lds = (int)wave_bytes;
+    env->finish_smem = 4 * wave_bytes;
+    if (env->finish_smem > 160 * 1024) { free_env(env); return fail(RT_ELIMIT, "LDS budget exceeded"); }
 
     // ---- device allocations ----
     const int N = env->N;
@@ -1282,8 +1473,14 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     dp.slices = env->slices;
     dp.vec_per_slice = env->vec_per_slice;
     if (ev) (void)hipEventRecord(ev[1], stream);
-    hipLaunchKernelGGL(k_dense, dim3(env->slices, N), dim3(kStepThreads), 0, stream, dp);
-    RT_LAUNCH_CHECK("k_dense");
+    if (env->visionless) {
+        hipLaunchKernelGGL(k_dense, dim3(env->slices, N), dim3(kStepThreads), 0, stream, dp);
+        RT_LAUNCH_CHECK("k_dense");
+    } else {
+        DenseVisParams dv{dp, obs};
+        hipLaunchKernelGGL(k_dense_vis, dim3(env->slices, N), dim3(kStepThreads), 0, stream, dv);
+        RT_LAUNCH_CHECK("k_dense_vis");
+    }
     if (ev) (void)hipEventRecord(ev[2], stream);
     FinishParams fp{};
     fp.G = env->G;
@@ -1299,6 +1496,9 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     fp.slices = env->slices;
     fp.max_tvox = env->max_tvox;
     fp.N = N;
+    fp.vision = env->visionless ? 0 : 1;
+    fp.hash_mask = env->view_hash_mask;
+    fp.wave_lds = env->finish_wave_lds;
     hipLaunchKernelGGL(k_finish, dim3((N + 3) / 4), dim3(256), env->finish_smem, stream, fp);
     RT_LAUNCH_CHECK("k_finish");
     if (ev) (void)hipEventRecord(ev[3], stream);

@@ -37,8 +37,6 @@ class RadiotherapyVecEnv:
 
     def __init__(self, num_envs: int, visionless: bool = True, grid=None, device=None, seed: int = 0,
                  library: TumourLibrary | None = None, env_id_base: int = 0):
-        if not visionless:
-            raise NotImplementedError("vision observations (4-channel volumes) are not built yet")
         if not torch.cuda.is_available():
             raise _lib.RtError("RadiotherapyVecEnv needs a HIP device (MI355X); no CPU fallback")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
