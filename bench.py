@@ -58,14 +58,26 @@ def parse():
     ap.add_argument("--no-update", action="store_true")
     ap.add_argument("--env-only", action="store_true", help="time rt_env_step alone (profiling)")
     ap.add_argument("--seed", type=int, default=1)
-    return ap.parse_args()
+    ap.add_argument("--vision", action="store_true",
+                    help="BASELINE configs[3]: C3D policy on 4-channel volume observations (512 envs, 64^3)")
+    ap.add_argument("--micro-batch", type=int, default=0)
+    ap.add_argument("--update-minibatches", type=int, default=0,
+                    help="time only this many minibatch steps of the update (0 = all)")
+    a = ap.parse_args()
+    if a.vision:
+        # 512 envs, 64^3, num_steps 16, vision.yaml minibatching
+        for k, v in dict(envs=512, num_steps=16, num_minibatches=2, micro_batch=128, update_minibatches=2).items():
+            if getattr(a, k) == ap.get_default(k):
+                setattr(a, k, v)
+    return a
 
 
 def trainer_cfg(a):
     # configs/default.yaml keys; C2 rollout/update shape
     return SimpleNamespace(num_steps=a.num_steps, num_minibatches=a.num_minibatches, update_epochs=a.update_epochs,
                            learning_rate=3e-4, anneal_lr=False, gamma=0.99, gae_lambda=0.95, norm_adv=True,
-                           clip_coef=0.1, clip_vloss=True, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5)
+                           clip_coef=0.1, clip_vloss=True, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
+                           micro_batch=a.micro_batch)
 
 
 def cpu_baseline(lib, seconds: float):
@@ -120,7 +132,7 @@ def main():
 
     import _rtpkg  # noqa: F401
     from ppo_radiotherapy_amd import assets
-    from ppo_radiotherapy_amd.networks import PPO
+    from ppo_radiotherapy_amd.networks import PPO, PPO_3DCNN
     from ppo_radiotherapy_amd.ppo import PPOTrainer, broadcast_parameters
     from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
 
@@ -142,10 +154,13 @@ def main():
 
     grid = (a.grid,) * 3
     lib = assets.synthetic_library(grid, 1000, 0)
-    env = RadiotherapyVecEnv(a.envs, visionless=True, library=lib, device=dev, seed=a.seed + rank,
+    env = RadiotherapyVecEnv(a.envs, visionless=not a.vision, library=lib, device=dev, seed=a.seed + rank,
                              env_id_base=rank * a.envs)
     torch.manual_seed(a.seed)
-    agent = PPO((9,), (6,), 64).to(dev)
+    if a.vision:
+        agent = PPO_3DCNN((4, *grid), (6,), 64).to(dev)
+    else:
+        agent = PPO((9,), (6,), 64).to(dev)
     broadcast_parameters(agent)
     gen = torch.Generator(device=dev)
     gen.manual_seed(a.seed * 1000 + rank)
@@ -157,6 +172,8 @@ def main():
     # ---------------- warmup
     for i in range(a.warmup):
         tr.rollout_step(i % T)
+    if a.update_minibatches:
+        tr.max_minibatches = a.update_minibatches
     if not a.no_update and not a.env_only:
         tr.compute_gae()
         tr.update()
@@ -208,7 +225,7 @@ def main():
         barrier()
         di = max_over_ranks(time.perf_counter() - t0)
         upd = {"ppo_updates_per_s": n_upd / du, "ppo_update_ms": 1000 * du / n_upd,
-               "minibatch_size_per_gpu": tr.minibatch_size,
+               "minibatch_size_per_gpu": tr.minibatch_size, "update_minibatches_timed": n_upd,
                "train_env_steps_per_s": total_envs * T / di, "train_iteration_s": di}
 
     # ---------------- roofline of the dominant kernel, k_dense
@@ -225,11 +242,15 @@ def main():
             "survey_model_bytes_per_env_step": 8 * V,
             "survey_model_frac": a.envs * 8 * V / (env_ms * 1e-3) / HBM_PEAK}
 
+    if a.vision:
+        roof["mfma_note"] = "C3D convolutions run in MIOpen (f32); the env roofline above is k_dense_vis"
     out = {"metric": METRIC, "value": steps_per_s, "unit": "env steps/s", "n_gpus": world, "steps": K,
            "warmup": a.warmup, "ms_per_step": 1000 * dt / K, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-           "config": {"workload": f"visionless MLP, {a.envs} envs/GPU, {a.grid}^3 voxel grid "
-                                  f"(BASELINE configs[{1 if world == 1 else 2}])" + (" env-only" if a.env_only else ""),
+           "config": {"workload": (f"vision C3D, {a.envs} envs/GPU, {a.grid}^3 voxel grid (BASELINE configs[3])"
+                                   if a.vision else
+                                   f"visionless MLP, {a.envs} envs/GPU, {a.grid}^3 voxel grid "
+                                   f"(BASELINE configs[{1 if world == 1 else 2}])") + (" env-only" if a.env_only else ""),
                       "envs_per_gpu": a.envs, "global_envs": total_envs, "grid": list(grid),
                       "num_steps": T, "num_minibatches": a.num_minibatches, "update_epochs": a.update_epochs,
                       "parallelism": f"dp{world}"},

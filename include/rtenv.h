@@ -69,6 +69,15 @@ enum {
 
 typedef struct rt_env rt_env; /* opaque */
 
+/* rt_env_config.step_mode */
+enum {
+    RT_STEP_DENSE = 0,       /* the reference's formulation: every step re-reduces each env's
+                                whole dose volume (k_dense, HBM-bound) */
+    RT_STEP_INCREMENTAL = 1  /* visionless only: the lung over-threshold count and lung dose sum
+                                are updated on the voxels the beam touches;
+                                rewards and termination identical, doses.lung within f64 rounding */
+};
+
 typedef struct {
     /* geometry */
     int32_t grid[3];          /* D, H, W (LUNG_SHAPE, environment.py:30) */
@@ -93,6 +102,7 @@ typedef struct {
     /* RNG for tumour sampling on autoreset (np.random.choice, environment.py:90) */
     uint64_t seed;
     int64_t env_id_base;      /* global id of env 0 of this handle (rank * N) */
+    int32_t step_mode;        /* RT_STEP_DENSE (default) or RT_STEP_INCREMENTAL */
 } rt_env_config;
 
 int rt_env_config_default(rt_env_config* cfg);

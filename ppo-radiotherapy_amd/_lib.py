@@ -21,6 +21,7 @@ INFO_NAMES = {
     "ep_return": 18, "ep_length": 19,
 }
 INFO_W = 20
+STEP_DENSE, STEP_INCREMENTAL = 0, 1
 
 RT_ERRORS = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EDEVICE", -4: "RT_ELAUNCH", -5: "RT_ELIMIT"}
 
@@ -58,6 +59,7 @@ class RtEnvConfig(ctypes.Structure):
         ("tumour_offsets_h", ctypes.c_void_p),
         ("seed", ctypes.c_uint64),
         ("env_id_base", ctypes.c_int64),
+        ("step_mode", ctypes.c_int32),
     ]
 
 

@@ -122,6 +122,8 @@ struct EnvState {
     int32_t* ep_len;
     int32_t* next_tumour;
     BeamSetup* setup;
+    int32_t* lung_cnt;    // incremental mode: # lung voxels with dose > threshold
+    double* lung_sum;     // incremental mode: sum of dose over lung voxels
 };
 
 struct Library {
@@ -375,6 +377,7 @@ struct BeamParams {
     const int32_t* reset_ids;     // RESET call: NULL = sample
     int32_t N;
     int32_t is_reset_call;
+    int32_t incremental;          // RT_STEP_INCREMENTAL (visionless only)
     uint64_t seed;
     int64_t env_id_base;
 };
@@ -470,7 +473,19 @@ __global__ __launch_bounds__(256) void k_beam(BeamParams P) {
         s = pose_step(P, e);
         P.st.setup[e] = s;
     }
-    if (rfl_i(s.mode) != MODE_STEP) return;
+    const int mode = rfl_i(s.mode);
+    if (P.incremental && mode == MODE_RESET) {
+        // reset_dose (environment.py:104) for the incremental step: k_dense is not run
+        float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
+        const int nvec = P.G.Vpad >> 2;
+        for (int q = lane; q < nvec; q += 64) d4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane == 0) {
+            P.st.lung_cnt[e] = 0;
+            P.st.lung_sum[e] = 0.0;
+        }
+        return;
+    }
+    if (mode != MODE_STEP) return;
     BeamSetup b;
     b.niter = rfl_i(s.niter);
     b.start = rfl_i(s.start);
@@ -483,11 +498,15 @@ __global__ __launch_bounds__(256) void k_beam(BeamParams P) {
     b.sgy = rfl_f(s.sgy);
     b.sgz = rfl_f(s.sgz);
     const int niter = b.niter;
-    if (niter <= 0) return;
+    if (niter <= 0) return;  // (incremental counters unchanged: the beam missed the box)
     float* dose = P.st.dose + (size_t)e * P.G.Vpad;
     const float bd = P.C.beam_dose;
     const bool pairs = b.dom != 0;
     // running march state: (ya, za) = iteration max(k-1, 0)
+    const uint32_t* lbits = P.lib.lung_bits;
+    const float thr = P.C.lung_thr;
+    int dcnt = 0;       // incremental: change of the lung over-threshold count
+    double dsum = 0.0;  // incremental: change of the lung dose sum
     float ya = b.intery0, za = b.interz0;
     int k = lane;
     for (int j = 0; j < k - 1; ++j) {
@@ -514,13 +533,30 @@ __global__ __launch_bounds__(256) void k_beam(BeamParams P) {
             float w = cw[i];
             for (int j = 0; j < nn; ++j)
                 if (ni[j] == v) w = w + nw[j];
-            dose[v] = clip01(dose[v] + w * bd);
+            const float old_d = dose[v];
+            const float new_d = clip01(old_d + w * bd);
+            dose[v] = new_d;
+            if (P.incremental && ((lbits[v >> 5] >> (v & 31)) & 1u)) {
+                dcnt += (new_d > thr ? 1 : 0) - (old_d > thr ? 1 : 0);
+                dsum += (double)new_d - (double)old_d;
+            }
         }
         // advance (ya, za) to iteration k + 63
         const int adds = k == 0 ? 63 : 64;
         for (int j = 0; j < adds; ++j) {
             ya = ya + b.sgy;
             za = za + b.sgz;
+        }
+    }
+    if (P.incremental) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            dcnt += __shfl_xor(dcnt, off, 64);
+            dsum += __shfl_xor(dsum, off, 64);
+        }
+        if (lane == 0) {
+            P.st.lung_cnt[e] += dcnt;
+            P.st.lung_sum[e] += dsum;
         }
     }
 }
@@ -749,6 +785,7 @@ struct FinishParams {
     int32_t max_tvox;    // per-wave LDS holds 2 * max_tvox floats
     int32_t N;
     int32_t vision;      // obs is f32 [N][4][V]
+    int32_t incremental; // lung count / sum from the k_beam-maintained counters
     uint32_t hash_mask;  // vision: beam-view hash slots - 1
     int32_t wave_lds;    // bytes of LDS per wave
 };
@@ -918,12 +955,17 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
     }
     int cnt = 0;
     double dl = 0.0;
-    for (int j = lane; j < P.slices; j += 64) {
-        cnt += P.part_cnt[(size_t)e * P.slices + j];
-        dl += P.part_sum[(size_t)e * P.slices + j];
+    if (P.incremental) {
+        cnt = P.st.lung_cnt[e];
+        dl = P.st.lung_sum[e];
+    } else {
+        for (int j = lane; j < P.slices; j += 64) {
+            cnt += P.part_cnt[(size_t)e * P.slices + j];
+            dl += P.part_sum[(size_t)e * P.slices + j];
+        }
+        cnt = wave_sum_i(cnt);
+        dl = wave_sum_d(dl);
     }
-    cnt = wave_sum_i(cnt);
-    dl = wave_sum_d(dl);
     if (lane == 0) {
         const long long c = (long long)cnt - ctum;  // lungs * (1 - tumours)
         const float S = m.result >= 0 ? tvals[m.result] : 0.0f;
@@ -1136,6 +1178,7 @@ struct rt_env {
     uint64_t seed = 0;
     int64_t env_id_base = 0;
     int visionless = 1;
+    int incremental = 0;
     EnvState st{};
     Library lib{};
     int max_tvox = 0;
@@ -1294,6 +1337,11 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     env->seed = cfg->seed;
     env->env_id_base = cfg->env_id_base;
     env->visionless = cfg->visionless;
+    if (cfg->step_mode != RT_STEP_DENSE && cfg->step_mode != RT_STEP_INCREMENTAL) {
+        delete env;
+        return fail(RT_EINVAL, "unknown step_mode");
+    }
+    env->incremental = (cfg->step_mode == RT_STEP_INCREMENTAL && cfg->visionless) ? 1 : 0;
     int rc = fill_geom(cfg->grid, env->G);
     if (rc) { free_env(env); return rc; }
     env->C = make_consts(*cfg);
@@ -1399,7 +1447,8 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         (rc = dev_alloc(env, &st.ep_return, N)) || (rc = dev_alloc(env, &st.ep_len, N)) ||
         (rc = dev_alloc(env, &st.next_tumour, N)) || (rc = dev_alloc(env, &st.setup, N)) ||
         (rc = dev_alloc(env, &env->part_cnt, (size_t)N * env->slices)) ||
-        (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices))) {
+        (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices)) ||
+        (rc = dev_alloc(env, &st.lung_cnt, N)) || (rc = dev_alloc(env, &st.lung_sum, N))) {
         free_env(env);
         return rc;
     }
@@ -1419,6 +1468,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         hipMemset(st.dose, 0, (size_t)N * G.Vpad * 4) || hipMemset(st.t, 0, N * 4) ||
         hipMemset(st.tumour, 0, N * 4) || hipMemset(st.episode, 0, N * 4) ||
         hipMemset(st.ep_return, 0, N * 8) || hipMemset(st.ep_len, 0, N * 4) ||
+        hipMemset(st.lung_cnt, 0, N * 4) || hipMemset(st.lung_sum, 0, N * 8) ||
         hipMemset(st.setup, 0, (size_t)N * sizeof(BeamSetup)) || hipDeviceSynchronize()) {
         free_env(env);
         return fail(RT_EDEVICE, "initial upload failed");
@@ -1459,6 +1509,7 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     bp.reset_ids = ids;
     bp.N = N;
     bp.is_reset_call = reset_call ? 1 : 0;
+    bp.incremental = env->incremental;
     bp.seed = env->seed;
     bp.env_id_base = env->env_id_base;
     hipLaunchKernelGGL(k_beam, dim3((N + 3) / 4), dim3(256), 0, stream, bp);
@@ -1473,7 +1524,9 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     dp.slices = env->slices;
     dp.vec_per_slice = env->vec_per_slice;
     if (ev) (void)hipEventRecord(ev[1], stream);
-    if (env->visionless) {
+    if (env->incremental) {
+        // no dense pass: k_beam maintains the lung count and sum
+    } else if (env->visionless) {
         hipLaunchKernelGGL(k_dense, dim3(env->slices, N), dim3(kStepThreads), 0, stream, dp);
         RT_LAUNCH_CHECK("k_dense");
     } else {
@@ -1497,6 +1550,7 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     fp.max_tvox = env->max_tvox;
     fp.N = N;
     fp.vision = env->visionless ? 0 : 1;
+    fp.incremental = env->incremental;
     fp.hash_mask = env->view_hash_mask;
     fp.wave_lds = env->finish_wave_lds;
     hipLaunchKernelGGL(k_finish, dim3((N + 3) / 4), dim3(256), env->finish_smem, stream, fp);

@@ -100,6 +100,7 @@ class PPOTrainer:
         lr = torch.tensor(float(cfg.learning_rate), device=self.device) if self.use_graphs else float(cfg.learning_rate)
         self.optimizer = torch.optim.Adam(self.params, lr=lr, eps=1e-5,
                                           foreach=self.device.type == "cuda", capturable=self.use_graphs)
+        self.max_minibatches = 0  # >0: stop the update after this many minibatch steps (benchmarks)
         self.next_obs = None
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
@@ -185,7 +186,27 @@ class PPOTrainer:
 
     def _minibatch_loss_backward(self, mb, adv_mean=None, adv_std=None):
         """train.py:200-246 for one minibatch: losses, then backward into the
-        flat gradient bucket.  Returns the logged statistics."""
+        flat gradient bucket.  Returns the logged statistics.  With
+        cfg.micro_batch set (vision: C3D activations of a whole minibatch do not
+        fit), the minibatch is processed in slices whose gradients accumulate;
+        each slice's loss is weighted by its share, so the gradient equals the
+        full-minibatch one (advantage statistics are those of the minibatch)."""
+        micro = int(getattr(self.cfg, "micro_batch", 0) or 0)
+        if micro and mb.numel() > micro:
+            if self.cfg.norm_adv and adv_mean is None:
+                a = self._b_adv[mb]
+                adv_mean, adv_std = a.mean(), a.std()
+            self.flat_grad.zero_()
+            acc = None
+            n = mb.numel()
+            for s in range(0, n, micro):
+                part = mb[s:s + micro]
+                st = self._loss_backward(part, adv_mean, adv_std, weight=part.numel() / n, zero=False)
+                acc = st * (part.numel() / n) if acc is None else acc + st * (part.numel() / n)
+            return acc
+        return self._loss_backward(mb, adv_mean, adv_std)
+
+    def _loss_backward(self, mb, adv_mean=None, adv_std=None, weight: float = 1.0, zero: bool = True):
         cfg = self.cfg
         clip = float(cfg.clip_coef)
         _, newlogprob, entropy, newvalue = self.agent.get_action_and_value(self._b_obs[mb], self._b_actions[mb])
@@ -212,8 +233,9 @@ class PPOTrainer:
             v_loss = 0.5 * ((newvalue - b_ret) ** 2).mean()
         entropy_loss = entropy.mean()
         loss = pg_loss - float(cfg.ent_coef) * entropy_loss + v_loss * float(cfg.vf_coef)
-        self.flat_grad.zero_()
-        loss.backward()
+        if zero:
+            self.flat_grad.zero_()
+        (loss * weight if weight != 1.0 else loss).backward()
         return torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,
                             approx_kl, clipfrac])
 
@@ -246,6 +268,10 @@ class PPOTrainer:
                 self._allreduce_(self.flat_grad)
                 self._optimizer_step()
                 n_mb += 1
+                if self.max_minibatches and n_mb >= self.max_minibatches:
+                    break
+            if self.max_minibatches and n_mb >= self.max_minibatches:
+                break
         self._last_stats = torch.cat([st[:5], (stats_sum[5] / max(n_mb, 1)).reshape(1)])
         return n_mb
 

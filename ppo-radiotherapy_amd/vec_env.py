@@ -36,7 +36,10 @@ class RadiotherapyVecEnv:
     metadata = {"render_modes": ["human"], "render_fps": 30, "autoreset_mode": "NextStep"}
 
     def __init__(self, num_envs: int, visionless: bool = True, grid=None, device=None, seed: int = 0,
-                 library: TumourLibrary | None = None, env_id_base: int = 0):
+                 library: TumourLibrary | None = None, env_id_base: int = 0, step_mode: str = "dense"):
+        """step_mode: "dense" (the reference's full-volume reductions every
+        step) or "incremental" (visionless: maintained on the touched voxels;
+        same rewards/termination)."""
         if not torch.cuda.is_available():
             raise _lib.RtError("RadiotherapyVecEnv needs a HIP device (MI355X); no CPU fallback")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -69,6 +72,10 @@ class RadiotherapyVecEnv:
         cfg.tumour_offsets_h = self._off.ctypes.data
         cfg.seed = self._seed & 0xFFFFFFFFFFFFFFFF
         cfg.env_id_base = int(env_id_base)
+        if step_mode not in ("dense", "incremental"):
+            raise ValueError("step_mode must be 'dense' or 'incremental'")
+        self.step_mode = step_mode if visionless else "dense"
+        cfg.step_mode = _lib.STEP_INCREMENTAL if self.step_mode == "incremental" else _lib.STEP_DENSE
         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         handle = ctypes_void_p()
         with torch.cuda.device(dev_index):

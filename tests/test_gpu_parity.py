@@ -25,10 +25,13 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _vec_env(n, library, seed=0):
+def _vec_env(n, library, seed=0, step_mode="dense"):
     from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
 
-    return RadiotherapyVecEnv(n, visionless=True, library=library, seed=seed)
+    return RadiotherapyVecEnv(n, visionless=True, library=library, seed=seed, step_mode=step_mode)
+
+
+MODES = ["dense", "incremental"]
 
 
 # ----------------------------------------------------------------- beams
@@ -107,9 +110,9 @@ def _run_pose(L, dev, grid, pos, dirs, act):
 
 
 # ----------------------------------------------------------------- env trajectories
-def _replay(z, lib, tol=1e-5):
+def _replay(z, lib, tol=1e-5, step_mode="dense"):
     n_eps = len(z["tumour_id"])
-    env = _vec_env(n_eps, lib)
+    env = _vec_env(n_eps, lib, step_mode=step_mode)
     obs, _ = env.reset(options={"tumour_ids": z["tumour_id"].astype(np.int32)})
     np.testing.assert_array_equal(obs.cpu().numpy(), z["obs0"].astype(np.float32))
     lens = z["ep_len"]
@@ -148,12 +151,14 @@ def _replay(z, lib, tol=1e-5):
     return worst
 
 
-def test_env_trajectories_reference_grid(golden, dev):
-    _replay(golden("env_traj_ref.npz"), assets.reference_library())
+@pytest.mark.parametrize("mode", MODES)
+def test_env_trajectories_reference_grid(golden, dev, mode):
+    _replay(golden("env_traj_ref.npz"), assets.reference_library(), step_mode=mode)
 
 
-def test_env_trajectories_64(golden, dev):
-    _replay(golden("env_traj_64.npz"), assets.synthetic_library((64, 64, 64), 64, 0))
+@pytest.mark.parametrize("mode", MODES)
+def test_env_trajectories_64(golden, dev, mode):
+    _replay(golden("env_traj_64.npz"), assets.synthetic_library((64, 64, 64), 64, 0), step_mode=mode)
 
 
 def _custom_library(shape, lungs, tumours):
@@ -163,7 +168,8 @@ def _custom_library(shape, lungs, tumours):
                                 voxels=np.concatenate(vox), offsets=off)
 
 
-def test_termination_and_autoreset(golden, dev):
+@pytest.mark.parametrize("mode", MODES)
+def test_termination_and_autoreset(golden, dev, mode):
     """Episodes ending by irradiation (environment.py:184-191,220) followed by
     gymnasium NEXT_STEP autoreset and RecordEpisodeStatistics."""
     z = golden("env_done_ref.npz")
@@ -174,7 +180,7 @@ def test_termination_and_autoreset(golden, dev):
         tumours.append(vv)
     lib = _custom_library(ref.shape, ref.lungs, tumours)
     E = len(tumours)
-    env = _vec_env(E, lib)
+    env = _vec_env(E, lib, step_mode=mode)
     env.reset(options={"tumour_ids": np.arange(E, dtype=np.int32)})
     acts = torch.tensor(z["actions"], dtype=torch.float32, device=env.device)
     ret = np.zeros(E)
@@ -263,3 +269,26 @@ def test_gae_matches_torch_loop(dev):
                         gamma, lam, adv.data_ptr(), ret.data_ptr(), None), "rt_gae")
     torch.testing.assert_close(adv, adv_ref, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(ret, ret_ref, rtol=1e-6, atol=1e-6)
+
+
+def test_incremental_equals_dense_over_resets(dev):
+    """4096 envs at 64^3 for 230 steps (>= 2 episodes each, Philox tumour draws):
+    the incremental step gives bitwise the same rewards, termination and dose
+    as the dense step; doses.lung within f32 rounding."""
+    lib = assets.synthetic_library((64, 64, 64), 1000, 0)
+    N = 4096
+    d = _vec_env(N, lib, seed=11, step_mode="dense")
+    i = _vec_env(N, lib, seed=11, step_mode="incremental")
+    d.reset()
+    i.reset()
+    g = torch.Generator(device=d.device).manual_seed(0)
+    for t in range(230):
+        a = torch.rand((N, 6), device=d.device, generator=g) * 2.4 - 1.2
+        od, rd, td, _, infd = d.step(a)
+        oi, ri, ti, _, infi = i.step(a)
+        assert torch.equal(rd, ri) and torch.equal(td, ti) and torch.equal(od, oi), t
+        assert torch.equal(infd["reward_components"]["lung"], infi["reward_components"]["lung"])
+        torch.testing.assert_close(infi["doses"]["lung"], infd["doses"]["lung"], rtol=2e-6, atol=1e-6)
+    assert torch.equal(d.dose(), i.dose())
+    d.close()
+    i.close()

@@ -122,3 +122,17 @@ def test_data_parallel_gloo_world2():
     np.testing.assert_array_equal(g0, g1)
     np.testing.assert_array_equal(p0, p1)  # replicas stay identical through the update
     assert e0 < 1e-5 and e1 < 1e-5
+
+
+def test_micro_batched_gradient_equals_full_minibatch():
+    tr = _trainer(16, 0)
+    tr.rollout()
+    tr.compute_gae()
+    tr._bind_batch()
+    mb = torch.randperm(tr.batch_size)[:64]
+    full = tr._minibatch_loss_backward(mb)
+    g_full = tr.flat_grad.clone()
+    tr.cfg.micro_batch = 24  # uneven slices 24 + 24 + 16
+    part = tr._minibatch_loss_backward(mb)
+    torch.testing.assert_close(tr.flat_grad, g_full, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(part[[0, 1, 2]], full[[0, 1, 2]], rtol=1e-5, atol=1e-6)
