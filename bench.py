@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--vision", action="store_true",
                     help="BASELINE configs[3]: C3D policy on 4-channel volume observations (512 envs, 64^3)")
     ap.add_argument("--micro-batch", type=int, default=0)
+    ap.add_argument("--step-mode", choices=["dense", "incremental"], default="dense",
+                    help="env step formulation measured as `value` (the other is reported beside it)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
     a = ap.parse_args()
@@ -155,7 +157,7 @@ def main():
     grid = (a.grid,) * 3
     lib = assets.synthetic_library(grid, 1000, 0)
     env = RadiotherapyVecEnv(a.envs, visionless=not a.vision, library=lib, device=dev, seed=a.seed + rank,
-                             env_id_base=rank * a.envs)
+                             env_id_base=rank * a.envs, step_mode=a.step_mode)
     torch.manual_seed(a.seed)
     if a.vision:
         agent = PPO_3DCNN((4, *grid), (6,), 64).to(dev)
@@ -242,6 +244,32 @@ def main():
             "survey_model_bytes_per_env_step": 8 * V,
             "survey_model_frac": a.envs * 8 * V / (env_ms * 1e-3) / HBM_PEAK}
 
+    # ---------------- the other step formulation, same workload (policy in the loop)
+    other = None
+    if not a.vision and not a.env_only:
+        other_mode = "incremental" if a.step_mode == "dense" else "dense"
+        env.close()
+        env2 = RadiotherapyVecEnv(a.envs, visionless=True, library=lib, device=dev, seed=a.seed + rank,
+                                  env_id_base=rank * a.envs, step_mode=other_mode)
+        tr.env = env2
+        tr.reset()
+        for i in range(a.warmup):
+            tr.rollout_step(i % T)
+        env2.kernel_timing(K)
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(K):
+            tr.rollout_step(i % T)
+        torch.cuda.synchronize()
+        barrier()
+        d2 = max_over_ranks(time.perf_counter() - t0)
+        k2, _ = env2.kernel_timing_read()
+        env2.kernel_timing(0)
+        env_ms2 = sum(max_over_ranks(v) for v in k2.values())
+        other = {"step_mode": other_mode, "env_steps_per_s": total_envs * K / d2, "ms_per_step": 1000 * d2 / K,
+                 "env_kernels_ms": k2, "env_only_kernel_steps_per_s": total_envs / (env_ms2 * 1e-3)}
+        env = env2
     if a.vision:
         roof["mfma_note"] = "C3D convolutions run in MIOpen (f32); the env roofline above is k_dense_vis"
     out = {"metric": METRIC, "value": steps_per_s, "unit": "env steps/s", "n_gpus": world, "steps": K,
@@ -256,6 +284,9 @@ def main():
                       "parallelism": f"dp{world}"},
            "env_only_kernel_steps_per_s": total_envs / (env_ms * 1e-3)}
     out.update(upd)
+    out["step_mode"] = a.step_mode
+    if other is not None:
+        out["other_step_mode"] = other
     out["roofline"] = roof
     if rank == 0 and world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(lib, a.cpu_seconds)

@@ -166,6 +166,18 @@ int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h);
  * the sorted flat indices idx_h (no device needed; parity hook). */
 int rt_host_tumour_sum(int64_t V, int32_t n, const int32_t* idx_h, const float* vals_h, float* out_h);
 
+/* Fused rollout policy step of the visionless agent (networks.py PPO,
+ * feature_dim 64): for every env, obs -> actor/critic MLPs -> Gaussian sample
+ * (Philox; key seed, counter `counter`, env id env_id_base + e) -> action,
+ * log_prob(action).sum, value; also copies obs and done (u8 -> f32; NULL = 0)
+ * into the rollout storage slices.  params_d: the 13 f32 parameter tensors
+ * in the order actor_mean.{0,2,4}.{weight,bias}, actor_logstd,
+ * critic.{0,2,4}.{weight,bias}.  Replaces train.py:143-149 per step. */
+int rt_policy_sample(const float* const* params_d, int32_t n_params_tensors, int32_t n_envs,
+                     const float* obs_d, const uint8_t* done_d, float* obs_out_d, float* done_out_d,
+                     float* act_out_d, float* logp_out_d, float* value_out_d, uint64_t seed,
+                     uint64_t counter, int64_t env_id_base, void* stream);
+
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */
 int rt_gae(int32_t T, int32_t N, const float* rewards_d, const float* values_d,

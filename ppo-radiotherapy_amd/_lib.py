@@ -30,7 +30,7 @@ EXPORTS = [
     "rt_env_config_default", "rt_env_create", "rt_env_destroy", "rt_env_reset", "rt_env_step",
     "rt_env_set_next_tumours", "rt_env_dose", "rt_env_get_state", "rt_env_set_pose", "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
-    "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_gae", "rt_last_error", "rt_abi_version",
+    "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae", "rt_last_error", "rt_abi_version",
 ]
 
 
@@ -103,6 +103,8 @@ def load(build_if_missing: bool = True):
         "rt_host_sincos": ([i32, vp, vp, vp], ctypes.c_int),
         "rt_host_tumour_sum": ([i64, i32, vp, vp, vp], ctypes.c_int),
         "rt_gae": ([i32, i32, vp, vp, vp, vp, vp, f64, f64, vp, vp, vp], ctypes.c_int),
+        "rt_policy_sample": ([ctypes.POINTER(vp), i32, i32, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint64,
+                              ctypes.c_uint64, i64, vp], ctypes.c_int),
         "rt_last_error": ([], ctypes.c_char_p),
         "rt_abi_version": ([], ctypes.c_int),
     }

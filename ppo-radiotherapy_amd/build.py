@@ -13,6 +13,7 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "rtenv.hip")
+SRCS = [SRC, os.path.join(PKG, "csrc", "policy.hip")]
 HDR = os.path.join(REPO, "include", "rtenv.h")
 OUT = os.path.join(PKG, "librtenv.so")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
@@ -36,14 +37,14 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = (SRC, HDR, os.path.join(PKG, "csrc", "rt_ddmath.h"), __file__)
+    deps = (*SRCS, HDR, os.path.join(PKG, "csrc", "rt_ddmath.h"), __file__)
     return any(os.path.getmtime(p) > t for p in deps)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return OUT
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), SRC, "-o", OUT + ".tmp"]
+    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), *SRCS, "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

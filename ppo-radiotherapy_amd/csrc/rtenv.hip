@@ -1266,6 +1266,9 @@ extern "C" {
 
 int rt_abi_version(void) { return RTENV_ABI_VERSION; }
 
+// shared error reporting for the other translation units of the library
+int rt_internal_fail(int code, const char* msg) { return fail(code, msg); }
+
 int rt_host_tumour_sum(int64_t V, int32_t n, const int32_t* idx_h, const float* vals_h, float* out_h) {
     if (V < 1 || n < 0 || !out_h || (n && (!idx_h || !vals_h))) return fail(RT_EINVAL, "bad argument");
     for (int32_t i = 0; i < n; ++i)

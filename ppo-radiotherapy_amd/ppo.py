@@ -101,20 +101,69 @@ class PPOTrainer:
         self.optimizer = torch.optim.Adam(self.params, lr=lr, eps=1e-5,
                                           foreach=self.device.type == "cuda", capturable=self.use_graphs)
         self.max_minibatches = 0  # >0: stop the update after this many minibatch steps (benchmarks)
+        # fused rollout policy step (rt_policy_sample): the visionless 64-wide
+        # MLP agent on the HIP env; otherwise the torch path below
+        self.fused_policy = (bool(getattr(cfg, "fused_policy", True)) and self.device.type == "cuda"
+                             and self._fusable(agent, env))
+        self._policy_counter = 0
+        self._policy_seed = int(getattr(cfg, "seed", 0)) * 1_000_003 + 7919 * rank + 1
+        self._done_valid = False
+        if self.fused_policy:
+            import ctypes
+
+            order = ["actor_mean.0.weight", "actor_mean.0.bias", "actor_mean.2.weight", "actor_mean.2.bias",
+                     "actor_mean.4.weight", "actor_mean.4.bias", "actor_logstd", "critic.0.weight", "critic.0.bias",
+                     "critic.2.weight", "critic.2.bias", "critic.4.weight", "critic.4.bias"]
+            named = dict(agent.named_parameters())
+            self._policy_params = [named[k] for k in order]
+            self._policy_ptrs = (ctypes.c_void_p * 13)(*[p.data_ptr() for p in self._policy_params])
         self.next_obs = None
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
         self.iteration = 0
+
+    @staticmethod
+    def _fusable(agent, env) -> bool:
+        from .networks import PPO
+        from .vec_env import RadiotherapyVecEnv
+
+        return (isinstance(agent, PPO) and isinstance(env, RadiotherapyVecEnv) and agent.feature_dim == 64
+                and tuple(agent.observation_shape) == (9,) and tuple(agent.action_space) == (6,)
+                and all(p.dtype == torch.float32 and p.is_contiguous() for p in agent.parameters()))
 
     # ------------------------------------------------------------------ rollout
     def reset(self, seed=None):
         obs, _ = self.env.reset(seed=seed)
         self.next_obs = obs.clone()
         self.next_done.zero_()
+        self._done_valid = False
+
+    def _rollout_step_fused(self, step: int, env_events=None):
+        """train.py:138-158 as two native calls: rt_policy_sample writes
+        obs/done/action/logprob/value of this step into the storage, then the
+        env steps on storage actions[step] and writes rewards[step]/infos[step]."""
+        env = self.env
+        L = _lib.load()
+        stream = _lib.stream_handle()
+        _lib.check(L.rt_policy_sample(self._policy_ptrs, 13, self.N, env.obs.data_ptr(),
+                                      env.terminated.data_ptr() if self._done_valid else None,
+                                      self.obs[step].data_ptr(), self.dones[step].data_ptr(),
+                                      self.actions[step].data_ptr(), self.logprobs[step].data_ptr(),
+                                      self.values[step].data_ptr(), self._policy_seed, self._policy_counter,
+                                      self.rank * self.N, stream), "rt_policy_sample")
+        self._policy_counter += 1
+        if env_events is not None:
+            env_events[0].record()
+        env.step(self.actions[step], info_out=self.infos[step], reward_out=self.rewards[step])
+        if env_events is not None:
+            env_events[1].record()
+        self._done_valid = True
 
     @torch.no_grad()
     def rollout_step(self, step: int, env_events=None):
         """One vectorised step of train.py:138-161 (policy sample + env step)."""
+        if self.fused_policy:
+            return self._rollout_step_fused(step, env_events)
         self.obs[step].copy_(self.next_obs)
         self.dones[step].copy_(self.next_done)
         action, logprob, _, value = self.agent.get_action_and_value(self.next_obs, generator=self.gen)
@@ -137,9 +186,17 @@ class PPOTrainer:
             self.rollout_step(step)
         self.global_step += self.N * self.T * self.world
 
+    def _sync_next(self):
+        """Fused rollout keeps next_obs/next_done in the env's buffers."""
+        if self.fused_policy:
+            self.next_obs.copy_(self.env.obs)
+            if self._done_valid:
+                self.next_done.copy_(self.env.terminated)
+
     @torch.no_grad()
     def compute_gae(self):
         """train.py:163-181 via the rt_gae HIP kernel."""
+        self._sync_next()
         next_value = self.agent.get_value(self.next_obs).reshape(-1).contiguous()
         if self.gae_fn is not None:
             return self.gae_fn(self, next_value)

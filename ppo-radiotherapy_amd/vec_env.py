@@ -107,9 +107,11 @@ class RadiotherapyVecEnv:
         self._episode_start.fill_(time.perf_counter())
         return self.obs, {}
 
-    def step(self, actions: torch.Tensor, info_out: torch.Tensor | None = None):
-        """`info_out` (f32 [N, INFO_W], contiguous) receives the info rows
-        instead of the env's own buffer (rollout storage writes in place)."""
+    def step(self, actions: torch.Tensor, info_out: torch.Tensor | None = None,
+             reward_out: torch.Tensor | None = None):
+        """`info_out` (f32 [N, INFO_W]) / `reward_out` (f32 [N]), contiguous,
+        receive the info rows / rewards instead of the env's own buffers
+        (the rollout storage is written in place)."""
         a = actions
         if a.dtype != torch.float32 or a.device != self.device or not a.is_contiguous():
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
@@ -118,10 +120,15 @@ class RadiotherapyVecEnv:
         info = self.info if info_out is None else info_out
         if info_out is not None and (info_out.shape != self.info.shape or not info_out.is_contiguous()):
             raise ValueError("info_out must be a contiguous f32 [N, INFO_W] tensor")
-        _lib.check(self._L.rt_env_step(self._h, _lib.ptr(a), _lib.ptr(self.obs), _lib.ptr(self.reward),
+        rew = self.reward
+        if reward_out is not None:
+            if reward_out.shape != (self.num_envs,) or reward_out.dtype != torch.float32 or not reward_out.is_contiguous():
+                raise ValueError("reward_out must be a contiguous f32 [N] tensor")
+            rew = reward_out
+        _lib.check(self._L.rt_env_step(self._h, _lib.ptr(a), _lib.ptr(self.obs), _lib.ptr(rew),
                                        _lib.ptr(self.terminated), _lib.ptr(info), _lib.stream_handle()),
                    "rt_env_step")
-        return self.obs, self.reward, self.terminated.bool(), self.truncated, self._infos(info)
+        return self.obs, rew, self.terminated.view(torch.bool), self.truncated, LazyInfos(self._infos, info)
 
     def set_next_tumours(self, ids):
         t = torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
@@ -193,6 +200,52 @@ class RadiotherapyVecEnv:
             "overshoot": {"translation": I[:, 6:9], "rotation": I[:, 9]}, "_overshoot": stepped,
             "episode": ep, "_episode": ep_done,
         }
+
+
+class LazyInfos(dict):
+    """The gymnasium-style infos dict, built (a few small device ops) only
+    when first read -- the rollout loop never reads it."""
+
+    def __init__(self, build, info):
+        super().__init__()
+        self._build, self._info, self._done = build, info, False
+
+    def _fill(self):
+        if not self._done:
+            self._done = True
+            super().update(self._build(self._info))
+
+    def __getitem__(self, k):
+        self._fill()
+        return super().__getitem__(k)
+
+    def __contains__(self, k):
+        self._fill()
+        return super().__contains__(k)
+
+    def __iter__(self):
+        self._fill()
+        return super().__iter__()
+
+    def __len__(self):
+        self._fill()
+        return super().__len__()
+
+    def keys(self):
+        self._fill()
+        return super().keys()
+
+    def items(self):
+        self._fill()
+        return super().items()
+
+    def values(self):
+        self._fill()
+        return super().values()
+
+    def get(self, k, default=None):
+        self._fill()
+        return super().get(k, default)
 
 
 def has_episode(infos) -> bool:

@@ -92,3 +92,47 @@ def test_eager_update_matches_float64_reference():
         torch.randperm = orig
     for p, q in zip(e.params, c.params):
         torch.testing.assert_close(p.detach().cpu().double(), q.detach(), rtol=1e-4, atol=2e-6)
+
+
+def test_fused_policy_matches_torch_agent():
+    """rt_policy_sample: mean/value as the torch agent, log_prob consistent
+    with the sampled action, unit-normal noise."""
+    import ctypes
+
+    import numpy as np
+
+    from ppo_radiotherapy_amd import _lib
+    from ppo_radiotherapy_amd.networks import PPO
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    agent = PPO((9,), (6,), 64).to(dev)
+    with torch.no_grad():
+        agent.actor_logstd.fill_(-0.5)
+        agent.actor_mean[4].weight.mul_(50.0)  # non-trivial means
+    N = 20000
+    obs = torch.rand(N, 9, device=dev) * 2 - 1
+    done = (torch.rand(N, device=dev) < 0.3).to(torch.uint8)
+    out = {k: torch.zeros(s, device=dev) for k, s in
+           dict(obs=(N, 9), done=(N,), act=(N, 6), logp=(N,), val=(N,)).items()}
+    named = dict(agent.named_parameters())
+    order = ["actor_mean.0.weight", "actor_mean.0.bias", "actor_mean.2.weight", "actor_mean.2.bias",
+             "actor_mean.4.weight", "actor_mean.4.bias", "actor_logstd", "critic.0.weight", "critic.0.bias",
+             "critic.2.weight", "critic.2.bias", "critic.4.weight", "critic.4.bias"]
+    ptrs = (ctypes.c_void_p * 13)(*[named[k].data_ptr() for k in order])
+    L = _lib.load()
+    _lib.check(L.rt_policy_sample(ptrs, 13, N, obs.data_ptr(), done.data_ptr(), out["obs"].data_ptr(),
+                                  out["done"].data_ptr(), out["act"].data_ptr(), out["logp"].data_ptr(),
+                                  out["val"].data_ptr(), 123, 0, 0, None), "rt_policy_sample")
+    torch.cuda.synchronize()
+    assert torch.equal(out["obs"], obs) and torch.equal(out["done"], done.float())
+    with torch.no_grad():
+        mean = agent.actor_mean(obs)
+        _, logp_t, _, val_t = agent.get_action_and_value(obs, out["act"])
+    torch.testing.assert_close(out["val"], val_t.view(-1), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out["logp"], logp_t, rtol=1e-4, atol=1e-4)
+    z = ((out["act"] - mean) / np.exp(-0.5)).cpu().numpy()
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+    assert abs(np.corrcoef(z[:, 0], z[:, 1])[0, 1]) < 0.03
