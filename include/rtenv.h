@@ -184,6 +184,63 @@ int rt_gae(int32_t T, int32_t N, const float* rewards_d, const float* values_d,
            const float* dones_d, const float* next_value_d, const float* next_done_d,
            double gamma, double gae_lambda, float* adv_d, float* ret_d, void* stream);
 
+/* ---- fused PPO update of the visionless agent (train.py:183-246) ----------
+ * The rollout batch, flattened [T*N] (rows of obs are 9 floats, of actions 6). */
+typedef struct rt_ppo_batch {
+    const float* obs;
+    const float* actions;
+    const float* logprobs;
+    const float* advantages;
+    const float* returns;
+    const float* values;
+    int64_t batch_size;
+} rt_ppo_batch;
+
+/* train.py:200-246 hyper-parameters (config keys of the same names). */
+typedef struct rt_ppo_hparams {
+    float clip_coef;
+    int32_t clip_vloss;
+    int32_t norm_adv;   /* adv_stats_d ([mean, std] per minibatch) required when set */
+    float ent_coef;
+    float vf_coef;
+    float max_grad_norm; /* <= 0: no clipping */
+    double adam_beta1, adam_beta2;
+    float adam_eps;
+} rt_ppo_hparams;
+
+/* Floats of workspace rt_ppo_grad / rt_ppo_update need for a minibatch. */
+int64_t rt_ppo_workspace_floats(int32_t minibatch_size);
+/* Parameters of the fused agent (10,061). */
+int32_t rt_ppo_num_params(void);
+
+/* Gradient of the minibatch PPO loss (train.py:200-238: clipped surrogate,
+ * [clipped] value loss * vf_coef, - ent_coef * entropy; advantages normalised
+ * with adv_stats_d when norm_adv) w.r.t. the 13 parameter tensors (order of
+ * rt_policy_sample), written (not accumulated) into grads_d[13].  mb_idx_d:
+ * the minibatch's rows of the batch.  stats_d[6] = pg_loss, v_loss, entropy,
+ * old_approx_kl, approx_kl, clipfrac of the minibatch (train.py:206-211);
+ * stats_accum_d[6] (optional) += the same. */
+int rt_ppo_grad(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
+                const int64_t* mb_idx_d, int32_t mb_size, const float* adv_stats_d,
+                const rt_ppo_hparams* hp, float* workspace_d, int64_t workspace_floats, float* stats_d,
+                float* stats_accum_d, void* stream);
+
+/* nn.utils.clip_grad_norm_(max_grad_norm) + torch.optim.Adam step number
+ * `step` (foreach op order) over flat parameter / gradient / state buffers. */
+int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp_avg_d, float* exp_avg_sq_d,
+                 int64_t step, double lr, const rt_ppo_hparams* hp, void* stream);
+
+/* n_minibatches consecutive optimizer steps (rt_ppo_grad + rt_adam_step) on
+ * the minibatches perm_d[i*mb_size, (i+1)*mb_size) of one epoch (single
+ * process; data-parallel callers interleave rt_ppo_grad, the all-reduce and
+ * rt_adam_step themselves).  params_d / grads_d are views of flat_param_d /
+ * flat_grad_d; the first step is numbered step0. */
+int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
+                  const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches, const float* adv_stats_d,
+                  const rt_ppo_hparams* hp, float* flat_param_d, float* flat_grad_d, float* exp_avg_d,
+                  float* exp_avg_sq_d, int64_t n_flat, int64_t step0, double lr, float* workspace_d,
+                  int64_t workspace_floats, float* stats_d, float* stats_accum_d, void* stream);
+
 const char* rt_last_error(void);
 int rt_abi_version(void);
 

@@ -30,7 +30,9 @@ EXPORTS = [
     "rt_env_config_default", "rt_env_create", "rt_env_destroy", "rt_env_reset", "rt_env_step",
     "rt_env_set_next_tumours", "rt_env_dose", "rt_env_get_state", "rt_env_set_pose", "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
-    "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae", "rt_last_error", "rt_abi_version",
+    "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
+    "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
+    "rt_last_error", "rt_abi_version",
 ]
 
 
@@ -60,6 +62,25 @@ class RtEnvConfig(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("env_id_base", ctypes.c_int64),
         ("step_mode", ctypes.c_int32),
+    ]
+
+
+class RtPpoBatch(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in ("obs", "actions", "logprobs", "advantages", "returns", "values")] + [
+        ("batch_size", ctypes.c_int64)]
+
+
+class RtPpoHparams(ctypes.Structure):
+    _fields_ = [
+        ("clip_coef", ctypes.c_float),
+        ("clip_vloss", ctypes.c_int32),
+        ("norm_adv", ctypes.c_int32),
+        ("ent_coef", ctypes.c_float),
+        ("vf_coef", ctypes.c_float),
+        ("max_grad_norm", ctypes.c_float),
+        ("adam_beta1", ctypes.c_double),
+        ("adam_beta2", ctypes.c_double),
+        ("adam_eps", ctypes.c_float),
     ]
 
 
@@ -105,6 +126,14 @@ def load(build_if_missing: bool = True):
         "rt_gae": ([i32, i32, vp, vp, vp, vp, vp, f64, f64, vp, vp, vp], ctypes.c_int),
         "rt_policy_sample": ([ctypes.POINTER(vp), i32, i32, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint64,
                               ctypes.c_uint64, i64, vp], ctypes.c_int),
+        "rt_ppo_workspace_floats": ([i32], i64),
+        "rt_ppo_num_params": ([], i32),
+        "rt_ppo_grad": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, vp,
+                         ctypes.POINTER(RtPpoHparams), vp, i64, vp, vp, vp], ctypes.c_int),
+        "rt_adam_step": ([i64, vp, vp, vp, vp, i64, f64, ctypes.POINTER(RtPpoHparams), vp], ctypes.c_int),
+        "rt_ppo_update": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, i32, vp,
+                           ctypes.POINTER(RtPpoHparams), vp, vp, vp, vp, i64, i64, f64, vp, i64, vp, vp, vp],
+                          ctypes.c_int),
         "rt_last_error": ([], ctypes.c_char_p),
         "rt_abi_version": ([], ctypes.c_int),
     }

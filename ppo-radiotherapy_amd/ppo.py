@@ -80,8 +80,28 @@ class PPOTrainer:
         self.batch_size = N * T                       # per rank
         self.minibatch_size = self.batch_size // int(cfg.num_minibatches)
         self.params = [p for p in agent.parameters()]
-        # one flat gradient bucket; every param.grad is a view of it
         n = sum(p.numel() for p in self.params)
+        # fused HIP update (rt_ppo_update: loss + backward + clip + Adam in 3
+        # kernels per minibatch) for the visionless 64-wide agent
+        self.fused_update = (bool(getattr(cfg, "fused_update", True)) and self.device.type == "cuda"
+                             and not bool(getattr(cfg, "cuda_graphs", False)) and self._agent_fusable(agent)
+                             and self.batch_size % self.minibatch_size == 0)
+        if self.fused_update:
+            # parameters become views of one flat buffer (Adam runs over it)
+            self.flat_param = torch.empty(n, dtype=self.params[0].dtype, **kw)
+            off = 0
+            with torch.no_grad():
+                for p in self.params:
+                    k = p.numel()
+                    self.flat_param[off:off + k].copy_(p.reshape(-1))
+                    p.data = self.flat_param[off:off + k].view_as(p)
+                    off += k
+            self._exp_avg = torch.zeros_like(self.flat_param)
+            self._exp_avg_sq = torch.zeros_like(self.flat_param)
+            self._adam_step = 0
+            self._ppo_stats = torch.zeros(6, **kw)
+            self._ppo_accum = torch.zeros(6, **kw)
+        # one flat gradient bucket; every param.grad is a view of it
         self.flat_grad = torch.zeros(n, dtype=self.params[0].dtype, **kw)
         off = 0
         for p in self.params:
@@ -108,28 +128,43 @@ class PPOTrainer:
         self._policy_counter = 0
         self._policy_seed = int(getattr(cfg, "seed", 0)) * 1_000_003 + 7919 * rank + 1
         self._done_valid = False
-        if self.fused_policy:
+        if self.fused_policy or self.fused_update:
             import ctypes
 
-            order = ["actor_mean.0.weight", "actor_mean.0.bias", "actor_mean.2.weight", "actor_mean.2.bias",
-                     "actor_mean.4.weight", "actor_mean.4.bias", "actor_logstd", "critic.0.weight", "critic.0.bias",
-                     "critic.2.weight", "critic.2.bias", "critic.4.weight", "critic.4.bias"]
             named = dict(agent.named_parameters())
-            self._policy_params = [named[k] for k in order]
+            self._policy_params = [named[k] for k in self.POLICY_ORDER]
             self._policy_ptrs = (ctypes.c_void_p * 13)(*[p.data_ptr() for p in self._policy_params])
+        if self.fused_update:
+            L = _lib.load()
+            self._grad_ptrs = (ctypes.c_void_p * 13)(*[p.grad.data_ptr() for p in self._policy_params])
+            self._hp = _lib.RtPpoHparams(
+                clip_coef=float(cfg.clip_coef), clip_vloss=int(bool(cfg.clip_vloss)), norm_adv=int(bool(cfg.norm_adv)),
+                ent_coef=float(cfg.ent_coef), vf_coef=float(cfg.vf_coef), max_grad_norm=float(cfg.max_grad_norm),
+                adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
+            self._ws = torch.empty(int(L.rt_ppo_workspace_floats(self.minibatch_size)), **kw)
         self.next_obs = None
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
         self.iteration = 0
 
-    @staticmethod
-    def _fusable(agent, env) -> bool:
-        from .networks import PPO
-        from .vec_env import RadiotherapyVecEnv
+    # parameter order of the fused kernels (include/rtenv.h rt_policy_sample)
+    POLICY_ORDER = ["actor_mean.0.weight", "actor_mean.0.bias", "actor_mean.2.weight", "actor_mean.2.bias",
+                    "actor_mean.4.weight", "actor_mean.4.bias", "actor_logstd", "critic.0.weight", "critic.0.bias",
+                    "critic.2.weight", "critic.2.bias", "critic.4.weight", "critic.4.bias"]
 
-        return (isinstance(agent, PPO) and isinstance(env, RadiotherapyVecEnv) and agent.feature_dim == 64
+    @staticmethod
+    def _agent_fusable(agent) -> bool:
+        from .networks import PPO
+
+        return (isinstance(agent, PPO) and agent.feature_dim == 64
                 and tuple(agent.observation_shape) == (9,) and tuple(agent.action_space) == (6,)
                 and all(p.dtype == torch.float32 and p.is_contiguous() for p in agent.parameters()))
+
+    @classmethod
+    def _fusable(cls, agent, env) -> bool:
+        from .vec_env import RadiotherapyVecEnv
+
+        return isinstance(env, RadiotherapyVecEnv) and cls._agent_fusable(agent)
 
     # ------------------------------------------------------------------ rollout
     def reset(self, seed=None):
@@ -308,8 +343,64 @@ class PPOTrainer:
         self._b_ret = self.returns.reshape(-1)
         self._b_val = self.values.reshape(-1)
 
+    def _batch_struct(self):
+        return _lib.RtPpoBatch(self._b_obs.data_ptr(), self._b_actions.data_ptr(), self._b_logprobs.data_ptr(),
+                               self._b_adv.data_ptr(), self._b_ret.data_ptr(), self._b_val.data_ptr(),
+                               self.batch_size)
+
+    def _update_fused(self):
+        """train.py:183-248 through the fused kernels: per epoch one device
+        randperm and one (all-reduced) advantage-statistics reduction, then per
+        minibatch rt_ppo_grad + rt_adam_step (world 1: the whole epoch is one
+        rt_ppo_update call; world > 1: RCCL all-reduce of the flat gradient
+        bucket between the two)."""
+        import ctypes
+
+        self._bind_batch()
+        L = _lib.load()
+        stream = _lib.stream_handle()
+        batch = self._batch_struct()
+        hp = ctypes.byref(self._hp)
+        mbs = self.minibatch_size
+        n_mb = self.batch_size // mbs
+        lr = float(self.optimizer.param_groups[0]["lr"])
+        n = self.flat_param.numel()
+        self._ppo_accum.zero_()
+        done = 0
+        for _ in range(int(self.cfg.update_epochs)):
+            perm = torch.randperm(self.batch_size, device=self.device, generator=self.gen)
+            adv = self._epoch_adv_stats(self._b_adv, perm).contiguous() if self.cfg.norm_adv else None
+            k = n_mb if not self.max_minibatches else min(n_mb, self.max_minibatches - done)
+            if self.world == 1:
+                _lib.check(L.rt_ppo_update(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch), perm.data_ptr(),
+                                           mbs, k, _lib.ptr(adv), hp, self.flat_param.data_ptr(),
+                                           self.flat_grad.data_ptr(), self._exp_avg.data_ptr(),
+                                           self._exp_avg_sq.data_ptr(), n, self._adam_step + 1, lr,
+                                           self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
+                                           self._ppo_accum.data_ptr(), stream), "rt_ppo_update")
+                self._adam_step += k
+            else:
+                for i in range(k):
+                    _lib.check(L.rt_ppo_grad(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch),
+                                             perm.data_ptr() + 8 * i * mbs, mbs,
+                                             None if adv is None else adv.data_ptr() + 8 * i, hp,
+                                             self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
+                                             self._ppo_accum.data_ptr(), stream), "rt_ppo_grad")
+                    self._allreduce_(self.flat_grad)
+                    self._adam_step += 1
+                    _lib.check(L.rt_adam_step(n, self.flat_param.data_ptr(), self.flat_grad.data_ptr(),
+                                              self._exp_avg.data_ptr(), self._exp_avg_sq.data_ptr(),
+                                              self._adam_step, lr, hp, stream), "rt_adam_step")
+            done += k
+            if self.max_minibatches and done >= self.max_minibatches:
+                break
+        self._last_stats = torch.cat([self._ppo_stats[:5], (self._ppo_accum[5] / max(done, 1)).reshape(1)])
+        return done
+
     def update(self):
         """train.py:183-248: update_epochs x num_minibatches optimizer steps."""
+        if self.fused_update:
+            return self._update_fused()
         if self.use_graphs:
             return self._update_graphed()
         self._bind_batch()

@@ -1,4 +1,5 @@
-"""The hipGraph-captured PPO update equals the eager update."""
+"""PPO update paths on the GPU: fused HIP update (rt_ppo_grad / rt_adam_step)
+vs autograd and a float64 reference; hipGraph-captured vs eager; fused policy."""
 import os
 import sys
 from types import SimpleNamespace
@@ -18,7 +19,7 @@ def _cfg(**kw):
     return SimpleNamespace(**c)
 
 
-def _make(graphs):
+def _make(graphs, fused=False):
     from fake_env import FakeVecEnv, torch_gae
 
     from ppo_radiotherapy_amd.networks import PPO
@@ -30,7 +31,7 @@ def _make(graphs):
     torch.manual_seed(0)
     agent = PPO((9,), (6,), 64).to(dev)
     gen = torch.Generator(device=dev).manual_seed(5)
-    tr = PPOTrainer(_cfg(cuda_graphs=graphs), FakeVecEnv(256), agent, dev, generator=gen, gae_fn=torch_gae)
+    tr = PPOTrainer(_cfg(cuda_graphs=graphs, fused_update=fused), FakeVecEnv(256), agent, dev, generator=gen, gae_fn=torch_gae)
     g = torch.Generator(device="cpu").manual_seed(1)
     for t in (tr.obs, tr.actions, tr.logprobs, tr.advantages, tr.returns, tr.values):
         t.copy_(torch.randn(t.shape, generator=g))
@@ -55,14 +56,17 @@ def test_graphed_update_matches_eager():
     assert float(graphed.optimizer.param_groups[0]["lr"]) == pytest.approx(3e-4 * 0.8)
 
 
-def test_eager_update_matches_float64_reference():
-    """The (default, eager) update vs a CPU float64 run of the same minibatches."""
+@pytest.mark.parametrize("fused", [False, True], ids=["torch", "fused"])
+def test_update_matches_float64_reference(fused):
+    """The eager torch update and the fused HIP update vs a CPU float64 run of
+    the same minibatches (2 iterations x 3 epochs x 4 minibatches)."""
     from fake_env import FakeVecEnv, torch_gae
 
     from ppo_radiotherapy_amd.networks import PPO
     from ppo_radiotherapy_amd.ppo import PPOTrainer
 
-    e = _make(False)
+    e = _make(False, fused)
+    assert e.fused_update == fused
     rec = []
     orig = torch.randperm
 
@@ -92,6 +96,131 @@ def test_eager_update_matches_float64_reference():
         torch.randperm = orig
     for p, q in zip(e.params, c.params):
         torch.testing.assert_close(p.detach().cpu().double(), q.detach(), rtol=1e-4, atol=2e-6)
+    torch.testing.assert_close(e._last_stats.cpu().double(), c._last_stats.detach().double(), rtol=1e-3, atol=1e-6)
+
+
+def _policy_ptrs(agent, grads=False):
+    import ctypes
+
+    from ppo_radiotherapy_amd.ppo import PPOTrainer
+
+    named = dict(agent.named_parameters())
+    ts = [named[k].grad if grads else named[k] for k in PPOTrainer.POLICY_ORDER]
+    return (ctypes.c_void_p * 13)(*[t.data_ptr() for t in ts]), ts
+
+
+@pytest.mark.parametrize("mb,clip_vloss,norm_adv,ent", [(4096, 1, 1, 0.0), (3001, 1, 0, 0.01), (77, 0, 1, 0.0)])
+def test_fused_grad_matches_autograd(mb, clip_vloss, norm_adv, ent):
+    """rt_ppo_grad vs float64 autograd of train.py:200-238 on one minibatch
+    (ragged sizes: partial last tile; ratios spread across both clip edges)."""
+    import ctypes
+
+    from ppo_radiotherapy_amd import _lib
+    from ppo_radiotherapy_amd.networks import PPO
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = torch.device("cuda")
+    torch.manual_seed(11)
+    agent = PPO((9,), (6,), 64).to(dev)
+    with torch.no_grad():
+        agent.actor_logstd.copy_(torch.linspace(-0.7, 0.2, 6).view(1, 6))
+        agent.actor_mean[4].weight.mul_(30.0)
+    B = 8192
+    g = torch.Generator(device="cpu").manual_seed(2)
+    obs = (torch.rand(B, 9, generator=g) * 2 - 1).to(dev)
+    with torch.no_grad():
+        act, logp, _, val = agent.get_action_and_value(obs)
+    logp = (logp + 0.3 * torch.randn(B, generator=g).to(dev)).contiguous()   # ratios around [0.5, 2]
+    adv = (torch.randn(B, generator=g) * 3 + 0.5).to(dev)
+    val = (val.view(-1) + 0.2 * torch.randn(B, generator=g).to(dev)).contiguous()
+    ret = (val + torch.randn(B, generator=g).to(dev)).contiguous()
+    idx = torch.randperm(B, generator=g)[:mb].to(dev)
+    a = adv[idx]
+    stats2 = torch.stack([a.mean(), a.std()]).contiguous()
+    for p in agent.parameters():
+        p.grad = torch.full_like(p, float("nan"))   # written, not accumulated
+    pp, _ = _policy_ptrs(agent)
+    gp, grads = _policy_ptrs(agent, grads=True)
+    hp = _lib.RtPpoHparams(clip_coef=0.1, clip_vloss=clip_vloss, norm_adv=norm_adv, ent_coef=ent, vf_coef=0.5,
+                           max_grad_norm=0.5, adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
+    batch = _lib.RtPpoBatch(obs.data_ptr(), act.data_ptr(), logp.data_ptr(), adv.data_ptr(), ret.data_ptr(),
+                            val.data_ptr(), B)
+    L = _lib.load()
+    ws = torch.empty(int(L.rt_ppo_workspace_floats(mb)), device=dev)
+    st = torch.zeros(6, device=dev)
+    acc = torch.ones(6, device=dev)
+    _lib.check(L.rt_ppo_grad(pp, gp, ctypes.byref(batch), idx.data_ptr(), mb, stats2.data_ptr(), ctypes.byref(hp),
+                             ws.data_ptr(), ws.numel(), st.data_ptr(), acc.data_ptr(), None), "rt_ppo_grad")
+    torch.cuda.synchronize()
+    # float64 autograd reference (ppo.PPOTrainer._loss_backward, the reference's formulas)
+    ref = PPO((9,), (6,), 64).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in agent.state_dict().items()})
+    i = idx.cpu()
+    d = lambda t: t.detach().cpu().double()[i]
+    _, nlp, ent_t, nv = ref.get_action_and_value(d(obs), d(act))
+    lr_ = nlp - d(logp)
+    ratio = lr_.exp()
+    A = d(adv)
+    if norm_adv:
+        A = (A - A.mean()) / (A.std() + 1e-8)
+    pg = torch.max(-A * ratio, -A * torch.clamp(ratio, 0.9, 1.1)).mean()
+    nv = nv.view(-1)
+    R, V = d(ret), d(val)
+    if clip_vloss:
+        vc = V + torch.clamp(nv - V, -0.1, 0.1)
+        vl = 0.5 * torch.max((nv - R) ** 2, (vc - R) ** 2).mean()
+    else:
+        vl = 0.5 * ((nv - R) ** 2).mean()
+    loss = pg - ent * ent_t.mean() + 0.5 * vl
+    loss.backward()
+    named = dict(ref.named_parameters())
+    from ppo_radiotherapy_amd.ppo import PPOTrainer
+    for k, gk in zip(PPOTrainer.POLICY_ORDER, grads):
+        r = named[k].grad
+        scale = float(r.abs().max()) + 1e-12
+        err = float((gk.detach().cpu().double() - r).abs().max()) / scale
+        assert err < 2e-4, (k, err)
+    want = torch.stack([pg, vl, ent_t.mean(), (-lr_).mean(), ((ratio - 1) - lr_).mean(),
+                        ((ratio - 1).abs() > 0.1).double().mean()]).detach()
+    torch.testing.assert_close(st.cpu().double(), want, rtol=2e-4, atol=2e-6)
+    torch.testing.assert_close(acc.cpu().double(), want + 1.0, rtol=2e-4, atol=2e-6)
+    frac = float(want[5])
+    assert 0.2 < frac < 0.95  # both clip branches exercised
+
+
+@pytest.mark.parametrize("max_norm", [0.5, 0.0])
+def test_fused_adam_matches_torch(max_norm):
+    """rt_adam_step == clip_grad_norm_ + torch.optim.Adam(eps=1e-5) step by step."""
+    from ppo_radiotherapy_amd import _lib
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(4)
+    n = 10061
+    p0 = torch.randn(n, generator=g).to(dev)
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=3e-4, eps=1e-5, foreach=True)
+    mine, m, v = p0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    hp = _lib.RtPpoHparams(clip_coef=0.1, clip_vloss=1, norm_adv=1, ent_coef=0.0, vf_coef=0.5,
+                           max_grad_norm=max_norm, adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
+    import ctypes
+    L = _lib.load()
+    for step in range(1, 6):
+        grad = (torch.randn(n, generator=g) * 0.05 * step).to(dev)
+        lr = 3e-4 * (1 - 0.1 * step)
+        opt.param_groups[0]["lr"] = lr
+        ref.grad = grad.clone()
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_([ref], max_norm)
+        opt.step()
+        gm = grad.clone()
+        _lib.check(L.rt_adam_step(n, mine.data_ptr(), gm.data_ptr(), m.data_ptr(), v.data_ptr(), step, lr,
+                                  ctypes.byref(hp), None), "rt_adam_step")
+        torch.cuda.synchronize()
+        torch.testing.assert_close(gm, ref.grad, rtol=1e-6, atol=1e-9)
+        torch.testing.assert_close(mine, ref.detach(), rtol=1e-6, atol=1e-7)
 
 
 def test_fused_policy_matches_torch_agent():
