@@ -226,9 +226,10 @@ int rt_ppo_grad(const float* const* params_d, float* const* grads_d, const rt_pp
                 float* stats_accum_d, void* stream);
 
 /* nn.utils.clip_grad_norm_(max_grad_norm) + torch.optim.Adam step number
- * `step` (foreach op order) over flat parameter / gradient / state buffers. */
+ * `step` (foreach op order) over flat parameter / gradient / state buffers.
+ * workspace_d: >= 256 floats of device scratch (the norm partials). */
 int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp_avg_d, float* exp_avg_sq_d,
-                 int64_t step, double lr, const rt_ppo_hparams* hp, void* stream);
+                 int64_t step, double lr, const rt_ppo_hparams* hp, float* workspace_d, void* stream);
 
 /* n_minibatches consecutive optimizer steps (rt_ppo_grad + rt_adam_step) on
  * the minibatches perm_d[i*mb_size, (i+1)*mb_size) of one epoch (single

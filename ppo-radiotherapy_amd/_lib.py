@@ -130,7 +130,7 @@ def load(build_if_missing: bool = True):
         "rt_ppo_num_params": ([], i32),
         "rt_ppo_grad": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, vp,
                          ctypes.POINTER(RtPpoHparams), vp, i64, vp, vp, vp], ctypes.c_int),
-        "rt_adam_step": ([i64, vp, vp, vp, vp, i64, f64, ctypes.POINTER(RtPpoHparams), vp], ctypes.c_int),
+        "rt_adam_step": ([i64, vp, vp, vp, vp, i64, f64, ctypes.POINTER(RtPpoHparams), vp, vp], ctypes.c_int),
         "rt_ppo_update": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, i32, vp,
                            ctypes.POINTER(RtPpoHparams), vp, vp, vp, vp, i64, i64, f64, vp, i64, vp, vp, vp],
                           ctypes.c_int),

@@ -27,6 +27,9 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
 
 #include "rtenv.h"
 
@@ -358,50 +361,550 @@ __global__ __launch_bounds__(kThreads) void k_ppo_grad(GradParams P) {
     trunk_bwd<NACT>(aw2, aw3, X, AH1, AH2, G2, GM, tid, out, O_AW1, O_AB1, O_AW2, O_AB2, O_AW3, O_AB3);
 }
 
+// ============================================================================
+// k_ppo_grad_mfma: the same computation on f32 MFMA (v_mfma_f32_16x16x4_f32,
+// exact f32 FMA chains).
+//
+// The PPO loss separates by head: the clipped surrogate and the entropy depend
+// only on actor_mean / actor_logstd, the value loss only on the critic.  A
+// block runs 4 wavefront pairs; in each pair one wave back-propagates the
+// actor and the other the critic over the same 16-sample tiles, so every SIMD
+// holds two independent instruction streams (one wave's MFMAs overlap the
+// other's VALU) within 256 registers per wave.
+//
+// Inside a wave every activation stays in registers in the transposed
+// [unit][sample] layout of the MFMA accumulator (lane l: sample c = l & 15,
+// units 4g..4g+3 of each 16-row tile, g = l >> 4):
+//   forward   Z^T = W . X^T           (sums over the accumulator's ROW index:
+//   data grad G1^T = W2^T . G2^T        the previous tile is the B operand as is)
+//   weight grad dW = G^T-tile . H       (sums over samples = the lane index: the
+//                                        tiles go through wave-private LDS
+//                                        scratch [unit][16 samples] and come back
+//                                        as ds_read_b128 fragments)
+// Weight gradients accumulate in MFMA accumulators across all tiles of the
+// wave; the 4 pairs of a block are summed through LDS in a fixed order
+// (deterministic) into one partial row.  Layer-1 biases ride in column 9 of an
+// augmented W1 (X^T row 9 = 1), so db1 comes out of the dW1 product.
+// ============================================================================
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int MT = 512;   // 8 wavefronts: 4 (actor, critic) pairs, 2 per SIMD
+constexpr int NPAIR = MT / 128;
+constexpr int WP = 68;    // LDS row stride of W2 (b128 fragment reads 2-way, b32 reads conflict-free)
+constexpr int W1P = 12;   // augmented W1 row: 9 weights, bias, 2 zeros
+constexpr int SP = 24;    // scratch row stride (16 samples + pad: b128 reads conflict-free)
+constexpr int SCR = 152;  // scratch rows per wave: A 0..63, B 64..127, X^T 128..143, GM^T 144..151
+constexpr int kMaxGradBlocks = 256;
+
+struct MfmaLds {
+    float w2[2][H * WP];
+    float w1[2][H * W1P];
+    float b2[2][H];
+    float w3[7 * H];  // rows 0..5 actor_mean.4, row 6 critic.4
+    float b3[8];
+    float ls[8];
+    float isd[8];  // 1 / exp(logstd), [6]: 1 / (adv std + 1e-8)
+    float scr[MT / 64][SCR * SP];
+};
+static_assert(sizeof(MfmaLds) <= 160 * 1024, "LDS");
+constexpr int kW2Region = 2 * H * H;    // reduction phase 1: both W2 of one pair
+constexpr int kRestRegion = 1880;       // phase 2: the other 1875 values + dump slot
+static_assert(sizeof(MfmaLds) >= NPAIR * kW2Region * sizeof(float), "reduction overlay");
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// lanes of a wavefront exchange data through LDS between these points
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float el(const float4& v, int r) { return r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w; }
+
+// tanh without branches: odd Taylor polynomial below |x| = 0.25 (truncation
+// < 1e-9 relative), 1 - 2 / (exp(2|x|) + 1) above (no cancellation there);
+// a few ulp from libm tanhf -- the update's forward need not be bit-exact
+// (ratio = exp(new - old logprob) is ~1 +- 1e-6 on the first epoch either way)
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float ax = fabsf(x);
+    const float e = __expf(2.0f * fminf(ax, 30.0f));
+    const float big = 1.0f - 2.0f * __frcp_rn(e + 1.0f);
+    const float x2 = x * x;
+    const float small =
+        x + x * x2 * (-0.333333333f + x2 * (0.133333333f + x2 * (-0.0539682540f + x2 * 0.0218694885f)));
+    return ax < 0.25f ? small : copysignf(big, x);
+}
+
+__device__ __forceinline__ float sum16(float v) {  // over the 16 lanes c of one g-group
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// index of a parameter in the phase-2 reduction region (everything but the two W2)
+__device__ __forceinline__ int rest_slot(int p) {
+    return p < O_AW2 ? p : (p < O_CW2 ? O_AW2 + (p - O_AB2) : O_AW2 + (O_CW2 - O_AB2) + (p - O_CB2));
+}
+constexpr int kRestDump = 1875;
+
+// forward of this wave's trunk for its tile: h1, h2 = tanh layers, transposed tiles
+__device__ __forceinline__ void mf_fwd(const MfmaLds& S, int h, const float* Xs, int c, int g, f4 h1[4], f4 h2[4]) {
+    float xb[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) xb[q] = Xs[(4 * q + g) * SP + c];
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int q = 0; q < 3; ++q) z = mfma4(S.w1[h][(16 * J + c) * W1P + 4 * q + g], xb[q], z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h1[J][r] = tanh_fast(z[r]);
+    }
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int T = 0; T < 4; ++T) {
+            const float4 a = ld4(&S.w2[h][(16 * J + c) * WP + 16 * T + 4 * g]);
+            z = mfma4(a.x, h1[T][0], z);
+            z = mfma4(a.y, h1[T][1], z);
+            z = mfma4(a.z, h1[T][2], z);
+            z = mfma4(a.w, h1[T][3], z);
+        }
+        const float4 b = ld4(&S.b2[h][16 * J + 4 * g]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h2[J][r] = tanh_fast(z[r] + el(b, r));
+    }
+}
+
+// per-role accumulators of one wave
+template <int HEAD>
+struct Acc {
+    f4 d2[4][4];       // dW2[16J+4g+r][16T+c]
+    f4 d1[4];          // [dW1 | db1][16J+4g+r][c]
+    f4 d3[4];          // actor: dW3[4g+r][16J+c] (rows < 6); critic: per-lane dW3 partial [16J+4g+r]
+    float db2[16];     // per-lane partial db2[16J+4g+r]
+    float sc[HEAD == 0 ? 2 * NACT + 5 : 2];  // actor: db3[6], dlogstd[6], pg, ent, -lr, r-1-lr, clipped; critic: db3, vl
+};
+
+template <int HEAD>
+__device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, float* A, float* Bs, float* Xs,
+                                        float* GMs, int c, int g, int t, float inv_n, Acc<HEAD>& acc) {
+    constexpr int NOUT = HEAD == 0 ? NACT : 1;
+    const int m = t * 16 + c;
+    const bool live = m < P.mb;
+    const int64_t row = live ? P.idx[m] : 0;
+    wave_sync();  // the previous tile's reads of the scratch are done
+    for (int i = g; i <= NOBS; i += 4) Xs[i * SP + c] = !live ? 0.0f : (i < NOBS ? P.obs[row * NOBS + i] : 1.0f);
+    wave_sync();
+    f4 h1[4], h2[4];
+    mf_fwd(S, HEAD, Xs, c, g, h1, h2);
+    // head outputs: partial dots over this lane's 16 units, summed over the sample's 4 g-lanes
+    float out[NOUT];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+        const int wr = HEAD == 0 ? o : NACT;
+        float p = 0.0f;
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {
+            const float4 w = ld4(&S.w3[wr * H + 16 * J + 4 * g]);
+            p += w.x * h2[J][0] + w.y * h2[J][1] + w.z * h2[J][2] + w.w * h2[J][3];
+        }
+        p += __shfl_xor(p, 16, 64);
+        p += __shfl_xor(p, 32, 64);
+        out[o] = p + S.b3[wr];
+    }
+    // ---- per-sample loss derivative w.r.t. this head's outputs (train.py:200-236)
+    float go[NOUT];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) go[o] = 0.0f;
+    if (live) {
+        if constexpr (HEAD == 0) {
+            float z[NACT], logp = 0.0f, ent = 0.0f;
+#pragma unroll
+            for (int k = 0; k < NACT; ++k) {
+                z[k] = (P.act[row * NACT + k] - out[k]) * S.isd[k];
+                logp += -0.5f * z[k] * z[k] - S.ls[k] - kHalfLog2Pi;
+                ent += 0.5f + kHalfLog2Pi + S.ls[k];
+            }
+            const float lr = logp - P.logp[row];
+            const float r = __expf(lr);
+            float Av = P.adv[row];
+            if (P.adv_stats) Av = (Av - P.adv_stats[0]) * S.isd[NACT];
+            const float pg1 = -Av * r;
+            const float rc = fminf(fmaxf(r, P.clip_lo), P.clip_hi);
+            const float pg2 = -Av * rc;
+            // torch.maximum backward: the larger input takes the gradient, ties split it
+            const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+            const float w2 = pg2 > pg1 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+            const float pass = (r >= P.clip_lo && r <= P.clip_hi) ? 1.0f : 0.0f;  // clamp backward
+            const float g_logp = inv_n * (w1 * -Av + w2 * -Av * pass) * r;
+#pragma unroll
+            for (int k = 0; k < NACT; ++k) go[k] = g_logp * z[k] * S.isd[k];
+            if (g == 0) {  // one contribution per sample
+#pragma unroll
+                for (int k = 0; k < NACT; ++k) {
+                    acc.sc[k] += go[k];
+                    acc.sc[NACT + k] += g_logp * (z[k] * z[k] - 1.0f);
+                }
+                acc.sc[2 * NACT + 0] += fmaxf(pg1, pg2);
+                acc.sc[2 * NACT + 1] += ent;
+                acc.sc[2 * NACT + 2] += -lr;
+                acc.sc[2 * NACT + 3] += (r - 1.0f) - lr;
+                acc.sc[2 * NACT + 4] += fabsf(r - 1.0f) > P.clip ? 1.0f : 0.0f;
+            }
+        } else {
+            const float value = out[0];
+            const float R = P.ret[row], V = P.val[row];
+            float vl, dv;
+            if (P.clip_vloss) {
+                const float d = value - V;
+                const float vc = V + fminf(fmaxf(d, -P.clip), P.clip);
+                const float vu = (value - R) * (value - R), vcc = (vc - R) * (vc - R);
+                vl = fmaxf(vu, vcc);
+                const float wu = vu > vcc ? 1.0f : (vu == vcc ? 0.5f : 0.0f);
+                const float wc = vcc > vu ? 1.0f : (vu == vcc ? 0.5f : 0.0f);
+                const float dpass = (d >= -P.clip && d <= P.clip) ? 1.0f : 0.0f;
+                dv = wu * 2.0f * (value - R) + wc * 2.0f * (vc - R) * dpass;
+            } else {
+                vl = (value - R) * (value - R);
+                dv = 2.0f * (value - R);
+            }
+            go[0] = P.vf_coef * 0.5f * inv_n * dv;
+            if (g == 0) {
+                acc.sc[0] += go[0];
+                acc.sc[1] += vl;
+            }
+        }
+    }
+    // ---- dW3
+    if constexpr (HEAD == 0) {
+        // GM^T -> scratch, H2^T -> A; dW3 += GM^T . H2 over the tile's samples
+        for (int o = g; o < NACT; o += 4) GMs[o * SP + c] = go[o];
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(16 * J + 4 * g + r) * SP + c] = h2[J][r];
+        wave_sync();
+        const float4 ga = c < NACT ? ld4(&GMs[c * SP + 4 * g]) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {
+            const float4 bq = ld4(&A[(16 * J + c) * SP + 4 * g]);
+            acc.d3[J] = mfma4(ga.x, bq.x, acc.d3[J]);
+            acc.d3[J] = mfma4(ga.y, bq.y, acc.d3[J]);
+            acc.d3[J] = mfma4(ga.z, bq.z, acc.d3[J]);
+            acc.d3[J] = mfma4(ga.w, bq.w, acc.d3[J]);
+        }
+    } else {
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc.d3[J][r] += go[0] * h2[J][r];
+    }
+    // ---- G2^T = (W3^T go) * (1 - H2^2); db2 += G2
+    f4 g2[4];
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+        f4 a = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o) {
+            const float4 w = ld4(&S.w3[(HEAD == 0 ? o : NACT) * H + 16 * J + 4 * g]);
+            a[0] += w.x * go[o];
+            a[1] += w.y * go[o];
+            a[2] += w.z * go[o];
+            a[3] += w.w * go[o];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            g2[J][r] = a[r] * (1.0f - h2[J][r] * h2[J][r]);
+            acc.db2[4 * J + r] += g2[J][r];
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            A[(16 * J + 4 * g + r) * SP + c] = g2[J][r];
+            Bs[(16 * J + 4 * g + r) * SP + c] = h1[J][r];
+        }
+    wave_sync();
+    // ---- dW2 += G2^T . H1 over the tile's samples
+    {
+        float4 a[4], bq[4];
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {
+            a[J] = ld4(&A[(16 * J + c) * SP + 4 * g]);
+            bq[J] = ld4(&Bs[(16 * J + c) * SP + 4 * g]);
+        }
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+#pragma unroll
+            for (int T = 0; T < 4; ++T) {
+                acc.d2[J][T] = mfma4(a[J].x, bq[T].x, acc.d2[J][T]);
+                acc.d2[J][T] = mfma4(a[J].y, bq[T].y, acc.d2[J][T]);
+                acc.d2[J][T] = mfma4(a[J].z, bq[T].z, acc.d2[J][T]);
+                acc.d2[J][T] = mfma4(a[J].w, bq[T].w, acc.d2[J][T]);
+            }
+    }
+    // ---- G1^T = (W2^T . G2^T) * (1 - H1^2)   (A operand W2[16J+4g+r][16I+c])
+    f4 g1[4];
+#pragma unroll
+    for (int I = 0; I < 4; ++I) {
+        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z = mfma4(S.w2[HEAD][(16 * J + 4 * g + r) * WP + 16 * I + c], g2[J][r], z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g1[I][r] = z[r] * (1.0f - h1[I][r] * h1[I][r]);
+    }
+    wave_sync();
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) A[(16 * J + 4 * g + r) * SP + c] = g1[J][r];
+    wave_sync();
+    // ---- [dW1 | db1] += G1^T . [X | 1]
+    const float4 xb = ld4(&Xs[c * SP + 4 * g]);
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+        const float4 a = ld4(&A[(16 * J + c) * SP + 4 * g]);
+        acc.d1[J] = mfma4(a.x, xb.x, acc.d1[J]);
+        acc.d1[J] = mfma4(a.y, xb.y, acc.d1[J]);
+        acc.d1[J] = mfma4(a.z, xb.z, acc.d1[J]);
+        acc.d1[J] = mfma4(a.w, xb.w, acc.d1[J]);
+    }
+}
+
+template <int HEAD>
+__device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pair, int lane) {
+    const int c = lane & 15, g = lane >> 4;
+    float* A = S.scr[2 * pair + HEAD];
+    float* Bs = A + 64 * SP;
+    float* Xs = A + 128 * SP;
+    float* GMs = A + 144 * SP;
+    Acc<HEAD> acc;
+    const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+#pragma unroll
+        for (int T = 0; T < 4; ++T) acc.d2[J][T] = zero;
+        acc.d1[J] = acc.d3[J] = zero;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc.db2[k] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(acc.sc) / sizeof(float)); ++k) acc.sc[k] = 0.0f;
+    const float inv_n = 1.0f / (float)P.mb;
+    const int ntiles = (P.mb + 15) / 16;
+    for (int t = blockIdx.x * NPAIR + pair; t < ntiles; t += gridDim.x * NPAIR)
+        mf_tile<HEAD>(S, P, A, Bs, Xs, GMs, c, g, t, inv_n, acc);
+
+    // ---- per-lane partials reduced over the 16 samples c of each g-group
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc.db2[k] = sum16(acc.db2[k]);
+    if constexpr (HEAD == 1) {
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc.d3[J][r] = sum16(acc.d3[J][r]);
+    }
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(acc.sc) / sizeof(float)); ++k) acc.sc[k] = sum16(acc.sc[k]);
+    __syncthreads();
+    // ---- phase 1: both W2 of every pair in its own region, summed in pair order
+    float* R = reinterpret_cast<float*>(&S);
+    {
+        float* Rp = R + pair * kW2Region + HEAD * H * H;
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int T = 0; T < 4; ++T) Rp[(16 * J + 4 * g + r) * H + 16 * T + c] = acc.d2[J][T][r];
+    }
+    __syncthreads();
+    float* out = P.ws + (size_t)blockIdx.x * PSTRIDE;
+    const int tid = threadIdx.x;
+    for (int q = tid; q < kW2Region; q += MT) {
+        float v = R[q];
+#pragma unroll
+        for (int pp = 1; pp < NPAIR; ++pp) v += R[pp * kW2Region + q];
+        out[(q < H * H ? O_AW2 : O_CW2 - H * H) + q] = v;
+    }
+    __syncthreads();
+    // ---- phase 2: everything else (1875 values), same scheme
+    {
+        float* Rp = R + pair * kRestRegion;
+        constexpr int o_w1 = HEAD == 0 ? O_AW1 : O_CW1, o_b1 = HEAD == 0 ? O_AB1 : O_CB1;
+        constexpr int o_b2 = HEAD == 0 ? O_AB2 : O_CB2;
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = 16 * J + 4 * g + r;
+                Rp[c < NOBS ? rest_slot(o_w1 + j * NOBS + c) : (c == NOBS ? rest_slot(o_b1 + j) : kRestDump)] =
+                    acc.d1[J][r];
+                if constexpr (HEAD == 0) {
+                    const int o = 4 * g + r;
+                    Rp[o < NACT ? rest_slot(O_AW3 + o * H + 16 * J + c) : kRestDump] = acc.d3[J][r];
+                } else {
+                    Rp[c == 0 ? rest_slot(O_CW3 + j) : kRestDump] = acc.d3[J][r];
+                }
+                Rp[c == 0 ? rest_slot(o_b2 + j) : kRestDump] = acc.db2[4 * J + r];
+            }
+        if (lane == 0) {
+            if constexpr (HEAD == 0) {
+#pragma unroll
+                for (int k = 0; k < NACT; ++k) {
+                    Rp[rest_slot(O_AB3 + k)] = acc.sc[k];
+                    Rp[rest_slot(O_LS + k)] = acc.sc[NACT + k];
+                }
+                Rp[rest_slot(NP + 0)] = acc.sc[2 * NACT + 0];
+                Rp[rest_slot(NP + 2)] = acc.sc[2 * NACT + 1];
+                Rp[rest_slot(NP + 3)] = acc.sc[2 * NACT + 2];
+                Rp[rest_slot(NP + 4)] = acc.sc[2 * NACT + 3];
+                Rp[rest_slot(NP + 5)] = acc.sc[2 * NACT + 4];
+            } else {
+                Rp[rest_slot(O_CB3)] = acc.sc[0];
+                Rp[rest_slot(NP + 1)] = acc.sc[1];
+            }
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < kRestDump; q += MT) {
+        float v = R[q];
+#pragma unroll
+        for (int pp = 1; pp < NPAIR; ++pp) v += R[pp * kRestRegion + q];
+        const int p = q < O_AW2 ? q : (q < O_AW2 + (O_CW2 - O_AB2) ? q - O_AW2 + O_AB2 : q - O_AW2 - (O_CW2 - O_AB2) + O_CB2);
+        out[p] = v;
+    }
+}
+
+__global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
+    __shared__ __attribute__((aligned(16))) MfmaLds S;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < H * H; i += MT) {
+        S.w2[0][(i >> 6) * WP + (i & 63)] = P.w.p[2][i];
+        S.w2[1][(i >> 6) * WP + (i & 63)] = P.w.p[9][i];
+    }
+    for (int i = tid; i < H * W1P; i += MT) {
+        const int j = i / W1P, k = i % W1P;
+        S.w1[0][i] = k < NOBS ? P.w.p[0][j * NOBS + k] : (k == NOBS ? P.w.p[1][j] : 0.0f);
+        S.w1[1][i] = k < NOBS ? P.w.p[7][j * NOBS + k] : (k == NOBS ? P.w.p[8][j] : 0.0f);
+    }
+    for (int i = tid; i < H; i += MT) {
+        S.b2[0][i] = P.w.p[3][i];
+        S.b2[1][i] = P.w.p[10][i];
+        S.w3[NACT * H + i] = P.w.p[11][i];
+    }
+    for (int i = tid; i < NACT * H; i += MT) S.w3[i] = P.w.p[4][i];
+    if (tid < NACT) {
+        S.b3[tid] = P.w.p[5][tid];
+        S.ls[tid] = P.w.p[6][tid];
+        S.isd[tid] = 1.0f / expf(P.w.p[6][tid]);
+    }
+    if (tid == NACT) {
+        S.b3[NACT] = P.w.p[12][0];
+        S.isd[NACT] = P.adv_stats ? 1.0f / (P.adv_stats[1] + 1e-8f) : 1.0f;
+    }
+    // X^T rows 10..15 stay zero (padding of the augmented K = 16)
+    for (int i = tid; i < (MT / 64) * 6 * SP; i += MT) S.scr[i / (6 * SP)][(138 + (i / SP) % 6) * SP + i % SP] = 0.0f;
+    __syncthreads();
+    const int wave = tid >> 6, lane = tid & 63;
+    if (wave & 1)
+        mf_wave<1>(S, P, wave >> 1, lane);
+    else
+        mf_wave<0>(S, P, wave >> 1, lane);
+}
+
+int grad_blocks(int mb) {
+    // RT_PPO_GRAD_BLOCKS caps the grid (tiles-per-wave experiments)
+    static const int cap = [] {
+        const char* e = std::getenv("RT_PPO_GRAD_BLOCKS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 && v < kMaxGradBlocks ? v : kMaxGradBlocks;
+    }();
+    const int tiles = (mb + 15) / 16;
+    const int b = (tiles + NPAIR - 1) / NPAIR;
+    return b < cap ? b : cap;
+}
+
+constexpr int kReduceCols = 64;
+constexpr int kReduceBlocks = (NP + NSTAT + kReduceCols - 1) / kReduceCols;
+constexpr int kNormSlots = 256;  // grad-norm partials at the workspace tail
+static_assert(kReduceBlocks <= kNormSlots, "norm partials");
+
 struct ReduceParams {
     const float* ws;
     int32_t nblk;
     Dst13 grad;
     float* stats;        // [6]
     float* stats_accum;  // [6] or null
+    float* norm_part;    // [kReduceBlocks] sum of squared gradients per block, or null
     float inv_n;
     float ent_coef;
 };
 
-// block: 64 columns; wave w sums rows w, w+4, ... (4 independent chains),
-// the 4 wave sums are combined in a fixed order (deterministic)
-__global__ __launch_bounds__(256) void k_ppo_reduce(ReduceParams P) {
-    __shared__ float part[4][64];
+// block: 64 columns; wave w of 16 sums rows w, w+16, ... (2 chains); the 16
+// wave sums are combined in a fixed order (deterministic).  Also emits the
+// block's share of ||grad||^2 for the clip in k_adam.
+__global__ __launch_bounds__(1024) void k_ppo_reduce(ReduceParams P) {
+    __shared__ float part[16][kReduceCols];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int p = blockIdx.x * 64 + lane;
+    const int p = blockIdx.x * kReduceCols + lane;
     const bool ok = p < NP + NSTAT;
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    float a0 = 0.0f, a1 = 0.0f;
     if (ok) {
         int b = w;
-        for (; b + 12 < P.nblk; b += 16) {
+        for (; b + 16 < P.nblk; b += 32) {
             a0 += P.ws[(size_t)b * PSTRIDE + p];
-            a1 += P.ws[(size_t)(b + 4) * PSTRIDE + p];
-            a2 += P.ws[(size_t)(b + 8) * PSTRIDE + p];
-            a3 += P.ws[(size_t)(b + 12) * PSTRIDE + p];
+            a1 += P.ws[(size_t)(b + 16) * PSTRIDE + p];
         }
-        for (; b < P.nblk; b += 4) a0 += P.ws[(size_t)b * PSTRIDE + p];
+        if (b < P.nblk) a0 += P.ws[(size_t)b * PSTRIDE + p];
     }
-    part[w][lane] = (a0 + a1) + (a2 + a3);
+    part[w][lane] = a0 + a1;
     __syncthreads();
-    if (w != 0 || !ok) return;
-    const float a = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
-    if (p < NP) {
-        int t = 0;
+    if (w != 0) return;
+    float a = 0.0f;
 #pragma unroll
-        for (int k = 1; k < 13; ++k) t += p >= kTensorOff[k] ? 1 : 0;
-        P.grad.p[t][p - kTensorOff[t]] = t == 6 ? a + -P.ent_coef : a;  // d(-ent_coef * mean(entropy)) / d logstd
-    } else {
-        const int k = p - NP;
-        float v = a * P.inv_n;
-        if (k == 1) v *= 0.5f;  // v_loss = 0.5 * mean(max(...))
-        P.stats[k] = v;
-        if (P.stats_accum) P.stats_accum[k] += v;
+    for (int k = 0; k < 16; ++k) a += part[k][lane];
+    float sq = 0.0f;
+    if (ok) {
+        if (p < NP) {
+            int t = 0;
+#pragma unroll
+            for (int k = 1; k < 13; ++k) t += p >= kTensorOff[k] ? 1 : 0;
+            if (t == 6) a += -P.ent_coef;  // d(-ent_coef * mean(entropy)) / d logstd
+            P.grad.p[t][p - kTensorOff[t]] = a;
+            sq = a * a;
+        } else {
+            const int k = p - NP;
+            float v = a * P.inv_n;
+            if (k == 1) v *= 0.5f;  // v_loss = 0.5 * mean(max(...))
+            P.stats[k] = v;
+            if (P.stats_accum) P.stats_accum[k] += v;
+        }
     }
+    sq = wave_sum(sq);
+    if (lane == 0 && P.norm_part) P.norm_part[blockIdx.x] = sq;
+}
+
+// ||grad||^2 partials of a flat gradient (after a data-parallel all-reduce)
+__global__ __launch_bounds__(256) void k_gnorm(const float* g, int64_t n, int64_t per_block, float* norm_part) {
+    __shared__ float part[4];
+    float a = 0.0f;
+    const int64_t lo = (int64_t)blockIdx.x * per_block, hi = lo + per_block < n ? lo + per_block : n;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) a += g[i] * g[i];
+    a = wave_sum(a);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) norm_part[blockIdx.x] = (part[0] + part[1]) + (part[2] + part[3]);
 }
 
 struct AdamParams {
@@ -410,6 +913,8 @@ struct AdamParams {
     float* grad;
     float* m;
     float* v;
+    const float* norm_part;  // [n_part] partial sums of squares
+    int32_t n_part;
     float max_norm;  // <= 0: no clipping
     float lerp_w;    // 1 - beta1
     float beta2, one_minus_beta2;
@@ -418,45 +923,50 @@ struct AdamParams {
     float eps;
 };
 
-__global__ __launch_bounds__(1024) void k_clip_adam(AdamParams P) {
-    __shared__ float part[16];
+// clip_grad_norm_ + torch.optim.Adam (foreach op order), one element per
+// thread; every block sums the norm partials in the same fixed order
+__global__ __launch_bounds__(256) void k_adam(AdamParams P) {
     __shared__ float coef_s;
-    const int tid = threadIdx.x;
-    float coef = 1.0f;
-    if (P.max_norm > 0.0f) {
-        float acc = 0.0f;
-        for (int64_t i = tid; i < P.n; i += 1024) acc += P.grad[i] * P.grad[i];
-        acc = wave_sum(acc);
-        if ((tid & 63) == 0) part[tid >> 6] = acc;
-        __syncthreads();
-        if (tid == 0) {
-            float t = 0.0f;
-            for (int w = 0; w < 16; ++w) t += part[w];
-            // clip_grad_norm_: coef = max_norm / (||g|| + 1e-6), clamped to 1
-            coef_s = fminf(P.max_norm / (sqrtf(t) + 1e-6f), 1.0f);
-        }
-        __syncthreads();
-        coef = coef_s;
+    if (threadIdx.x < 64) {
+        float t = 0.0f;
+        if (P.max_norm > 0.0f)
+            for (int k = threadIdx.x; k < P.n_part; k += 64) t += P.norm_part[k];
+        t = wave_sum(t);
+        // clip_grad_norm_: coef = max_norm / (||g|| + 1e-6), clamped to 1
+        if (threadIdx.x == 0) coef_s = P.max_norm > 0.0f ? fminf(P.max_norm / (sqrtf(t) + 1e-6f), 1.0f) : 1.0f;
     }
-    for (int64_t i = tid; i < P.n; i += 1024) {
-        const float g = P.grad[i] * coef;
-        P.grad[i] = g;
-        float m = P.m[i];
-        m = m + P.lerp_w * (g - m);                   // exp_avg.lerp_(grad, 1 - beta1)
-        float v = P.v[i] * P.beta2;                   // exp_avg_sq.mul_(beta2)
-        v = v + P.one_minus_beta2 * g * g;            //   .addcmul_(grad, grad, 1 - beta2)
-        const float denom = sqrtf(v) / P.bc2_sqrt + P.eps;
-        P.param[i] = P.param[i] + P.step_size * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
-        P.m[i] = m;
-        P.v[i] = v;
-    }
+    __syncthreads();
+    const float coef = coef_s;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= P.n) return;
+    const float g = P.grad[i] * coef;
+    P.grad[i] = g;
+    float m = P.m[i];
+    m = m + P.lerp_w * (g - m);                   // exp_avg.lerp_(grad, 1 - beta1)
+    float v = P.v[i] * P.beta2;                   // exp_avg_sq.mul_(beta2)
+    v = v + P.one_minus_beta2 * g * g;            //   .addcmul_(grad, grad, 1 - beta2)
+    const float denom = sqrtf(v) / P.bc2_sqrt + P.eps;
+    P.param[i] = P.param[i] + P.step_size * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
+    P.m[i] = m;
+    P.v[i] = v;
+}
+
+// RT_PPO_GRAD_KERNEL=valu selects the VALU kernel (A/B comparisons); default MFMA
+bool rt_ppo_use_mfma() {
+    static const int v = [] {
+        const char* e = std::getenv("RT_PPO_GRAD_KERNEL");
+        return (e && std::strcmp(e, "valu") == 0) ? 0 : 1;
+    }();
+    return v != 0;
 }
 
 int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* b,
                     const int64_t* idx_d, int32_t mb, const float* adv_stats_d, const rt_ppo_hparams* hp,
                     float* ws_d, int64_t ws_floats, float* stats_d, float* accum_d, hipStream_t st) {
-    const int nblk = (mb + TS - 1) / TS;
-    if ((int64_t)nblk * PSTRIDE > ws_floats) return rt_internal_fail(RT_EINVAL, "rt_ppo_grad: workspace too small");
+    const bool use_mfma = rt_ppo_use_mfma();
+    const int nblk = use_mfma ? grad_blocks(mb) : (mb + TS - 1) / TS;
+    if ((int64_t)nblk * PSTRIDE + kNormSlots > ws_floats)
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_grad: workspace too small");
     GradParams G{};
     ReduceParams R{};
     for (int i = 0; i < 13; ++i) {
@@ -478,21 +988,27 @@ int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const r
     G.clip_vloss = hp->clip_vloss;
     G.vf_coef = hp->vf_coef;
     G.ws = ws_d;
-    hipLaunchKernelGGL(k_ppo_grad, dim3(nblk), dim3(kThreads), 0, st, G);
+    if (use_mfma)
+        hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblk), dim3(MT), 0, st, G);
+    else
+        hipLaunchKernelGGL(k_ppo_grad, dim3(nblk), dim3(kThreads), 0, st, G);
     R.ws = ws_d;
     R.nblk = nblk;
     R.stats = stats_d;
     R.stats_accum = accum_d;
+    R.norm_part = ws_d + (ws_floats - kNormSlots);
     R.inv_n = 1.0f / (float)mb;
     R.ent_coef = hp->ent_coef;
-    hipLaunchKernelGGL(k_ppo_reduce, dim3((NP + NSTAT + 63) / 64), dim3(256), 0, st, R);
+    hipLaunchKernelGGL(k_ppo_reduce, dim3(kReduceBlocks), dim3(1024), 0, st, R);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
 }
 
+// norm_part: the kReduceBlocks partials k_ppo_reduce left (fresh = true), or
+// scratch for k_gnorm over the (all-reduced) flat gradient
 int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step, double lr,
-                const rt_ppo_hparams* hp, hipStream_t st) {
+                const rt_ppo_hparams* hp, float* norm_part, bool fresh, hipStream_t st) {
     AdamParams A{};
     A.n = n;
     A.param = p;
@@ -500,6 +1016,12 @@ int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step,
     A.m = m;
     A.v = v;
     A.max_norm = hp->max_grad_norm;
+    A.norm_part = norm_part;
+    A.n_part = kReduceBlocks;
+    if (A.max_norm > 0.0f && !fresh) {
+        const int64_t per = (n + kReduceBlocks - 1) / kReduceBlocks;
+        hipLaunchKernelGGL(k_gnorm, dim3(kReduceBlocks), dim3(256), 0, st, g, n, per, norm_part);
+    }
     const double b1 = hp->adam_beta1, b2 = hp->adam_beta2;
     // torch.optim.Adam (foreach): host-side scalars in double, applied in f32
     A.lerp_w = (float)(1.0 - b1);
@@ -508,7 +1030,7 @@ int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step,
     A.step_size = (float)(-(lr / (1.0 - std::pow(b1, (double)step))));
     A.bc2_sqrt = (float)std::pow(1.0 - std::pow(b2, (double)step), 0.5);
     A.eps = hp->adam_eps;
-    hipLaunchKernelGGL(k_clip_adam, dim3(1), dim3(1024), 0, st, A);
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
@@ -530,7 +1052,8 @@ bool bad_batch(const rt_ppo_batch* b) {
 
 extern "C" int64_t rt_ppo_workspace_floats(int32_t minibatch_size) {
     if (minibatch_size < 1) return 0;
-    return (int64_t)((minibatch_size + TS - 1) / TS) * PSTRIDE;
+    const int64_t a = (int64_t)((minibatch_size + TS - 1) / TS), b = grad_blocks(minibatch_size);
+    return (a > b ? a : b) * PSTRIDE + kNormSlots;
 }
 
 extern "C" int32_t rt_ppo_num_params(void) { return NP; }
@@ -548,10 +1071,10 @@ extern "C" int rt_ppo_grad(const float* const* params_d, float* const* grads_d, 
 }
 
 extern "C" int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp_avg_d, float* exp_avg_sq_d,
-                            int64_t step, double lr, const rt_ppo_hparams* hp, void* stream) {
-    if (n < 1 || !param_d || !grad_d || !exp_avg_d || !exp_avg_sq_d || step < 1 || !hp)
+                            int64_t step, double lr, const rt_ppo_hparams* hp, float* workspace_d, void* stream) {
+    if (n < 1 || !param_d || !grad_d || !exp_avg_d || !exp_avg_sq_d || step < 1 || !hp || !workspace_d)
         return rt_internal_fail(RT_EINVAL, "rt_adam_step: bad argument");
-    return adam_launch(n, param_d, grad_d, exp_avg_d, exp_avg_sq_d, step, lr, hp,
+    return adam_launch(n, param_d, grad_d, exp_avg_d, exp_avg_sq_d, step, lr, hp, workspace_d, false,
                        reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -572,7 +1095,8 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
                                  adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,
                                  stats_d, stats_accum_d, st);
         if (rc) return rc;
-        rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, st);
+        rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp,
+                         workspace_d + (workspace_floats - kNormSlots), true, st);
         if (rc) return rc;
     }
     return RT_OK;

@@ -142,6 +142,7 @@ class PPOTrainer:
                 ent_coef=float(cfg.ent_coef), vf_coef=float(cfg.vf_coef), max_grad_norm=float(cfg.max_grad_norm),
                 adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
             self._ws = torch.empty(int(L.rt_ppo_workspace_floats(self.minibatch_size)), **kw)
+            self._norm_ws = torch.empty(256, **kw)
         self.next_obs = None
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
@@ -390,7 +391,8 @@ class PPOTrainer:
                     self._adam_step += 1
                     _lib.check(L.rt_adam_step(n, self.flat_param.data_ptr(), self.flat_grad.data_ptr(),
                                               self._exp_avg.data_ptr(), self._exp_avg_sq.data_ptr(),
-                                              self._adam_step, lr, hp, stream), "rt_adam_step")
+                                              self._adam_step, lr, hp, self._norm_ws.data_ptr(), stream),
+                               "rt_adam_step")
             done += k
             if self.max_minibatches and done >= self.max_minibatches:
                 break

@@ -203,6 +203,7 @@ def test_fused_adam_matches_torch(max_norm):
     ref = p0.clone().requires_grad_(True)
     opt = torch.optim.Adam([ref], lr=3e-4, eps=1e-5, foreach=True)
     mine, m, v = p0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    ws = torch.empty(256, device=dev)
     hp = _lib.RtPpoHparams(clip_coef=0.1, clip_vloss=1, norm_adv=1, ent_coef=0.0, vf_coef=0.5,
                            max_grad_norm=max_norm, adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
     import ctypes
@@ -217,7 +218,7 @@ def test_fused_adam_matches_torch(max_norm):
         opt.step()
         gm = grad.clone()
         _lib.check(L.rt_adam_step(n, mine.data_ptr(), gm.data_ptr(), m.data_ptr(), v.data_ptr(), step, lr,
-                                  ctypes.byref(hp), None), "rt_adam_step")
+                                  ctypes.byref(hp), ws.data_ptr(), None), "rt_adam_step")
         torch.cuda.synchronize()
         torch.testing.assert_close(gm, ref.grad, rtol=1e-6, atol=1e-9)
         torch.testing.assert_close(mine, ref.detach(), rtol=1e-6, atol=1e-7)
