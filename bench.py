@@ -16,6 +16,10 @@ Also reported:
                          gradient all-reduce per step when n_gpus > 1)
   train_env_steps_per_s  env steps/s of a full PPO iteration
                          (64 rollout steps + GAE + 80 updates)
+  update_mfma            the fused update (rt_ppo_update) vs the f32 MFMA peak
+  other_step_mode        the same rollout + iteration with the other env step
+                         formulation (incremental, SURVEY §8 f-2: bitwise-equal
+                         rewards/termination, touches only the beam's voxels)
   roofline               k_dense (the dominant kernel) vs HBM: HIP events the
                          library records around it on the env stream over
                          the timed region; traffic from profiles/k_dense_pmc.json
@@ -41,6 +45,9 @@ sys.path.insert(0, REPO)
 
 METRIC = "env steps/sec (whole node) + PPO updates/sec, visionless 64³ voxel, 1/2/4/8 GPU"
 HBM_PEAK = 8.0e12  # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
+F32_MFMA_PEAK = 157.3e12  # dense f32 MFMA (= f32 vector) peak, FLOP/s (MI355X_MICROARCH.md)
+UPDATE_MACS_PER_SAMPLE = (9 * 64 + 64 * 64 + 64 * 6) + (9 * 64 + 64 * 64 + 64) \
+    + (2 * 64 * 6 + 2 * 64 * 64 + 9 * 64) + (2 * 64 + 2 * 64 * 64 + 9 * 64)
 
 
 def parse():
@@ -229,6 +236,13 @@ def main():
         upd = {"ppo_updates_per_s": n_upd / du, "ppo_update_ms": 1000 * du / n_upd,
                "minibatch_size_per_gpu": tr.minibatch_size, "update_minibatches_timed": n_upd,
                "train_env_steps_per_s": total_envs * T / di, "train_iteration_s": di}
+        if tr.fused_update:
+            # MLP forward + backward of both heads: 28,224 MACs per sample
+            # (DESIGN.md §3); whole minibatch step (grad + reduce + clip/Adam + epoch overheads)
+            fl = 2 * UPDATE_MACS_PER_SAMPLE * tr.minibatch_size
+            upd["update_mfma"] = {"bound": "mfma", "flop_per_minibatch": fl,
+                                  "achieved": fl / (du / n_upd) / 1e12, "peak": F32_MFMA_PEAK / 1e12,
+                                  "unit": "TFLOP/s", "frac": fl / (du / n_upd) / F32_MFMA_PEAK}
 
     # ---------------- roofline of the dominant kernel, k_dense
     V = int(np.prod(grid))
@@ -269,6 +283,16 @@ def main():
         env_ms2 = sum(max_over_ranks(v) for v in k2.values())
         other = {"step_mode": other_mode, "env_steps_per_s": total_envs * K / d2, "ms_per_step": 1000 * d2 / K,
                  "env_kernels_ms": k2, "env_only_kernel_steps_per_s": total_envs / (env_ms2 * 1e-3)}
+        if not a.no_update:
+            barrier()
+            t0 = time.perf_counter()
+            tr.rollout()
+            tr.compute_gae()
+            tr.update()
+            torch.cuda.synchronize()
+            barrier()
+            di2 = max_over_ranks(time.perf_counter() - t0)
+            other.update({"train_env_steps_per_s": total_envs * T / di2, "train_iteration_s": di2})
         env = env2
     if a.vision:
         roof["mfma_note"] = "C3D convolutions run in MIOpen (f32); the env roofline above is k_dense_vis"
