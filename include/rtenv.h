@@ -14,6 +14,8 @@
  *   beam_voxels               draw_line.py:4    | rt_debug_beam (parity hook)
  *   apply_rotation/translation transforms.py:7,62| rt_debug_pose (parity hook)
  *   GAE loop                  train.py:163-181  | rt_gae
+ *   agent.get_action_and_value train.py:143-149 | rt_policy_sample (visionless agent)
+ *   PPO minibatch step        train.py:197-246  | rt_ppo_grad + rt_adam_step / rt_ppo_update
  *
  * Conventions
  *  - Plain pointers and sizes only; `*_d` arguments are DEVICE pointers
