@@ -16,6 +16,7 @@
  *   GAE loop                  train.py:163-181  | rt_gae
  *   agent.get_action_and_value train.py:143-149 | rt_policy_sample (visionless agent)
  *   PPO minibatch step        train.py:197-246  | rt_ppo_grad + rt_adam_step / rt_ppo_update
+ *   FeaturesExtractor3D.cnn   networks.py:8-45  | rt_conv_relu_pool_fwd (+ backward kernels)
  *
  * Conventions
  *  - Plain pointers and sizes only; `*_d` arguments are DEVICE pointers
@@ -243,6 +244,26 @@ int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_
                   const rt_ppo_hparams* hp, float* flat_param_d, float* flat_grad_d, float* exp_avg_d,
                   float* exp_avg_sq_d, int64_t n_flat, int64_t step0, double lr, float* workspace_d,
                   int64_t workspace_floats, float* stats_d, float* stats_accum_d, void* stream);
+
+/* ---- C3D feature extractor of the vision agent (networks.py:8-45) ----------
+ * One stage = Conv3d(cin, 16, 3, groups) + ReLU + MaxPool3d(2, 2, pool_pad):
+ * stage 1 (4, 1, pad (S_i - 2) % 2), stage 2 (16, 2, 0), stage 3 (16, 4, 0).
+ * Tensors are NCDHW f32; weights as torch ([16][cin/groups][3][3][3], [16]). */
+typedef struct rt_conv_layer {
+    int32_t cin;          /* 4 or 16 */
+    int32_t groups;       /* 1 (cin 4); 1, 2 or 4 (cin 16) */
+    int32_t in_dims[3];   /* D, H, W of the input */
+    int32_t pool_pad[3];  /* 0 or 1 per axis */
+} rt_conv_layer;
+
+/* Pooled output dims of a stage. */
+int rt_conv_out_dims(const rt_conv_layer* layer, int32_t* out_dims);
+
+/* y[b] = maxpool(relu(conv(x[rows[b]]) + bias)) for b < batch (rows_d NULL:
+ * row b).  argmax_d (u8, shape of y, NULL for inference): bits 0-2 = index of
+ * the window's first maximum in (z, y, x) order, bit 3 = max > 0. */
+int rt_conv_relu_pool_fwd(const rt_conv_layer* layer, int32_t batch, const float* x_d, const int64_t* rows_d,
+                          const float* w_d, const float* b_d, float* y_d, uint8_t* argmax_d, void* stream);
 
 const char* rt_last_error(void);
 int rt_abi_version(void);

@@ -13,7 +13,8 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "rtenv.hip")
-SRCS = [SRC, os.path.join(PKG, "csrc", "policy.hip"), os.path.join(PKG, "csrc", "ppo_update.hip")]
+SRCS = [SRC, os.path.join(PKG, "csrc", "policy.hip"), os.path.join(PKG, "csrc", "ppo_update.hip"),
+        os.path.join(PKG, "csrc", "c3d.hip")]
 HDR = os.path.join(REPO, "include", "rtenv.h")
 OUT = os.path.join(PKG, "librtenv.so")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
