@@ -46,6 +46,8 @@ sys.path.insert(0, REPO)
 METRIC = "env steps/sec (whole node) + PPO updates/sec, visionless 64³ voxel, 1/2/4/8 GPU"
 HBM_PEAK = 8.0e12  # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
 F32_MFMA_PEAK = 157.3e12  # dense f32 MFMA (= f32 vector) peak, FLOP/s (MI355X_MICROARCH.md)
+# C3D forward FLOPs per sample at 64^3 (convolutions; SURVEY §8 a-15: 0.999 GFLOP)
+C3D_FWD_FLOP_64 = 2 * (16 * 4 * 27 * 62 ** 3 + 16 * 8 * 27 * 29 ** 3 + 16 * 4 * 27 * 12 ** 3)
 UPDATE_MACS_PER_SAMPLE = (9 * 64 + 64 * 64 + 64 * 6) + (9 * 64 + 64 * 64 + 64) \
     + (2 * 64 * 6 + 2 * 64 * 64 + 9 * 64) + (2 * 64 + 2 * 64 * 64 + 9 * 64)
 
@@ -295,7 +297,22 @@ def main():
             other.update({"train_env_steps_per_s": total_envs * T / di2, "train_iteration_s": di2})
         env = env2
     if a.vision:
-        roof["mfma_note"] = "C3D convolutions run in MIOpen (f32); the env roofline above is k_dense_vis"
+        roof["note"] = "vision: the env kernel above is k_dense_vis; the policy is C3D on f32 MFMA (c3d_mfma)"
+        # C3D forward of one rollout step (512 envs), timed separately on the same agent
+        fe = agent.features_extractor
+        xo = env.obs
+        with torch.no_grad():
+            fe(xo)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(4):
+                fe(xo)
+            torch.cuda.synchronize()
+        dfe = (time.perf_counter() - t0) / 4
+        fl = C3D_FWD_FLOP_64 * a.envs if a.grid == 64 else None
+        roof["c3d_mfma"] = {"bound": "mfma", "forward_ms": dfe * 1e3, "flop": fl,
+                            "achieved": fl / dfe / 1e12 if fl else None, "peak": F32_MFMA_PEAK / 1e12,
+                            "unit": "TFLOP/s", "frac": fl / dfe / F32_MFMA_PEAK if fl else None}
     out = {"metric": METRIC, "value": steps_per_s, "unit": "env steps/s", "n_gpus": world, "steps": K,
            "warmup": a.warmup, "ms_per_step": 1000 * dt / K, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "f32", "data": "synthetic",

@@ -265,6 +265,18 @@ int rt_conv_out_dims(const rt_conv_layer* layer, int32_t* out_dims);
 int rt_conv_relu_pool_fwd(const rt_conv_layer* layer, int32_t batch, const float* x_d, const int64_t* rows_d,
                           const float* w_d, const float* b_d, float* y_d, uint8_t* argmax_d, void* stream);
 
+/* Weight/bias gradient of a stage from the pooled-output gradient dy_d and the
+ * forward's argmax bytes: dW [16][cin/groups][27], db [16] (written).
+ * workspace_d: rt_conv_wgrad_workspace_floats(layer, batch) floats. */
+int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* layer, int32_t batch);
+int rt_conv_relu_pool_wgrad(const rt_conv_layer* layer, int32_t batch, const float* x_d, const int64_t* rows_d,
+                            const float* dy_d, const uint8_t* argmax_d, float* dw_d, float* db_d,
+                            float* workspace_d, int64_t workspace_floats, void* stream);
+
+/* Gradient w.r.t. the stage input (cin 16 stages): dx [B][16][D][H][W]. */
+int rt_conv_relu_pool_dgrad(const rt_conv_layer* layer, int32_t batch, const float* w_d, const float* dy_d,
+                            const uint8_t* argmax_d, float* dx_d, void* stream);
+
 const char* rt_last_error(void);
 int rt_abi_version(void);
 

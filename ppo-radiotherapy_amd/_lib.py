@@ -32,7 +32,8 @@ EXPORTS = [
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
-    "rt_conv_out_dims", "rt_conv_relu_pool_fwd",
+    "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
+    "rt_conv_relu_pool_dgrad",
     "rt_last_error", "rt_abi_version",
 ]
 
@@ -142,6 +143,10 @@ def load(build_if_missing: bool = True):
                           ctypes.c_int),
         "rt_conv_out_dims": ([ctypes.POINTER(RtConvLayer), ctypes.POINTER(i32)], ctypes.c_int),
         "rt_conv_relu_pool_fwd": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "rt_conv_wgrad_workspace_floats": ([ctypes.POINTER(RtConvLayer), i32], i64),
+        "rt_conv_relu_pool_wgrad": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp, vp, vp, i64, vp],
+                                    ctypes.c_int),
+        "rt_conv_relu_pool_dgrad": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_last_error": ([], ctypes.c_char_p),
         "rt_abi_version": ([], ctypes.c_int),
     }

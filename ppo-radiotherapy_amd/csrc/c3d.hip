@@ -184,31 +184,20 @@ __device__ __forceinline__ void load_tile(float* xs, const float* xb, const Geom
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's copies have landed (barrier follows)
 }
 
-template <int CIN, int G, int PZB, int PYB>
-__global__ __launch_bounds__(kThreads) void k_conv_relu_pool(FwdParams P) {
-    extern __shared__ float xs[];
+// The MFMA main loop shared by the forward and the data-gradient kernels: the
+// block's LDS tile xs holds a [cin][ZL][YL][XL] input region; rows r of
+// (tz, ty) = (r / PYB, r % PYB) times x-tile pairs (tx, tx + 1) are spread
+// round-robin over the 4 wavefronts; tile (r, tx) covers the 2x2x4 positions
+// at LDS (2tz, 2ty, 4tx).  epi(acc[2], r, xp) consumes the two tiles' D
+// (lane (c, g): rows 4g..4g+3, position c).
+template <int CIN, int PYB, class Epi>
+__device__ __forceinline__ void conv_core(const float* xs, const float (&af)[nsteps<CIN>()], const Geom& g,
+                                          int nrows, Epi&& epi) {
     constexpr int NS = nsteps<CIN>();
-    const Geom& g = P.g;
-    const int b = blockIdx.z, pz0 = blockIdx.y * PZB, py0 = blockIdx.x * PYB;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, gq = lane >> 4;
-    const int64_t srow = P.rows ? P.rows[b] : b;
-    const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
-    const int z0 = 2 * pz0 - g.pd, y0 = 2 * py0 - g.ph, x0 = -g.pw;
-    load_tile<CIN>(xs, xb, g, z0, y0, x0);
-    float af[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) af[s] = a_frag<CIN, G>(P.w, s, c, gq);
-    float bias[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bias[r] = P.bias[4 * gq + r];
-    __syncthreads();
-
     const int zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
-    const int widx = zc * 4 + yc * 2 + (xc & 1);
     const int lane_base = gq * g.CS + zc * g.ZS + yc * g.YS + xc;
-    // work items: pairs of x-adjacent tiles (tx, tx + 1) of one (tz, ty) row,
-    // distributed round-robin over the 4 wavefronts; (row, xp) advance incrementally
-    const int nxp = (g.XT + 1) / 2, nrows = PZB * PYB;
+    const int nxp = (g.XT + 1) / 2;
     int row = 0, xp = wave;
     while (xp >= nxp) {
         xp -= nxp;
@@ -258,6 +247,41 @@ __global__ __launch_bounds__(kThreads) void k_conv_relu_pool(FwdParams P) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMAs
             }
         }
+        epi(acc, row, xp);
+        row = nrow;
+        xp = nx;
+    };
+    while (row < nrows) {
+        item(std::integral_constant<int, 0>{});
+        if constexpr (NJ % 2 == 1) {
+            if (row >= nrows) break;
+            item(std::integral_constant<int, 1>{});
+        }
+    }
+}
+
+template <int CIN, int G, int PZB, int PYB>
+__global__ __launch_bounds__(kThreads) void k_conv_relu_pool(FwdParams P) {
+    extern __shared__ float xs[];
+    constexpr int NS = nsteps<CIN>();
+    const Geom& g = P.g;
+    const int b = blockIdx.z, pz0 = blockIdx.y * PZB, py0 = blockIdx.x * PYB;
+    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
+    const int64_t srow = P.rows ? P.rows[b] : b;
+    const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
+    const int z0 = 2 * pz0 - g.pd, y0 = 2 * py0 - g.ph, x0 = -g.pw;
+    load_tile<CIN>(xs, xb, g, z0, y0, x0);
+    float af[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) af[s] = a_frag<CIN, G>(P.w, s, c, gq);
+    float bias[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[r] = P.bias[4 * gq + r];
+    __syncthreads();
+
+    const int zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
+    const int widx = zc * 4 + yc * 2 + (xc & 1);
+    conv_core<CIN, PYB>(xs, af, g, PZB * PYB, [&](const f4 (&acc)[2], int row, int xp) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int tx = 2 * xp + u;
@@ -279,16 +303,203 @@ __global__ __launch_bounds__(kThreads) void k_conv_relu_pool(FwdParams P) {
                 }
             }
         }
-        row = nrow;
-        xp = nx;
-    };
-    while (row < nrows) {
-        item(std::integral_constant<int, 0>{});
-        if constexpr (NJ % 2 == 1) {
-            if (row >= nrows) break;
-            item(std::integral_constant<int, 1>{});
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Gradient of the conv-output (pre-pool, post-ReLU-mask) at conv position
+// (cz, cy, cx) of channel co: the pooled gradient if that position is its
+// window's recorded maximum and the ReLU was active, else 0.
+__device__ __forceinline__ float dy_at(const float* dP, const uint8_t* am, const Geom& g, int64_t plane, int cz,
+                                       int cy, int cx) {
+    if (cz < 0 || cz >= g.cd || cy < 0 || cy >= g.ch || cx < 0 || cx >= g.cw) return 0.0f;
+    const int qz = cz + g.pd, qy = cy + g.ph, qx = cx + g.pw;
+    const int pz = qz >> 1, py = qy >> 1, px = qx >> 1;
+    if (pz >= g.PD || py >= g.PH || px >= g.PW) return 0.0f;  // dropped by the floor of the pooled size
+    const int64_t o = plane + ((int64_t)pz * g.PH + py) * g.PW + px;
+    const int byte = am[o];
+    return ((byte & 8) && (byte & 7) == ((qz & 1) * 4 + (qy & 1) * 2 + (qx & 1))) ? dP[o] : 0.0f;
+}
+
+struct DgradParams {
+    const float* w;    // stage weights [16][16/G][27]
+    const float* dP;   // [B][16][PD][PH][PW]
+    const uint8_t* am; // same shape
+    float* dx;         // [B][16][D][H][W]
+    Geom g;            // D,H,W = stage input = dx dims; XT = x tiles of 4 over W
+};
+
+// dX[ci][p] = sum_{co, t} W[co][ci][t] dY[co][p - t]: the forward main loop over
+// the zero-padded dY region with flipped, transposed weights
+template <int G, int PZB, int PYB>
+__global__ __launch_bounds__(kThreads) void k_conv_dgrad(DgradParams P) {
+    extern __shared__ float xs[];
+    constexpr int NS = nsteps<16>();
+    const Geom& g = P.g;
+    const int b = blockIdx.z, z0 = blockIdx.y * 2 * PZB, y0 = blockIdx.x * 2 * PYB;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, gq = lane >> 4;
+    // stage dY[co][z0-2 .., y0-2 .., -2 ..] into LDS (zero outside)
+    for (int r = wave; r < CO * g.ZL * g.YL; r += kThreads / 64) {
+        const int co = r / (g.ZL * g.YL), zz = (r / g.YL) % g.ZL, yy = r % g.YL;
+        const int64_t plane = ((int64_t)b * CO + co) * g.PD * g.PH * g.PW;
+        float* dst = xs + co * g.CS + zz * g.ZS + yy * g.YS;
+        for (int xx = lane; xx < g.XL; xx += 64) dst[xx] = dy_at(P.dP, P.am, g, plane, z0 + zz - 2, y0 + yy - 2, xx - 2);
+    }
+    float af[NS];
+    constexpr int cpg = CO / G;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int q = s % 27, co = 4 * (s / 27) + gq;  // lane group = dY channel, row c = dX channel
+        const int gi = c / cpg, go = co / cpg;
+        af[s] = gi == go ? P.w[(co * cpg + (c - gi * cpg)) * 27 + (26 - q)] : 0.0f;
+    }
+    __syncthreads();
+    const int zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
+    conv_core<16, PYB>(xs, af, g, PZB * PYB, [&](const f4 (&acc)[2], int row, int xp) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int tx = 2 * xp + u;
+            const int z = z0 + 2 * (row / PYB) + zc, y = y0 + 2 * (row % PYB) + yc, x = 4 * tx + xc;
+            if (z < g.D && y < g.H && x < g.W) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    P.dx[((((size_t)b * CO + 4 * gq + r) * g.D + z) * g.H + y) * g.W + x] = acc[u][r];
+            }
+        }
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient: D[co][k'] += sum_pos dY[co][pos] * X[ci][pos + tap],
+// k' = ci * 27 + tap (column CIN*27 = the constant 1 -> db).  A (dY) is built
+// per lane from the pooled gradient + argmax byte: lane (c, g) holds channel
+// co = c at the 4 positions n = 4q + g of a tile, which all lie in window
+// g >> 1.  B is gathered from the same LDS input tile as the forward.
+// Persistent: each block loops over (sample, region) items and keeps its
+// column tiles in MFMA accumulators; conv1 splits positions over the 4 waves
+// (7 column tiles each, summed through LDS), conv2/3 split the 28 column tiles.
+template <int CIN>
+constexpr int ncol_tiles() {
+    return (CIN * 27 + 1 + 15) / 16;
+}
+constexpr int kWgradTiles = 7;  // column tiles per wave
+
+struct WgradParams {
+    const float* x;
+    const int64_t* rows;
+    const float* dP;
+    const uint8_t* am;
+    float* part;  // [gridDim.x][16 * ncol * 16]
+    int32_t B;
+    int32_t nby, nbz;  // regions per sample (as the forward grid)
+    Geom g;
+};
+
+template <int CIN, int PZB, int PYB>
+__global__ __launch_bounds__(kThreads) void k_conv_wgrad(WgradParams P) {
+    extern __shared__ float xs[];
+    constexpr int NCT = ncol_tiles<CIN>();
+    constexpr int WP = CIN == 4 ? 4 : 1;  // waves splitting the positions
+    static_assert(CIN != 4 || NCT == kWgradTiles, "conv1 columns");
+    static_assert(CIN != 16 || NCT == 4 * kWgradTiles, "conv2/3 columns");
+    const Geom& g = P.g;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, gq = lane >> 4;
+    const int t0c = WP == 4 ? 0 : wave * kWgradTiles;  // first column tile of this wave
+    // per column tile: LDS offset of (ci, tap) of column 16T + c, or a constant
+    int koff[kWgradTiles];
+    float kconst[kWgradTiles];  // -1: gather; else the constant B value
+#pragma unroll
+    for (int t = 0; t < kWgradTiles; ++t) {
+        const int k = 16 * (t0c + t) + c;
+        if (k < CIN * 27) {
+            const int ci = k / 27, q = k % 27;
+            koff[t] = ci * g.CS + (q / 9) * g.ZS + ((q / 3) % 3) * g.YS + q % 3;
+            kconst[t] = -1.0f;
+        } else {
+            koff[t] = 0;
+            kconst[t] = k == CIN * 27 ? 1.0f : 0.0f;
         }
     }
+    f4 acc[kWgradTiles];
+#pragma unroll
+    for (int t = 0; t < kWgradTiles; ++t) acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int items = P.B * P.nbz * P.nby;
+    const int nxt = g.XT, ntile = PZB * PYB * nxt;
+    for (int it = blockIdx.x; it < items; it += gridDim.x) {
+        const int b = it / (P.nbz * P.nby), rz = (it / P.nby) % P.nbz, ry = it % P.nby;
+        const int pz0 = rz * PZB, py0 = ry * PYB;
+        const int64_t srow = P.rows ? P.rows[b] : b;
+        __syncthreads();  // the previous item's reads of xs are done
+        load_tile<CIN>(xs, P.x + srow * (int64_t)CIN * g.D * g.H * g.W, g, 2 * pz0 - g.pd, 2 * py0 - g.ph, -g.pw);
+        __syncthreads();
+        const int64_t plane = ((int64_t)b * CO + c) * g.PD * g.PH * g.PW;
+        for (int t = (WP == 4 ? wave : 0); t < ntile; t += WP) {
+            const int tz = t / (PYB * nxt), ty = (t / nxt) % PYB, tx = t % nxt;
+            const int pz = pz0 + tz, py = py0 + ty, px = 2 * tx + (gq >> 1);
+            float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (pz < g.PD && py < g.PH && px < g.PW) {
+                const int64_t o = plane + ((int64_t)pz * g.PH + py) * g.PW + px;
+                const int byte = P.am[o];
+                if (byte & 8) {
+                    const float d = P.dP[o];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)  // position n = 4q + g: zc = q >> 1, yc = q & 1, xc = g
+                        a[q] = (byte & 7) == ((q >> 1) * 4 + (q & 1) * 2 + (gq & 1)) ? d : 0.0f;
+                }
+            }
+            const int tb = 2 * tz * g.ZS + 2 * ty * g.YS + 4 * tx + gq;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int pb = tb + (q >> 1) * g.ZS + (q & 1) * g.YS;
+#pragma unroll
+                for (int T = 0; T < kWgradTiles; ++T) {
+                    const float bv = kconst[T] < 0.0f ? xs[pb + koff[T]] : kconst[T];
+                    acc[T] = mfma4(a[q], bv, acc[T]);
+                }
+            }
+        }
+    }
+    // D (lane (c, g)): rows co = 4g + r, column 16T + c
+    float* out = P.part + (size_t)blockIdx.x * (CO * NCT * 16);
+    if constexpr (WP == 1) {
+#pragma unroll
+        for (int T = 0; T < kWgradTiles; ++T)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(4 * gq + r) * (NCT * 16) + 16 * (t0c + T) + c] = acc[T][r];
+    } else {
+        __syncthreads();
+        float* R = xs;  // 4 wave regions of 16 x 112 (after the last item)
+#pragma unroll
+        for (int T = 0; T < kWgradTiles; ++T)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) R[wave * (CO * NCT * 16) + (4 * gq + r) * (NCT * 16) + 16 * T + c] = acc[T][r];
+        __syncthreads();
+        for (int i = threadIdx.x; i < CO * NCT * 16; i += kThreads)
+            out[i] = (R[i] + R[CO * NCT * 16 + i]) + (R[2 * CO * NCT * 16 + i] + R[3 * CO * NCT * 16 + i]);
+    }
+}
+
+// sum of the block partials -> dW [16][cin/G][27] (in-group columns) and db [16]
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* part, int nblk, int cin, int groups, int ncol,
+                                                      float* dw, float* db) {
+    const int cpg = cin / groups, nw = CO * cpg * 27;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i > nw + CO - 1) return;
+    int co, col;
+    if (i < nw) {
+        co = i / (cpg * 27);
+        const int rem = i % (cpg * 27), cil = rem / 27, q = rem % 27;
+        col = ((co / (CO / groups)) * cpg + cil) * 27 + q;
+    } else {
+        co = i - nw;
+        col = cin * 27;
+    }
+    float a = 0.0f;
+    for (int k = 0; k < nblk; ++k) a += part[(size_t)k * CO * ncol + co * ncol + col];
+    if (i < nw)
+        dw[i] = a;
+    else
+        db[co] = a;
 }
 
 template <int CIN, int G, int PZB, int PYB>
@@ -312,6 +523,87 @@ int launch_fwd(const rt_conv_layer* L, int32_t B, const float* x, const int64_t*
     }
     dim3 grid((P.g.PH + PYB - 1) / PYB, (P.g.PD + PZB - 1) / PZB, B);
     hipLaunchKernelGGL((k_conv_relu_pool<CIN, G, PZB, PYB>), grid, dim3(kThreads), lds, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+template <int PZB, int PYB>
+Geom make_dgrad_geom(const rt_conv_layer* L) {
+    Geom g = make_geom<PZB, PYB>(L);
+    g.XT = (g.W + 3) / 4;
+    g.XL = 4 * g.XT + 2;
+    g.YS = round_mod(g.XL, 4);
+    g.ZS = round_mod(g.YL * g.YS, 8);
+    g.CS = round_mod(g.ZL * g.ZS, 16);
+    return g;
+}
+
+template <class K>
+void allow_big_lds(K* kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+
+template <int G, int PZB, int PYB>
+int launch_dgrad(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am, float* dx,
+                 hipStream_t st) {
+    DgradParams P{};
+    P.g = make_dgrad_geom<PZB, PYB>(L);
+    P.w = w;
+    P.dP = dP;
+    P.am = am;
+    P.dx = dx;
+    const size_t lds = (size_t)CO * P.g.CS * sizeof(float);
+    if (lds > 160 * 1024) return rt_internal_fail(RT_ELIMIT, "rt_conv_dgrad: tile exceeds LDS");
+    static bool attr = false;
+    if (!attr) {
+        allow_big_lds(&k_conv_dgrad<G, PZB, PYB>);
+        attr = true;
+    }
+    dim3 grid((P.g.H + 2 * PYB - 1) / (2 * PYB), (P.g.D + 2 * PZB - 1) / (2 * PZB), B);
+    hipLaunchKernelGGL((k_conv_dgrad<G, PZB, PYB>), grid, dim3(kThreads), lds, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+constexpr int kWgradBlocks = 512;
+
+template <int CIN, int PZB, int PYB>
+int wgrad_blocks(const rt_conv_layer* L, int32_t B) {
+    const Geom g = make_geom<PZB, PYB>(L);
+    const int64_t items = (int64_t)B * ((g.PD + PZB - 1) / PZB) * ((g.PH + PYB - 1) / PYB);
+    return (int)(items < kWgradBlocks ? items : kWgradBlocks);
+}
+
+template <int CIN, int PZB, int PYB>
+int launch_wgrad(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
+                 const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
+    WgradParams P{};
+    P.g = make_geom<PZB, PYB>(L);
+    P.x = x;
+    P.rows = rows;
+    P.dP = dP;
+    P.am = am;
+    P.B = B;
+    P.nby = (P.g.PH + PYB - 1) / PYB;
+    P.nbz = (P.g.PD + PZB - 1) / PZB;
+    P.part = ws;
+    constexpr int NCT = ncol_tiles<CIN>();
+    const int nblk = wgrad_blocks<CIN, PZB, PYB>(L, B);
+    if ((int64_t)nblk * CO * NCT * 16 > ws_floats) return rt_internal_fail(RT_EINVAL, "rt_conv_wgrad: workspace too small");
+    const size_t lds = (size_t)CIN * P.g.CS * sizeof(float);
+    if (lds > 160 * 1024) return rt_internal_fail(RT_ELIMIT, "rt_conv_wgrad: tile exceeds LDS");
+    static bool attr = false;
+    if (!attr) {
+        allow_big_lds(&k_conv_wgrad<CIN, PZB, PYB>);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_conv_wgrad<CIN, PZB, PYB>), dim3(nblk), dim3(kThreads), lds, st, P);
+    const int nout = CO * (L->cin / L->groups) * 27 + CO;
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((nout + 255) / 256), dim3(256), 0, st, (const float*)ws, nblk, L->cin,
+                       L->groups, NCT * 16, dw, db);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
@@ -347,4 +639,30 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     if (L->groups == 1) return launch_fwd<16, 1, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     if (L->groups == 2) return launch_fwd<16, 2, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     return launch_fwd<16, 4, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+}
+
+extern "C" int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* L, int32_t batch) {
+    if (bad_layer(L) || batch < 1) return 0;
+    if (L->cin == 4) return (int64_t)wgrad_blocks<4, 2, 4>(L, batch) * CO * ncol_tiles<4>() * 16;
+    return (int64_t)wgrad_blocks<16, 1, 2>(L, batch) * CO * ncol_tiles<16>() * 16;
+}
+
+extern "C" int rt_conv_relu_pool_wgrad(const rt_conv_layer* L, int32_t batch, const float* x_d, const int64_t* rows_d,
+                                       const float* dy_d, const uint8_t* argmax_d, float* dw_d, float* db_d,
+                                       float* ws_d, int64_t ws_floats, void* stream) {
+    if (bad_layer(L) || batch < 1 || !x_d || !dy_d || !argmax_d || !dw_d || !db_d || !ws_d)
+        return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_wgrad: bad argument");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (L->cin == 4) return launch_wgrad<4, 2, 4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+    return launch_wgrad<16, 1, 2>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+}
+
+extern "C" int rt_conv_relu_pool_dgrad(const rt_conv_layer* L, int32_t batch, const float* w_d, const float* dy_d,
+                                       const uint8_t* argmax_d, float* dx_d, void* stream) {
+    if (bad_layer(L) || L->cin != 16 || batch < 1 || batch > 65535 || !w_d || !dy_d || !argmax_d || !dx_d)
+        return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_dgrad: bad argument");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (L->groups == 1) return launch_dgrad<1, 1, 2>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
+    if (L->groups == 2) return launch_dgrad<2, 1, 2>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
+    return launch_dgrad<4, 1, 2>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
 }

@@ -13,6 +13,7 @@ per rollout step); the math is identical (log N(a; mu, sigma) summed over the
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
@@ -120,10 +121,81 @@ class PPO(GaussianHeadMixin, nn.Module):
         self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
 
 
+def _conv_layer(cin, groups, dims, pad):
+    from . import _lib
+
+    return _lib.RtConvLayer(cin, groups, (ctypes.c_int32 * 3)(*dims), (ctypes.c_int32 * 3)(*pad))
+
+
+def _stage_fwd(layer, out_dims, x, w, b, train: bool):
+    """One fused Conv3d + ReLU + MaxPool3d stage (rt_conv_relu_pool_fwd)."""
+    from . import _lib
+
+    L = _lib.load()
+    B = x.shape[0]
+    y = torch.empty((B, 16, *out_dims), device=x.device, dtype=torch.float32)
+    am = torch.empty((B, 16, *out_dims), device=x.device, dtype=torch.uint8) if train else None
+    _lib.check(L.rt_conv_relu_pool_fwd(ctypes.byref(layer), B, x.data_ptr(), None, w.data_ptr(), b.data_ptr(),
+                                       y.data_ptr(), _lib.ptr(am), _lib.stream_handle()), "rt_conv_relu_pool_fwd")
+    return y, am
+
+
+class _C3DStack(torch.autograd.Function):
+    """The three C3D stages (networks.py:13-33) on the HIP kernels of
+    csrc/c3d.hip; backward = weight gradients of all stages and the data
+    gradients of stages 3 and 2 (the observation needs none)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w3, b3, plan):
+        (l1, d1), (l2, d2), (l3, d3) = plan
+        p1, a1 = _stage_fwd(l1, d1, x, w1, b1, True)
+        p2, a2 = _stage_fwd(l2, d2, p1, w2, b2, True)
+        p3, a3 = _stage_fwd(l3, d3, p2, w3, b3, True)
+        ctx.plan = plan
+        ctx.save_for_backward(x, w2, w3, p1, a1, p2, a2, a3)
+        return p3
+
+    @staticmethod
+    def backward(ctx, gp3):
+        from . import _lib
+
+        L = _lib.load()
+        st = _lib.stream_handle()
+        (l1, _), (l2, _), (l3, _) = ctx.plan
+        x, w2, w3, p1, a1, p2, a2, a3 = ctx.saved_tensors
+        B = x.shape[0]
+        gp3 = gp3.contiguous()
+
+        def wgrad(layer, xin, gy, am, cin, groups):
+            dw = torch.empty((16, cin // groups, 3, 3, 3), device=x.device)
+            db = torch.empty(16, device=x.device)
+            ws = torch.empty(int(L.rt_conv_wgrad_workspace_floats(ctypes.byref(layer), B)), device=x.device)
+            _lib.check(L.rt_conv_relu_pool_wgrad(ctypes.byref(layer), B, xin.data_ptr(), None, gy.data_ptr(),
+                                                 am.data_ptr(), dw.data_ptr(), db.data_ptr(), ws.data_ptr(),
+                                                 ws.numel(), st), "rt_conv_relu_pool_wgrad")
+            return dw, db
+
+        def dgrad(layer, w, gy, am, like):
+            dx = torch.empty_like(like)
+            _lib.check(L.rt_conv_relu_pool_dgrad(ctypes.byref(layer), B, w.data_ptr(), gy.data_ptr(), am.data_ptr(),
+                                                 dx.data_ptr(), st), "rt_conv_relu_pool_dgrad")
+            return dx
+
+        dw3, db3 = wgrad(l3, p2, gp3, a3, 16, 4)
+        gp2 = dgrad(l3, w3, gp3, a3, p2)
+        dw2, db2 = wgrad(l2, p1, gp2, a2, 16, 2)
+        gp1 = dgrad(l2, w2, gp2, a2, p1)
+        dw1, db1 = wgrad(l1, x, gp1, a1, int(x.shape[1]), 1)
+        return None, dw1, db1, dw2, db2, dw3, db3, None
+
+
 class FeaturesExtractor3D(nn.Module):
     """C3D-lite encoder (networks.py:8-45): three 3x3x3 convs (groups 1/2/4)
     with ReLU and 2x2x2 max-pools, flatten, Linear -> features_dim, ReLU.
-    The first pool pads each axis by (S_i - 2) % 2 (networks.py:18-20)."""
+    The first pool pads each axis by (S_i - 2) % 2 (networks.py:18-20).
+    On the GPU the three stages run as the fused f32-MFMA kernels of
+    csrc/c3d.hip (forward + backward); the Conv3d modules hold the parameters
+    (same state-dict keys)."""
 
     def __init__(self, observation_shape, features_dim: int):
         super().__init__()
@@ -148,8 +220,39 @@ class FeaturesExtractor3D(nn.Module):
         s = [(x - 2 - 2) // 2 + 1 for x in s]                  # conv3 + pool3
         return 16 * int(np.prod(s))
 
+    def _plan(self):
+        """rt_conv_layer descriptors + pooled dims of the three stages."""
+        if getattr(self, "_plan_cache", None) is None:
+            from . import _lib
+
+            L = _lib.load()
+            c_in, *spatial = self.observation_shape
+            pads = [tuple((s - 2) % 2 for s in spatial), (0, 0, 0), (0, 0, 0)]
+            dims, plan = tuple(spatial), []
+            for (cin, groups), pad in zip([(c_in, 1), (16, 2), (16, 4)], pads):
+                layer = _conv_layer(cin, groups, dims, pad)
+                od = (ctypes.c_int32 * 3)()
+                _lib.check(L.rt_conv_out_dims(ctypes.byref(layer), od), "rt_conv_out_dims")
+                plan.append((layer, tuple(od)))
+                dims = tuple(od)
+            self._plan_cache = tuple(plan)
+        return self._plan_cache
+
     def forward(self, observations: torch.Tensor) -> torch.Tensor:
-        return self.mlp(self.cnn(observations))
+        if observations.device.type != "cuda":
+            return self.mlp(self.cnn(observations))  # CPU: the reference's torch modules
+        x = observations.contiguous()
+        c1, c2, c3 = self.cnn[0], self.cnn[3], self.cnn[6]
+        params = (c1.weight, c1.bias, c2.weight, c2.bias, c3.weight, c3.bias)
+        plan = self._plan()
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            p3 = _C3DStack.apply(x, *params, plan)
+        else:
+            (l1, d1), (l2, d2), (l3, d3) = plan
+            p1, _ = _stage_fwd(l1, d1, x, c1.weight, c1.bias, False)
+            p2, _ = _stage_fwd(l2, d2, p1, c2.weight, c2.bias, False)
+            p3, _ = _stage_fwd(l3, d3, p2, c3.weight, c3.bias, False)
+        return self.mlp(p3.flatten(1))
 
 
 class PPO_3DCNN(GaussianHeadMixin, nn.Module):

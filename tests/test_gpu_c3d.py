@@ -79,3 +79,89 @@ def test_conv_relu_pool_forward(cin, groups, dims, pad, B):
     clear = (top2[..., 0] - top2[..., 1] > 1e-6) & (ref > 0)
     assert clear.float().mean() > 0.5
     assert torch.equal(flat[clear], idx[clear])
+
+
+def _fwd(lib, L, B, xd, rd, wd, bd, od):
+    from ppo_radiotherapy_amd import _lib
+
+    dev = xd.device
+    y = torch.empty((B, 16, *od), device=dev)
+    am = torch.empty((B, 16, *od), dtype=torch.uint8, device=dev)
+    _lib.check(lib.rt_conv_relu_pool_fwd(ctypes.byref(L), B, xd.data_ptr(), _lib.ptr(rd), wd.data_ptr(),
+                                         bd.data_ptr(), y.data_ptr(), am.data_ptr(), None), "fwd")
+    return y, am
+
+
+@pytest.mark.parametrize("cin,groups,dims,pad,B", STAGES)
+def test_conv_relu_pool_backward(cin, groups, dims, pad, B):
+    """rt_conv_relu_pool_wgrad (dW, db) and, for 16-channel stages,
+    rt_conv_relu_pool_dgrad (dX) vs float64 autograd of the same stage."""
+    from ppo_radiotherapy_amd import _lib
+
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(7 + cin + groups)
+    x = torch.rand((B, cin, *dims), generator=g)
+    if cin == 16:
+        x = torch.relu(x - 0.3)
+    w = torch.randn((16, cin // groups, 3, 3, 3), generator=g) * (1.0 / np.sqrt(cin // groups * 27))
+    b = torch.randn(16, generator=g) * 0.1
+    L = _layer(cin, groups, dims, pad)
+    od = (ctypes.c_int32 * 3)()
+    lib = _lib.load()
+    _lib.check(lib.rt_conv_out_dims(ctypes.byref(L), od), "dims")
+    xd, wd, bd = x.to(dev), w.to(dev), b.to(dev)
+    y, am = _fwd(lib, L, B, xd, None, wd, bd, od)
+    gy = torch.randn((B, 16, *od), generator=g)
+    gyd = gy.to(dev)
+    dw = torch.full_like(wd, float("nan"))
+    db = torch.full_like(bd, float("nan"))
+    ws = torch.empty(int(lib.rt_conv_wgrad_workspace_floats(ctypes.byref(L), B)), device=dev)
+    _lib.check(lib.rt_conv_relu_pool_wgrad(ctypes.byref(L), B, xd.data_ptr(), None, gyd.data_ptr(), am.data_ptr(),
+                                           dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(), None), "wgrad")
+    dx = None
+    if cin == 16:
+        dx = torch.full_like(xd, float("nan"))
+        _lib.check(lib.rt_conv_relu_pool_dgrad(ctypes.byref(L), B, wd.data_ptr(), gyd.data_ptr(), am.data_ptr(),
+                                               dx.data_ptr(), None), "dgrad")
+    torch.cuda.synchronize()
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    yr = F.max_pool3d(F.relu(F.conv3d(xr, wr, br, groups=groups)), 2, 2, padding=pad)
+    yr.backward(gy.double())
+    # torch's own float32 error on the same data sets the scale of the tolerance
+    xf, wf, bf = (t.clone().requires_grad_(True) for t in (x, w, b))
+    F.max_pool3d(F.relu(F.conv3d(xf, wf, bf, groups=groups)), 2, 2, padding=pad).backward(gy)
+    for mine, f32, ref in ((dw, wf.grad, wr.grad), (db, bf.grad, br.grad)):
+        err = float((mine.cpu().double() - ref).abs().max())
+        err32 = float((f32.double() - ref).abs().max())
+        assert err <= 10 * err32 + 1e-6 * float(ref.abs().max()), (err, err32)
+    if dx is not None:
+        d = (dx.cpu().double() - xr.grad).abs()
+        scale = float(xr.grad.abs().max())
+        assert float((d <= 1e-4 * scale).double().mean()) > 0.999
+        assert float(d.norm() / xr.grad.norm()) < 1e-3
+
+
+def test_features_extractor_matches_torch_modules():
+    """FeaturesExtractor3D on the GPU (fused kernels) vs its own torch modules
+    on the CPU in float64: features and every parameter gradient."""
+    from ppo_radiotherapy_amd.networks import FeaturesExtractor3D
+
+    torch.manual_seed(0)
+    fe = FeaturesExtractor3D((4, 34, 27, 40), 64)
+    ref = FeaturesExtractor3D((4, 34, 27, 40), 64).double()
+    ref.load_state_dict({k: v.double() for k, v in fe.state_dict().items()})
+    fe = fe.cuda()
+    x = torch.rand((6, 4, 34, 27, 40))
+    f = fe(x.cuda())
+    fr = ref(x.double())
+    torch.testing.assert_close(f.cpu().double(), fr, rtol=1e-4, atol=1e-5)
+    gf = torch.randn_like(fr)
+    f.backward(gf.float().cuda())
+    fr.backward(gf)
+    for (n, p), q in zip(fe.named_parameters(), ref.parameters()):
+        err = float((p.grad.cpu().double() - q.grad).abs().max()) / (float(q.grad.abs().max()) + 1e-12)
+        assert err < 2e-3, (n, err)
+    with torch.no_grad():
+        torch.testing.assert_close(fe(x.cuda()), f.detach())  # inference path (no argmax) = training forward
