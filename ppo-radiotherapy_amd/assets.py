@@ -17,6 +17,10 @@ Two sources:
 * `synthetic_library(shape, ...)` -- BASELINE configs at 64^3 / 128^3: lungs
   nearest-resampled from the reference mask, spherical tumours inside the lung
   mask with radii drawn so voxel counts span the reference's 16-586 range.
+* `reference_style_library(n, seed, shape)` -- graphics.py's own generator
+  (graphics.py:110-208) restated in voxel space (no trimesh): position and
+  radius draws, the 20-point inside-the-lungs acceptance, sphere voxelization
+  at pitch 0.05 mesh units, reference filename format.
 """
 from __future__ import annotations
 
@@ -118,6 +122,81 @@ def synthetic_library(shape=(64, 64, 64), n_tumours: int = 1000, seed: int = 0,
         names.append(f"{c[0]:.2f}_{c[1]:.2f}_{c[2]:.2f}_{r:.2f}.npy")
     return TumourLibrary(shape=tuple(shape), lungs=lungs, names=names,
                          voxels=np.concatenate(parts), offsets=np.asarray(offsets, np.int64))
+
+
+# graphics.py:190-208 voxelizes the lung mesh at pitch 0.05; the mesh->voxel
+# origin of the reference grid, fitted from the 1000 reference tumours
+# (filename position vs voxel centroid, per-axis std 0.02 mesh units)
+REF_PITCH = 0.05
+REF_ORIGIN = (-17.5098, -1.3827, -1.8291)
+# sphere voxelization slack (voxels): trimesh's subdivide + fill of an
+# icosphere(subdivisions=2) marks every voxel its surface touches; d <= r/p +
+# 0.65 matches the reference voxel counts (median ratio 1.0) with a mean Jaccard
+# of ~0.64 per tumour -- the residual is the reference's astype(int) truncation
+# of the tumour bounds (alignment noise 0.4-0.5 voxel, uncorrelated with the
+# sub-voxel position), which no voxel-space restatement can reproduce
+REF_VOXEL_SLACK = 0.65
+
+
+def _sphere_voxels(center_mesh, radius, shape, origin, pitch):
+    """Sorted flat indices of the voxels whose centres lie within
+    radius/pitch + REF_VOXEL_SLACK of the sphere centre (per-axis pitch)."""
+    pitch = np.broadcast_to(np.asarray(pitch, np.float64), (3,))
+    c = (np.asarray(center_mesh, np.float64) - np.asarray(origin)) / pitch
+    R = radius / pitch + REF_VOXEL_SLACK
+    lo = np.maximum(np.floor(c - R).astype(int), 0)
+    hi = np.minimum(np.ceil(c + R).astype(int) + 1, np.asarray(shape))
+    if np.any(hi <= lo):
+        return np.zeros(0, np.int32)
+    zz, yy, xx = np.meshgrid(*[np.arange(a, b) for a, b in zip(lo, hi)], indexing="ij")
+    inside = ((zz - c[0]) / R[0]) ** 2 + ((yy - c[1]) / R[1]) ** 2 + ((xx - c[2]) / R[2]) ** 2 <= 1.0
+    return np.sort(np.ravel_multi_index((zz[inside], yy[inside], xx[inside]), shape)).astype(np.int32)
+
+
+def reference_style_library(n_tumours: int = 1000, seed: int = 0, shape=None, data_dir: str = DATA_DIR,
+                            mean_radius: float = 0.1, std_radius: float = 0.05, resolution: int = 20,
+                            min_size: float = 0.05) -> TumourLibrary:
+    """graphics.py:133-208 (generate_tumour / get_random_sphere_bounded /
+    is_inside / pregenerate_voxel_data) in voxel space:
+
+    * position = round(U(lung bounds), 2) mesh units, radius =
+      round(|N(0.1, 0.05)|, 2), redrawn while radius < 0.05 (graphics.py:158-163);
+    * accepted when `resolution` random points of the sphere surface lie in
+      the lungs (graphics.py:110-122) -- here: in a lung voxel of the mask;
+    * voxelized at pitch 0.05 (graphics.py:166-188), see REF_VOXEL_SLACK;
+    * named f"{x}_{y}_{z}_{r}.npy" (graphics.py:204).
+
+    `shape` other than the reference 67x43x70 resamples the lungs and scales
+    the pitch per axis.  Deterministic in `seed` (numpy Generator, not the
+    reference's global np.random stream)."""
+    ref = np.load(os.path.join(data_dir, "lungs.npy"))
+    shape = tuple(ref.shape) if shape is None else tuple(int(x) for x in shape)
+    lungs = (ref if shape == tuple(ref.shape) else resample_nearest(ref, shape)).astype(np.uint8)
+    pitch = REF_PITCH * np.asarray(ref.shape, np.float64) / np.asarray(shape, np.float64)
+    origin = np.asarray(REF_ORIGIN)
+    lo_b = origin
+    hi_b = origin + pitch * (np.asarray(shape) - 1)
+    rng = np.random.default_rng(seed)
+    names, parts, offsets = [], [], [0]
+    while len(names) < n_tumours:
+        position = np.round(rng.uniform(lo_b, hi_b), 2)
+        radius = float(np.round(abs(rng.normal(mean_radius, std_radius)), 2))
+        if radius < min_size:
+            continue
+        d = rng.normal(size=(resolution, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        pts = np.rint((position + d * radius - origin) / pitch).astype(np.int64)
+        ok = np.all((pts >= 0) & (pts < np.asarray(shape)), axis=1)
+        if not ok.all() or not lungs[pts[:, 0], pts[:, 1], pts[:, 2]].all():
+            continue
+        flat = _sphere_voxels(position, radius, shape, origin, pitch)
+        if flat.size == 0:
+            continue
+        parts.append(flat)
+        offsets.append(offsets[-1] + flat.size)
+        names.append(f"{position[0]}_{position[1]}_{position[2]}_{radius}.npy")
+    return TumourLibrary(shape=shape, lungs=lungs, names=names, voxels=np.concatenate(parts),
+                         offsets=np.asarray(offsets, np.int64))
 
 
 def library_for(grid) -> TumourLibrary:

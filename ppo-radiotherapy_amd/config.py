@@ -23,7 +23,7 @@ DEFAULTS = {
     "num_iterations": 0, "save_frequency_iterations": 0,
     # additions of this framework (optional in user configs)
     "grid": None,              # None: the reference grid and assets (67x43x70); else [D,H,W] synthetic
-    "tumour_library": "auto",  # auto | reference | synthetic
+    "tumour_library": "auto",  # auto | reference | synthetic | reference_style
     "n_synthetic_tumours": 1000,
 }
 

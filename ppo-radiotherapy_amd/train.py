@@ -41,7 +41,10 @@ def _library(cfg):
         if grid is not None and tuple(grid) != lib.shape:
             raise ValueError("the reference tumour library exists only at 67x43x70")
         return lib
-    return assets.synthetic_library(grid or (64, 64, 64), int(cfg.get("n_synthetic_tumours", 1000)), int(cfg.seed))
+    n = int(cfg.get("n_synthetic_tumours", 1000))
+    if kind == "reference_style":  # graphics.py's generator (assets.reference_style_library)
+        return assets.reference_style_library(n, int(cfg.seed), grid)
+    return assets.synthetic_library(grid or (64, 64, 64), n, int(cfg.seed))
 
 
 def train(cfg, writer, device, output_dir=None, run_name=None, rank=0, world=1):

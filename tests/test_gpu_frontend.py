@@ -144,3 +144,33 @@ def test_ppo_learns_on_64cubed():
         first = r if first is None else first
     assert r > first + 0.3, (first, r)
     env.close()
+
+
+def test_export_trajectory_format(tmp_path, golden):
+    """RadiotherapyEnv.export_trajectory writes environment.py:69-75's npz:
+    tumours (f32 volume), dose (f32 volume), beams = [(position, direction)]
+    per step as f64 [n, 2, 3]; replaying golden actions gives the golden dose."""
+    from environment import RadiotherapyEnv
+
+    z = golden("env_traj_ref.npz")
+    env = RadiotherapyEnv(visionless=True)
+    env.reset(options={"tumour_id": int(z["tumour_id"][0])})
+    n = int(z["ep_len"][0])
+    infos = []
+    for t in range(n):
+        _, _, _, _, info = env.step(z["actions"][0][t])
+        infos.append(info)
+    path = tmp_path / "traj.npz"
+    env.export_trajectory(path)
+    d = np.load(path, allow_pickle=False)
+    assert set(d.files) == {"tumours", "dose", "beams"}
+    assert d["tumours"].dtype == np.float32 and d["tumours"].shape == (67, 43, 70)
+    assert d["dose"].dtype == np.float32 and d["dose"].shape == (67, 43, 70)
+    assert d["beams"].dtype == np.float64 and d["beams"].shape == (n, 2, 3)
+    np.testing.assert_array_equal(d["dose"], env.dose)
+    for t, info in enumerate(infos):
+        np.testing.assert_array_equal(d["beams"][t, 0], np.array(info["beam_position"]["translation"]))
+        np.testing.assert_array_equal(d["beams"][t, 1], np.array(info["beam_position"]["rotation"]))
+    nz = np.flatnonzero(d["dose"].ravel())
+    np.testing.assert_array_equal(nz, z["dose_idx"][z["dose_off"][0]:z["dose_off"][1]])
+    env.close()

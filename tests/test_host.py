@@ -74,3 +74,35 @@ def test_facade_draws_tumours_like_the_reference():
         np.random.seed(seed)
         b = names[int(np.random.choice(len(names)))]
         assert a == b
+
+
+def test_reference_style_generator_against_reference_library():
+    """assets.reference_style_library restates graphics.py:110-208: its sphere
+    voxelization reproduces the reference voxel sets of the reference names
+    (counts, overlap) and its draws follow the reference's distributions."""
+    from ppo_radiotherapy_amd import assets
+
+    ref = assets.reference_library()
+    J, Q = [], []
+    for k in range(0, ref.n_tumours, 4):
+        x, y, z, r = (float(t) for t in ref.names[k][:-4].split("_"))
+        mine = set(assets._sphere_voxels((x, y, z), r, ref.shape, assets.REF_ORIGIN, assets.REF_PITCH).tolist())
+        theirs = set(ref.tumour_voxels(k).tolist())
+        J.append(len(mine & theirs) / len(mine | theirs))
+        Q.append(len(mine) / len(theirs))
+    assert np.mean(J) > 0.6 and 0.9 < np.median(Q) < 1.15, (np.mean(J), np.median(Q))
+    lib = assets.reference_style_library(300, seed=3)
+    assert lib.shape == ref.shape and lib.n_tumours == 300
+    radii = np.array([float(n[:-4].split("_")[3]) for n in lib.names])
+    ref_radii = np.array([float(n[:-4].split("_")[3]) for n in ref.names])
+    assert radii.min() >= 0.05 and np.allclose(radii, np.round(radii, 2))
+    assert abs(radii.mean() - ref_radii.mean()) < 0.01 and abs(radii.std() - ref_radii.std()) < 0.01
+    counts = np.diff(lib.offsets)
+    ref_counts = np.diff(ref.offsets)
+    assert abs(np.median(counts) / np.median(ref_counts) - 1) < 0.25
+    inside = np.mean([ref.lungs.ravel()[lib.tumour_voxels(k)].mean() for k in range(lib.n_tumours)])
+    assert inside > 0.9
+    again = assets.reference_style_library(300, seed=3)
+    assert again.names == lib.names and np.array_equal(again.voxels, lib.voxels)
+    lib64 = assets.reference_style_library(20, seed=1, shape=(64, 64, 64))
+    assert lib64.shape == (64, 64, 64) and lib64.n_tumours == 20
