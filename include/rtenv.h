@@ -245,6 +245,13 @@ int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_
                   float* exp_avg_sq_d, int64_t n_flat, int64_t step0, double lr, float* workspace_d,
                   int64_t workspace_floats, float* stats_d, float* stats_accum_d, void* stream);
 
+/* Per-epoch helpers of the update: perm_d[i] = a keyed pseudo-random
+ * permutation of [0, n) (train.py:195's shuffle); stats_d[n_mb][2] = mean and
+ * unbiased std of adv over each minibatch perm[i*mb, (i+1)*mb) (train.py:215-218). */
+int rt_ppo_shuffle(int64_t n, uint64_t key, int64_t* perm_d, void* stream);
+int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
+                     float* stats_d, void* stream);
+
 /* ---- C3D feature extractor of the vision agent (networks.py:8-45) ----------
  * One stage = Conv3d(cin, 16, 3, groups) + ReLU + MaxPool3d(2, 2, pool_pad):
  * stage 1 (4, 1, pad (S_i - 2) % 2), stage 2 (16, 2, 0), stage 3 (16, 4, 0).

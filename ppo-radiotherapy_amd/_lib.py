@@ -32,6 +32,7 @@ EXPORTS = [
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
+    "rt_ppo_shuffle", "rt_ppo_adv_stats",
     "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
     "rt_conv_relu_pool_dgrad",
     "rt_last_error", "rt_abi_version",
@@ -141,6 +142,8 @@ def load(build_if_missing: bool = True):
         "rt_ppo_update": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, i32, vp,
                            ctypes.POINTER(RtPpoHparams), vp, vp, vp, vp, i64, i64, f64, vp, i64, vp, vp, vp],
                           ctypes.c_int),
+        "rt_ppo_shuffle": ([i64, ctypes.c_uint64, vp, vp], ctypes.c_int),
+        "rt_ppo_adv_stats": ([vp, vp, i32, i32, vp, vp], ctypes.c_int),
         "rt_conv_out_dims": ([ctypes.POINTER(RtConvLayer), ctypes.POINTER(i32)], ctypes.c_int),
         "rt_conv_relu_pool_fwd": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_conv_wgrad_workspace_floats": ([ctypes.POINTER(RtConvLayer), i32], i64),

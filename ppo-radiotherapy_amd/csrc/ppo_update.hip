@@ -951,6 +951,70 @@ __global__ __launch_bounds__(256) void k_adam(AdamParams P) {
     P.v[i] = v;
 }
 
+// ---- per-epoch shuffle and minibatch advantage statistics ------------------
+// A keyed pseudo-random permutation of [0, n): a 4-round Feistel network on
+// 2h bits (2^(2h) >= n) with cycle-walking, one index per thread -- replaces
+// the device randperm (a multi-kernel radix sort) the reference's
+// np.random.permutation maps to (train.py:195).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+__global__ __launch_bounds__(256) void k_shuffle(int64_t n, int h, uint64_t key, int64_t* perm) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t mask = (1u << h) - 1u;
+    const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+    uint32_t v = (uint32_t)i;
+    do {
+        uint32_t L = v >> h, R = v & mask;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t f = mix32(R ^ mix32(k0 + 0x9E3779B9U * (uint32_t)(r + 1)) ^ k1) & mask;
+            const uint32_t t = L ^ f;
+            L = R;
+            R = t;
+        }
+        v = (L << h) | R;
+    } while ((int64_t)v >= n);
+    perm[i] = v;
+}
+
+// [n_mb][2] = (mean, unbiased std) of adv over each minibatch of perm
+// (train.py:215-218), sums in f64
+__global__ __launch_bounds__(256) void k_adv_stats(const float* adv, const int64_t* perm, int mb, float* stats) {
+    __shared__ double ps[4], pq[4];
+    const int64_t base = (int64_t)blockIdx.x * mb;
+    double s = 0.0, q = 0.0;
+    for (int j = threadIdx.x; j < mb; j += 256) {
+        const double a = adv[perm[base + j]];
+        s += a;
+        q += a * a;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off, 64);
+        q += __shfl_xor(q, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ps[threadIdx.x >> 6] = s;
+        pq[threadIdx.x >> 6] = q;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double S = (ps[0] + ps[1]) + (ps[2] + ps[3]), Q = (pq[0] + pq[1]) + (pq[2] + pq[3]);
+        const double mean = S / mb;
+        const double var = mb > 1 ? (Q - S * mean) / (mb - 1) : 0.0;
+        stats[2 * blockIdx.x] = (float)mean;
+        stats[2 * blockIdx.x + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
+    }
+}
+
 // RT_PPO_GRAD_KERNEL=valu selects the VALU kernel (A/B comparisons); default MFMA
 bool rt_ppo_use_mfma() {
     static const int v = [] {
@@ -1099,5 +1163,28 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
                          workspace_d + (workspace_floats - kNormSlots), true, st);
         if (rc) return rc;
     }
+    return RT_OK;
+}
+
+extern "C" int rt_ppo_shuffle(int64_t n, uint64_t key, int64_t* perm_d, void* stream) {
+    if (n < 1 || n > ((int64_t)1 << 31) || !perm_d) return rt_internal_fail(RT_EINVAL, "rt_ppo_shuffle: bad argument");
+    int b = 1;
+    while (((int64_t)1 << b) < n) ++b;
+    const int h = (b + 1) / 2;
+    hipLaunchKernelGGL(k_shuffle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), n, h, key, perm_d);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
+                                float* stats_d, void* stream) {
+    if (!adv_d || !perm_d || mb_size < 1 || n_minibatches < 1 || !stats_d)
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_adv_stats: bad argument");
+    hipLaunchKernelGGL(k_adv_stats, dim3(n_minibatches), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), adv_d,
+                       perm_d, mb_size, stats_d);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
 }

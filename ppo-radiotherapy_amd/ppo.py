@@ -143,6 +143,10 @@ class PPOTrainer:
                 adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
             self._ws = torch.empty(int(L.rt_ppo_workspace_floats(self.minibatch_size)), **kw)
             self._norm_ws = torch.empty(256, **kw)
+            self._perm_buf = torch.empty(self.batch_size, dtype=torch.int64, **kw)
+            self._adv_stats_buf = torch.empty((self.batch_size // self.minibatch_size, 2), **kw)
+            # epoch shuffle keys: a host generator seeded from the trainer's seed and rank
+            self._host_gen = torch.Generator().manual_seed(int(getattr(cfg, "seed", 0)) * 7919 + 104729 * rank + 17)
         self.next_obs = None
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
@@ -349,6 +353,21 @@ class PPOTrainer:
                                self._b_adv.data_ptr(), self._b_ret.data_ptr(), self._b_val.data_ptr(),
                                self.batch_size)
 
+    def _epoch_perm_stats(self, L, stream, n_mb):
+        """One epoch's shuffle (rt_ppo_shuffle, keyed by a draw from the
+        trainer's generator) and minibatch advantage statistics
+        (rt_ppo_adv_stats; all-reduced sums when world > 1)."""
+        key = int(torch.randint(0, 2 ** 62, (1,), generator=self._host_gen).item())
+        perm = self._perm_buf
+        _lib.check(L.rt_ppo_shuffle(self.batch_size, key, perm.data_ptr(), stream), "rt_ppo_shuffle")
+        if not self.cfg.norm_adv:
+            return perm, None
+        if self.world > 1:
+            return perm, self._epoch_adv_stats(self._b_adv, perm).contiguous()
+        _lib.check(L.rt_ppo_adv_stats(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, n_mb,
+                                      self._adv_stats_buf.data_ptr(), stream), "rt_ppo_adv_stats")
+        return perm, self._adv_stats_buf
+
     def _update_fused(self):
         """train.py:183-248 through the fused kernels: per epoch one device
         randperm and one (all-reduced) advantage-statistics reduction, then per
@@ -369,8 +388,7 @@ class PPOTrainer:
         self._ppo_accum.zero_()
         done = 0
         for _ in range(int(self.cfg.update_epochs)):
-            perm = torch.randperm(self.batch_size, device=self.device, generator=self.gen)
-            adv = self._epoch_adv_stats(self._b_adv, perm).contiguous() if self.cfg.norm_adv else None
+            perm, adv = self._epoch_perm_stats(L, stream, n_mb)
             k = n_mb if not self.max_minibatches else min(n_mb, self.max_minibatches - done)
             if self.world == 1:
                 _lib.check(L.rt_ppo_update(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch), perm.data_ptr(),

@@ -76,6 +76,15 @@ def test_update_matches_float64_reference(fused):
         return out
 
     torch.randperm = rp
+    if fused:  # the fused update shuffles with rt_ppo_shuffle: record those permutations
+        eps = e._epoch_perm_stats
+
+        def rec_eps(*a, **k):
+            perm, adv = eps(*a, **k)
+            rec.append(perm.cpu().clone())
+            return perm, adv
+
+        e._epoch_perm_stats = rec_eps
     try:
         e.update()
         e.update()
@@ -266,3 +275,33 @@ def test_fused_policy_matches_torch_agent():
     z = ((out["act"] - mean) / np.exp(-0.5)).cpu().numpy()
     assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
     assert abs(np.corrcoef(z[:, 0], z[:, 1])[0, 1]) < 0.03
+
+
+@pytest.mark.parametrize("n", [1, 1000, 3001, 32768, 262144])
+def test_shuffle_is_a_permutation_and_adv_stats(n):
+    """rt_ppo_shuffle: a bijection of [0, n) that depends on the key;
+    rt_ppo_adv_stats: minibatch mean / unbiased std as torch computes them."""
+    from ppo_radiotherapy_amd import _lib
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = torch.device("cuda")
+    L = _lib.load()
+    p1 = torch.empty(n, dtype=torch.int64, device=dev)
+    p2 = torch.empty(n, dtype=torch.int64, device=dev)
+    _lib.check(L.rt_ppo_shuffle(n, 12345, p1.data_ptr(), None), "shuffle")
+    _lib.check(L.rt_ppo_shuffle(n, 67890, p2.data_ptr(), None), "shuffle")
+    torch.cuda.synchronize()
+    assert torch.equal(torch.sort(p1).values, torch.arange(n, device=dev))
+    if n >= 1000:
+        assert float((p1 != p2).double().mean()) > 0.99
+        # no residual order: rank correlation with the identity is small
+        r = torch.corrcoef(torch.stack([p1.double(), torch.arange(n, device=dev, dtype=torch.float64)]))[0, 1]
+        assert abs(float(r)) < 0.1
+    if n % 8 == 0:
+        mb = n // 8
+        adv = torch.randn(n, device=dev) * 3 + 1
+        st = torch.empty((8, 2), device=dev)
+        _lib.check(L.rt_ppo_adv_stats(adv.data_ptr(), p1.data_ptr(), mb, 8, st.data_ptr(), None), "adv_stats")
+        a = adv[p1].view(8, mb)
+        torch.testing.assert_close(st, torch.stack([a.mean(1), a.std(1)], 1), rtol=1e-5, atol=1e-6)
