@@ -46,8 +46,18 @@ sys.path.insert(0, REPO)
 METRIC = "env steps/sec (whole node) + PPO updates/sec, visionless 64³ voxel, 1/2/4/8 GPU"
 HBM_PEAK = 8.0e12  # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
 F32_MFMA_PEAK = 157.3e12  # dense f32 MFMA (= f32 vector) peak, FLOP/s (MI355X_MICROARCH.md)
-# C3D forward FLOPs per sample at 64^3 (convolutions; SURVEY §8 a-15: 0.999 GFLOP)
-C3D_FWD_FLOP_64 = 2 * (16 * 4 * 27 * 62 ** 3 + 16 * 8 * 27 * 29 ** 3 + 16 * 4 * 27 * 12 ** 3)
+
+
+def c3d_fwd_flop(grid) -> int:
+    """Convolution FLOPs of one C3D forward (networks.py:13-33) on `grid`
+    (0.999 GFLOP at 64^3, 8.56 at 128^3)."""
+    dims, total = list(grid), 0
+    for k, (cin_per_group, pad) in enumerate([(4, None), (8, 0), (4, 0)]):
+        conv = [d - 2 for d in dims]
+        total += 2 * 16 * cin_per_group * 27 * int(np.prod(conv))
+        pads = [(d - 2) % 2 for d in dims] if pad is None else [0, 0, 0]
+        dims = [(c + 2 * p - 2) // 2 + 1 for c, p in zip(conv, pads)]
+    return total
 UPDATE_MACS_PER_SAMPLE = (9 * 64 + 64 * 64 + 64 * 6) + (9 * 64 + 64 * 64 + 64) \
     + (2 * 64 * 6 + 2 * 64 * 64 + 9 * 64) + (2 * 64 + 2 * 64 * 64 + 9 * 64)
 
@@ -309,14 +319,14 @@ def main():
                 fe(xo)
             torch.cuda.synchronize()
         dfe = (time.perf_counter() - t0) / 4
-        fl = C3D_FWD_FLOP_64 * a.envs if a.grid == 64 else None
-        roof["c3d_mfma"] = {"bound": "mfma", "forward_ms": dfe * 1e3, "flop": fl,
-                            "achieved": fl / dfe / 1e12 if fl else None, "peak": F32_MFMA_PEAK / 1e12,
-                            "unit": "TFLOP/s", "frac": fl / dfe / F32_MFMA_PEAK if fl else None}
+        fl = c3d_fwd_flop(grid) * a.envs
+        roof["c3d_mfma"] = {"bound": "mfma", "forward_ms": dfe * 1e3, "flop": fl, "achieved": fl / dfe / 1e12,
+                            "peak": F32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": fl / dfe / F32_MFMA_PEAK}
     out = {"metric": METRIC, "value": steps_per_s, "unit": "env steps/s", "n_gpus": world, "steps": K,
            "warmup": a.warmup, "ms_per_step": 1000 * dt / K, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-           "config": {"workload": (f"vision C3D, {a.envs} envs/GPU, {a.grid}^3 voxel grid (BASELINE configs[3])"
+           "config": {"workload": (f"vision C3D, {a.envs} envs/GPU, {a.grid}^3 voxel grid (BASELINE "
+                                   + ("configs[3])" if a.grid == 64 else "configs[4], per-GPU share)")
                                    if a.vision else
                                    f"visionless MLP, {a.envs} envs/GPU, {a.grid}^3 voxel grid "
                                    f"(BASELINE configs[{1 if world == 1 else 2}])") + (" env-only" if a.env_only else ""),

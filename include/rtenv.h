@@ -138,6 +138,12 @@ float* rt_env_dose(rt_env* env, int64_t* dose_stride);
 int rt_env_get_state(rt_env* env, double* pose_d /* f64[N,6] pos,dir */, int32_t* t_d,
                      int32_t* tumour_d, void* stream);
 int rt_env_set_pose(rt_env* env, const double* pose_d /* f64[N,6] */, void* stream);
+/* Current tumour of each env (i32[N]; out-of-range entries leave it), without
+ * a reset.  With rt_env_set_pose, a copy into rt_env_dose and rt_env_reset
+ * with an all-zero mask, a handle re-renders the observation of any stored
+ * (dose, pose, tumour) state -- the vision rollout's compact storage (SURVEY
+ * §8 f-3). */
+int rt_env_set_tumours(rt_env* env, const int32_t* tumour_d, void* stream);
 int rt_env_num_envs(const rt_env* env);
 
 /* Live kernel timing.  rt_env_kernel_timing(env, K) creates HIP events for

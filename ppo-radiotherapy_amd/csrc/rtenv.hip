@@ -39,7 +39,7 @@ namespace {
 constexpr int kStepThreads = 256;
 constexpr int kUnroll = 8;               // float4 loads in flight per thread
 constexpr int kSliceVec = 8192;          // k_dense slice: 8192 float4 = 128 KiB of dose
-constexpr int kMaxTumourVoxels = 1024;   // capacity of the per-block tumour phase
+constexpr int kMaxTumourVoxels = 16384;  // tumour voxels (op slots n + n-1 < 2^16; k_finish LDS per wave)
 constexpr int kMaxGridDim = 1024;
 constexpr float kEpsF = 1e-6f;           // draw_line.py:4 (f32 under NEP 50)
 
@@ -797,6 +797,7 @@ struct FinishParams {
     int32_t incremental; // lung count / sum from the k_beam-maintained counters
     uint32_t hash_mask;  // vision: beam-view hash slots - 1
     int32_t wave_lds;    // bytes of LDS per wave
+    int32_t wpb;         // envs (waves) per block: 4, or fewer when big tumours need the LDS
 };
 
 __device__ __forceinline__ void write_obs9(float* obs, const Geom& G, int e, const double* pose,
@@ -893,7 +894,7 @@ __device__ void vision_scatter(const FinishParams& P, int e, int lane, const dou
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int e = blockIdx.x * 4 + w;
+    const int e = blockIdx.x * P.wpb + w;
     if (e >= P.N) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm_raw[];
     unsigned char* wave_lds = fsm_raw + (size_t)w * P.wave_lds;
@@ -1075,6 +1076,11 @@ __global__ void k_set_next(EnvState st, int N, const int32_t* ids) {
     if (e < N) st.next_tumour[e] = ids[e];
 }
 
+__global__ void k_set_tumours(EnvState st, int N, int K, const int32_t* ids) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < N && ids[e] >= 0 && ids[e] < K) st.tumour[e] = ids[e];
+}
+
 __global__ void k_get_state(EnvState st, int N, double* pose, int32_t* t, int32_t* tum) {
     int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= N) return;
@@ -1195,6 +1201,7 @@ struct rt_env {
     int vec_per_slice = 0;   // float4 per slice
     size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
     int finish_wave_lds = 0; // bytes per wave
+    int finish_wpb = 4;      // k_finish envs per block
     uint32_t view_hash_mask = 0;
     int32_t* part_cnt = nullptr;
     double* part_sum = nullptr;
@@ -1378,7 +1385,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         int64_t a = cfg->tumour_offsets_h[k], b = cfg->tumour_offsets_h[k + 1];
         int n = (int)(b - a);
         if (n < 1) { free_env(env); return fail(RT_EINVAL, "empty tumour in library"); }
-        if (n > kMaxTumourVoxels) { free_env(env); return fail(RT_ELIMIT, "tumour larger than 1024 voxels"); }
+        if (n > kMaxTumourVoxels) { free_env(env); return fail(RT_ELIMIT, "tumour larger than 16384 voxels"); }
         const int32_t* iv = cfg->tumour_voxels_h + a;
         int64_t in_lung = 0;
         double csum[3] = {0, 0, 0};
@@ -1440,7 +1447,9 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     if (!env->visionless) wave_bytes += (size_t)(env->view_hash_mask + 1) * 8;
     wave_bytes = (wave_bytes + 15) / 16 * 16;
     env->finish_wave_lds = (int)wave_bytes;
-    env->finish_smem = 4 * wave_bytes;
+    env->finish_wpb = 4;
+    while (env->finish_wpb > 1 && (size_t)env->finish_wpb * wave_bytes > 160 * 1024) env->finish_wpb /= 2;
+    env->finish_smem = (size_t)env->finish_wpb * wave_bytes;
     if (env->finish_smem > 160 * 1024) { free_env(env); return fail(RT_ELIMIT, "LDS budget exceeded"); }
 
     // ---- device allocations ----
@@ -1565,7 +1574,14 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     fp.incremental = env->incremental;
     fp.hash_mask = env->view_hash_mask;
     fp.wave_lds = env->finish_wave_lds;
-    hipLaunchKernelGGL(k_finish, dim3((N + 3) / 4), dim3(256), env->finish_smem, stream, fp);
+    fp.wpb = env->finish_wpb;
+    static bool big_lds = false;
+    if (!big_lds && env->finish_smem > 64 * 1024) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_finish),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        big_lds = true;
+    }
+    hipLaunchKernelGGL(k_finish, dim3((N + fp.wpb - 1) / fp.wpb), dim3(64 * fp.wpb), env->finish_smem, stream, fp);
     RT_LAUNCH_CHECK("k_finish");
     if (ev) (void)hipEventRecord(ev[3], stream);
     return RT_OK;
@@ -1629,6 +1645,14 @@ int rt_env_get_state(rt_env* env, double* pose_d, int32_t* t_d, int32_t* tumour_
     hipLaunchKernelGGL(k_get_state, dim3((env->N + 255) / 256), dim3(256), 0, as_stream(stream), env->st,
                        env->N, pose_d, t_d, tumour_d);
     RT_LAUNCH_CHECK("k_get_state");
+    return RT_OK;
+}
+
+int rt_env_set_tumours(rt_env* env, const int32_t* tumour_d, void* stream) {
+    if (!env || !tumour_d) return fail(RT_EINVAL, "NULL argument");
+    hipLaunchKernelGGL(k_set_tumours, dim3((env->N + 255) / 256), dim3(256), 0, as_stream(stream), env->st,
+                       env->N, env->lib.K, tumour_d);
+    RT_LAUNCH_CHECK("k_set_tumours");
     return RT_OK;
 }
 

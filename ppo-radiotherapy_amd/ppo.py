@@ -68,7 +68,18 @@ class PPOTrainer:
         obs_shape = env.single_observation_space.shape
         act_shape = env.single_action_space.shape
         kw = dict(device=self.device)
-        self.obs = torch.zeros((T, N, *obs_shape), **kw)
+        # vision on the HIP env: store (dose, pose, tumour) per step and render
+        # observations at update time instead of [T, N, 4, V]
+        self.compact_obs = (len(obs_shape) == 4 and hasattr(env, "render") and hasattr(env, "snapshot")
+                            and bool(getattr(cfg, "compact_vision_rollout", True)))
+        if self.compact_obs:
+            V = int(np.prod(obs_shape[1:]))
+            self.obs = None
+            self.dose_snap = torch.zeros((T, N, V), **kw)
+            self.pose_snap = torch.zeros((T, N, 6), dtype=torch.float64, **kw)
+            self.tumour_snap = torch.zeros((T, N), dtype=torch.int32, **kw)
+        else:
+            self.obs = torch.zeros((T, N, *obs_shape), **kw)
         self.actions = torch.zeros((T, N, *act_shape), **kw)
         self.logprobs = torch.zeros((T, N), **kw)
         self.rewards = torch.zeros((T, N), **kw)
@@ -174,7 +185,8 @@ class PPOTrainer:
     # ------------------------------------------------------------------ rollout
     def reset(self, seed=None):
         obs, _ = self.env.reset(seed=seed)
-        self.next_obs = obs.clone()
+        # compact vision storage: the policy reads the env's own obs buffer
+        self.next_obs = obs if self.compact_obs else obs.clone()
         self.next_done.zero_()
         self._done_valid = False
 
@@ -204,7 +216,10 @@ class PPOTrainer:
         """One vectorised step of train.py:138-161 (policy sample + env step)."""
         if self.fused_policy:
             return self._rollout_step_fused(step, env_events)
-        self.obs[step].copy_(self.next_obs)
+        if self.compact_obs:
+            self.env.snapshot(self.dose_snap[step], self.pose_snap[step], self.tumour_snap[step])
+        else:
+            self.obs[step].copy_(self.next_obs)
         self.dones[step].copy_(self.next_done)
         action, logprob, _, value = self.agent.get_action_and_value(self.next_obs, generator=self.gen)
         self.values[step].copy_(value.flatten())
@@ -216,7 +231,8 @@ class PPOTrainer:
         if env_events is not None:
             env_events[1].record()
         self.rewards[step].copy_(reward)
-        self.next_obs.copy_(next_obs)
+        if not self.compact_obs:
+            self.next_obs.copy_(next_obs)
         self.next_done.copy_(term)
 
     @torch.no_grad()
@@ -303,10 +319,17 @@ class PPOTrainer:
             return acc
         return self._loss_backward(mb, adv_mean, adv_std)
 
+    def _obs_rows(self, mb):
+        """Observations of the batch rows mb (rendered from the stored states
+        in compact vision mode)."""
+        if not self.compact_obs:
+            return self._b_obs[mb]
+        return self.env.render(self._b_dose[mb], self._b_pose[mb], self._b_tumour[mb])
+
     def _loss_backward(self, mb, adv_mean=None, adv_std=None, weight: float = 1.0, zero: bool = True):
         cfg = self.cfg
         clip = float(cfg.clip_coef)
-        _, newlogprob, entropy, newvalue = self.agent.get_action_and_value(self._b_obs[mb], self._b_actions[mb])
+        _, newlogprob, entropy, newvalue = self.agent.get_action_and_value(self._obs_rows(mb), self._b_actions[mb])
         logratio = newlogprob - self._b_logprobs[mb]
         ratio = logratio.exp()
         with torch.no_grad():
@@ -341,7 +364,13 @@ class PPOTrainer:
         self.optimizer.step()
 
     def _bind_batch(self):
-        self._b_obs = self.obs.reshape((-1,) + self.obs.shape[2:])
+        if self.compact_obs:
+            self._b_obs = None
+            self._b_dose = self.dose_snap.view(-1, self.dose_snap.shape[-1])
+            self._b_pose = self.pose_snap.view(-1, 6)
+            self._b_tumour = self.tumour_snap.view(-1)
+        else:
+            self._b_obs = self.obs.reshape((-1,) + self.obs.shape[2:])
         self._b_logprobs = self.logprobs.reshape(-1)
         self._b_actions = self.actions.reshape((-1,) + self.actions.shape[2:])
         self._b_adv = self.advantages.reshape(-1)

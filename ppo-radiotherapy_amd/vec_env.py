@@ -148,6 +148,51 @@ class RadiotherapyVecEnv:
         p = pose.to(device=self.device, dtype=torch.float64).contiguous()
         _lib.check(self._L.rt_env_set_pose(self._h, _lib.ptr(p), _lib.stream_handle()), "rt_env_set_pose")
 
+    def set_tumours(self, ids: torch.Tensor):
+        """Current tumour of each env, without a reset (rt_env_set_tumours)."""
+        t = ids.to(device=self.device, dtype=torch.int32).contiguous()
+        _lib.check(self._L.rt_env_set_tumours(self._h, _lib.ptr(t), _lib.stream_handle()), "rt_env_set_tumours")
+
+    # ---- compact vision rollout storage (SURVEY §8 f-3) ----------------------
+    def snapshot(self, dose_out: torch.Tensor, pose_out: torch.Tensor, tumour_out: torch.Tensor):
+        """Store what the current observation is rendered from: dose f32
+        [N, V], pose f64 [N, 6], tumour i32 [N] (4x less than the [N, 4, V]
+        vision observation; the lungs, tumour and beam-view channels follow
+        from the mask, the tumour id and the pose)."""
+        N, V = self.num_envs, int(np.prod(self.grid))
+        dose_out.view(N, V).copy_(self.dose().reshape(N, V))
+        _lib.check(self._L.rt_env_get_state(self._h, _lib.ptr(pose_out), None, _lib.ptr(tumour_out),
+                                            _lib.stream_handle()), "rt_env_get_state")
+
+    def render(self, dose: torch.Tensor, pose: torch.Tensor, tumour: torch.Tensor) -> torch.Tensor:
+        """Observations [M, 4, D, H, W] of M stored states, bit-identical to
+        what the env emitted in them: a render handle is loaded with the states
+        and reset with an all-zero mask, which re-emits every observation (the
+        same k_dense_vis / k_finish code).  The returned tensor is the render
+        handle's buffer, valid until the next render call."""
+        if self.visionless:
+            raise ValueError("render() is for vision observations")
+        M = int(dose.shape[0])
+        r = getattr(self, "_renderer", None)
+        if r is None or r.num_envs < M:
+            if r is not None:
+                r.close()
+            r = RadiotherapyVecEnv(M, visionless=False, library=self.library, device=self.device, seed=self._seed)
+            self._renderer = r
+            self._render_mask = torch.zeros(M, dtype=torch.uint8, device=self.device)
+        V = int(np.prod(self.grid))
+        r.dose().reshape(r.num_envs, V)[:M].copy_(dose.reshape(M, V))
+        p = torch.zeros((r.num_envs, 6), dtype=torch.float64, device=self.device)
+        p[:M] = pose
+        p[M:, 4] = 1.0
+        t = torch.zeros(r.num_envs, dtype=torch.int32, device=self.device)
+        t[:M] = tumour
+        _lib.check(self._L.rt_env_set_pose(r._h, _lib.ptr(p), _lib.stream_handle()), "rt_env_set_pose")
+        _lib.check(self._L.rt_env_set_tumours(r._h, _lib.ptr(t), _lib.stream_handle()), "rt_env_set_tumours")
+        _lib.check(self._L.rt_env_reset(r._h, _lib.ptr(self._render_mask), None, _lib.ptr(r.obs),
+                                        _lib.stream_handle()), "rt_env_reset")
+        return r.obs[:M]
+
     def dose(self) -> torch.Tensor:
         """View [N, D, H, W] of the library-owned dose volumes."""
         stride = ctypes_int64()
@@ -172,6 +217,10 @@ class RadiotherapyVecEnv:
         return {"k_beam": ms[0] / k, "k_dense": ms[1] / k, "k_finish": ms[2] / k}, n.value
 
     def close(self):
+        r = getattr(self, "_renderer", None)
+        if r is not None:
+            r.close()
+            self._renderer = None
         if getattr(self, "_h", None):
             self._L.rt_env_destroy(self._h)
             self._h = None

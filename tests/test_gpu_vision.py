@@ -101,3 +101,70 @@ def test_vision_large_batch_rewards_match_visionless():
     torch.testing.assert_close(ov[:, 2], ev.dose(), rtol=0, atol=0)
     ev.close()
     el.close()
+
+
+def test_render_reproduces_observations():
+    """Compact vision storage: observations re-rendered from
+    (dose, pose, tumour) snapshots equal the emitted ones bit for bit,
+    including across the t = 100 truncation autoreset."""
+    from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    N = 4
+    env = RadiotherapyVecEnv(N, visionless=False, seed=5)
+    obs, _ = env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    keep = {0, 1, 2, 37, 99, 100, 101, 104}
+    V = int(np.prod(env.grid))
+    snaps, seen = [], []
+    for t in range(105):
+        if t in keep:
+            d = torch.empty((N, V), device="cuda")
+            p = torch.empty((N, 6), dtype=torch.float64, device="cuda")
+            k = torch.empty(N, dtype=torch.int32, device="cuda")
+            env.snapshot(d, p, k)
+            snaps.append((d, p, k))
+            seen.append(obs.clone())
+        a = torch.rand((N, 6), device="cuda", generator=g) * 2 - 1
+        obs, _, _, _, _ = env.step(a)
+    dd = torch.cat([s[0] for s in snaps])
+    pp = torch.cat([s[1] for s in snaps])
+    kk = torch.cat([s[2] for s in snaps])
+    r = env.render(dd, pp, kk)
+    torch.cuda.synchronize()
+    assert torch.equal(r, torch.cat(seen))
+    env.close()
+
+
+def test_compact_trainer_sees_stored_observations():
+    """A trainer with compact storage renders exactly the observations a
+    trainer with full [T, N, 4, V] storage keeps, and computes the same loss."""
+    from types import SimpleNamespace
+
+    from ppo_radiotherapy_amd.networks import PPO_3DCNN
+    from ppo_radiotherapy_amd.ppo import PPOTrainer
+    from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    out = {}
+    for compact in (False, True):
+        env = RadiotherapyVecEnv(6, visionless=False, seed=2)
+        torch.manual_seed(0)
+        agent = PPO_3DCNN((4, *env.grid), (6,), 64).cuda()
+        cfg = SimpleNamespace(num_steps=5, num_minibatches=2, update_epochs=1, learning_rate=3e-4, anneal_lr=False,
+                              gamma=0.99, gae_lambda=0.95, norm_adv=True, clip_coef=0.1, clip_vloss=True,
+                              ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5, compact_vision_rollout=compact,
+                              micro_batch=8)
+        tr = PPOTrainer(cfg, env, agent, "cuda", generator=torch.Generator(device="cuda").manual_seed(1))
+        assert tr.compact_obs == compact
+        tr.reset()
+        tr.rollout()
+        tr.compute_gae()
+        tr._bind_batch()
+        rows = torch.arange(tr.batch_size, device="cuda")
+        out[compact] = (tr._obs_rows(rows).clone(), tr._loss_backward(rows).cpu())
+        env.close()
+    assert torch.equal(out[True][0], out[False][0])
+    torch.testing.assert_close(out[True][1], out[False][1], rtol=0, atol=0)
