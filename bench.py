@@ -84,6 +84,8 @@ def parse():
                     help="env step formulation measured as `value` (the other is reported beside it)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
+    ap.add_argument("--rehearse-same-device", action="store_true",
+                    help="multi-rank rehearsal on one GPU: every rank on cuda:0, gloo instead of RCCL")
     a = ap.parse_args()
     if a.vision:
         # 512 envs, 64^3, num_steps 16, vision.yaml minibatching
@@ -157,10 +159,15 @@ def main():
     from ppo_radiotherapy_amd.ppo import PPOTrainer, broadcast_parameters
     from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
 
+    if a.rehearse_same_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.rehearse_same_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
         if world > 1:
