@@ -38,7 +38,19 @@ extern "C" int rt_internal_fail(int code, const char* msg);
 namespace {
 
 constexpr int CO = 16;
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;      // weight-gradient kernel
+// forward / data-gradient kernels: conv1 (4 input channels, 95 VGPRs) runs
+// 8-wave blocks (4 waves per SIMD at 2 blocks per CU) on 9-step register
+// batches; the 16-channel stages (108 A fragments in registers) 4-wave blocks
+// on 27-step batches
+template <int CIN>
+constexpr int conv_threads() {
+    return CIN == 4 ? 512 : 256;
+}
+template <int CIN>
+constexpr int conv_batch() {
+    return CIN == 4 ? 9 : 27;
+}
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -90,16 +102,20 @@ Geom make_geom(const rt_conv_layer* L) {
 // max / min over a pooling window = the 8 lanes of a 16-lane row that share
 // bit 1 of the row index (lanes c, c^1 and c+4, c+8, c+12 mod 16): DPP
 // quad_perm [1,0,3,2] and row_ror 4, 8 -- full-rate VALU, no LDS crossbar
+// (the pooled values are ReLU outputs >= 0 or -inf for masked positions; their
+// int bit patterns order as the floats do, so the max runs as a DPP-fused
+// integer max)
 __device__ __forceinline__ float win_max(float v) {
-    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));
-    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, false)));
-    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false)));
-    return v;
+    int k = __float_as_int(v);
+    k = max(k, __builtin_amdgcn_mov_dpp(k, 0xB1, 0xF, 0xF, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, 0x124, 0xF, 0xF, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, 0x128, 0xF, 0xF, true));
+    return __int_as_float(k);
 }
 __device__ __forceinline__ int win_min(int k) {
-    k = min(k, __builtin_amdgcn_mov_dpp(k, 0xB1, 0xF, 0xF, false));
-    k = min(k, __builtin_amdgcn_mov_dpp(k, 0x124, 0xF, 0xF, false));
-    k = min(k, __builtin_amdgcn_mov_dpp(k, 0x128, 0xF, 0xF, false));
+    k = min(k, __builtin_amdgcn_mov_dpp(k, 0xB1, 0xF, 0xF, true));
+    k = min(k, __builtin_amdgcn_mov_dpp(k, 0x124, 0xF, 0xF, true));
+    k = min(k, __builtin_amdgcn_mov_dpp(k, 0x128, 0xF, 0xF, true));
     return k;
 }
 
@@ -152,9 +168,9 @@ struct FwdParams {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* glb_ptr_t;
 
-template <int CIN>
+template <int CIN, int NTHREADS>
 __device__ __forceinline__ void load_tile(float* xs, const float* xb, const Geom& g, int z0, int y0, int x0) {
-    constexpr int NWV = kThreads / 64;
+    constexpr int NWV = NTHREADS / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int ci = 0, zz = 0, yy = wave;
     while (yy >= g.YL) {
@@ -204,15 +220,20 @@ __device__ __forceinline__ void conv_core(const float* xs, const float (&af)[nst
         ++row;
     }
     auto tile_base = [&](int r, int tx) { return lane_base + 2 * (r / PYB) * g.ZS + 2 * (r % PYB) * g.YS + 4 * tx; };
-    constexpr int CH = 27;  // k-steps per register batch (one tap set)
+    constexpr int CH = conv_batch<CIN>();  // k-steps per register batch (9: one dz slice, 27: a tap set)
+    constexpr int NTH = conv_threads<CIN>();
     float bv[2][2][CH];     // [buffer][tile][step]
+    int toff[27];           // tap offsets (wave-uniform: scalar registers)
+#pragma unroll
+    for (int q = 0; q < 27; ++q) toff[q] = (q / 9) * g.ZS + ((q / 3) % 3) * g.YS + q % 3;
+    // batch j = k-steps CH*j .. CH*j + CH-1: input-channel quad j / BPQ, taps (j % BPQ) * CH ..
+    constexpr int BPQ = 27 / CH;  // batches per input-channel quad
     auto fetch = [&](float (&dst)[2][CH], int r, int xq, int j) {
-        const int b0 = tile_base(r, 2 * xq) + j * 4 * g.CS, b1 = b0 + 4;
+        const int b0 = tile_base(r, 2 * xq) + (j / BPQ) * 4 * g.CS, b1 = b0 + 4;
 #pragma unroll
         for (int q = 0; q < CH; ++q) {
-            const int off = (q / 9) * g.ZS + ((q / 3) % 3) * g.YS + q % 3;
-            dst[0][q] = xs[b0 + off];
-            dst[1][q] = xs[b1 + off];
+            dst[0][q] = xs[b0 + toff[(j % BPQ) * CH + q]];
+            dst[1][q] = xs[b1 + toff[(j % BPQ) * CH + q]];
         }
     };
     constexpr int NJ = NS / CH;  // tap sets (input-channel quads) per tile
@@ -221,7 +242,7 @@ __device__ __forceinline__ void conv_core(const float* xs, const float (&af)[nst
     auto item = [&](auto start) {
         constexpr int S0 = decltype(start)::value;
         f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-        int nrow = row, nx = xp + kThreads / 64;
+        int nrow = row, nx = xp + NTH / 64;
         while (nx >= nxp) {
             nx -= nxp;
             ++nrow;
@@ -231,15 +252,17 @@ __device__ __forceinline__ void conv_core(const float* xs, const float (&af)[nst
             const int cb = (S0 + j) & 1;
             // the next batch (next tap set of this item, or the next item) is read
             // two values per MFMA pair, so few LDS reads are ever outstanding
-            const bool pf = j + 1 < NJ || nrow < nrows;
-            const int fr = j + 1 < NJ ? row : nrow, fx = j + 1 < NJ ? xp : nx, fj = j + 1 < NJ ? j + 1 : 0;
-            const int b0 = tile_base(fr, 2 * fx) + fj * 4 * g.CS, b1 = b0 + 4;
+            // (after the last item the "next" batch re-reads this item's tile:
+            // unconditional loads, no exec-mask branches in the loop)
+            const bool nxt = j + 1 < NJ || nrow < nrows;
+            const int fr = j + 1 < NJ ? row : (nxt ? nrow : row), fx = j + 1 < NJ ? xp : (nxt ? nx : xp);
+            const int fj = j + 1 < NJ ? j + 1 : 0;
+            const int b0 = tile_base(fr, 2 * fx) + (fj / BPQ) * 4 * g.CS, b1 = b0 + 4;
 #pragma unroll
             for (int q = 0; q < CH; ++q) {
-                if (pf) {
-                    const int off = (q / 9) * g.ZS + ((q / 3) % 3) * g.YS + q % 3;
-                    bv[cb ^ 1][0][q] = xs[b0 + off];
-                    bv[cb ^ 1][1][q] = xs[b1 + off];
+                {
+                    bv[cb ^ 1][0][q] = xs[b0 + toff[(fj % BPQ) * CH + q]];
+                    bv[cb ^ 1][1][q] = xs[b1 + toff[(fj % BPQ) * CH + q]];
                 }
                 acc[0] = mfma4(af[j * CH + q], bv[cb][0][q], acc[0]);
                 acc[1] = mfma4(af[j * CH + q], bv[cb][1][q], acc[1]);
@@ -260,8 +283,8 @@ __device__ __forceinline__ void conv_core(const float* xs, const float (&af)[nst
     }
 }
 
-template <int CIN, int G, int PZB, int PYB>
-__global__ __launch_bounds__(kThreads) void k_conv_relu_pool(FwdParams P) {
+template <int CIN, int G, int PZB, int PYB, bool TRAIN>
+__global__ __launch_bounds__(conv_threads<CIN>()) void k_conv_relu_pool(FwdParams P) {
     extern __shared__ float xs[];
     constexpr int NS = nsteps<CIN>();
     const Geom& g = P.g;
@@ -270,7 +293,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_relu_pool(FwdParams P) {
     const int64_t srow = P.rows ? P.rows[b] : b;
     const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
     const int z0 = 2 * pz0 - g.pd, y0 = 2 * py0 - g.ph, x0 = -g.pw;
-    load_tile<CIN>(xs, xb, g, z0, y0, x0);
+    load_tile<CIN, conv_threads<CIN>()>(xs, xb, g, z0, y0, x0);
     float af[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) af[s] = a_frag<CIN, G>(P.w, s, c, gq);
@@ -280,7 +303,14 @@ __global__ __launch_bounds__(kThreads) void k_conv_relu_pool(FwdParams P) {
     __syncthreads();
 
     const int zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
-    const int widx = zc * 4 + yc * 2 + (xc & 1);
+    const int widx = zc * 4 + yc * 2 + (xc & 1);  // = rank of the lane in its window (0..7)
+    const int64_t chan = (int64_t)g.PD * g.PH * g.PW;
+    // after the window reduction every lane of a window holds its 4 channels'
+    // maxima: the lane of rank i < 4 stores channel 4g + i (one store per lane)
+    const int myr = widx & 3;
+    const bool storer = widx < 4;
+    float* ybase = P.y + ((int64_t)b * CO + 4 * gq + myr) * chan;
+    uint8_t* abase = TRAIN ? P.amax + ((int64_t)b * CO + 4 * gq + myr) * chan : nullptr;
     conv_core<CIN, PYB>(xs, af, g, PZB * PYB, [&](const f4 (&acc)[2], int row, int xp) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -290,17 +320,22 @@ __global__ __launch_bounds__(kThreads) void k_conv_relu_pool(FwdParams P) {
             const int cz = 2 * pz - g.pd + zc, cy = 2 * py - g.ph + yc, cx = 4 * tx - g.pw + xc;
             const bool valid = cz >= 0 && cz < g.cd && cy >= 0 && cy < g.ch && cx >= 0 && cx < g.cw;
             const int px = 2 * tx + (xc >> 1);
-            const bool writer = (c & 0xD) == 0 && tx < g.XT && pz < g.PD && py < g.PH && px < g.PW;
+            float mine = 0.0f;
+            int kmine = 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float v = valid ? fmaxf(acc[u][r] + bias[r], 0.0f) : -INFINITY;
+                const float v = valid ? fmaxf(acc[u][r] + bias[r], 0.0f) : -INFINITY;
                 const float m = win_max(v);
-                const int k = win_min(v == m ? widx : 8);  // torch: first maximum in (z, y, x) window order
-                if (writer) {
-                    const size_t o = ((((size_t)b * CO + 4 * gq + r) * g.PD + pz) * g.PH + py) * g.PW + px;
-                    P.y[o] = m;
-                    if (P.amax) P.amax[o] = (uint8_t)(k | (m > 0.0f ? 8 : 0));
+                mine = r == myr ? m : mine;
+                if constexpr (TRAIN) {
+                    const int k = win_min(v == m ? widx : 8);  // torch: first maximum in (z, y, x) window order
+                    kmine = r == myr ? k : kmine;
                 }
+            }
+            if (storer && tx < g.XT && pz < g.PD && py < g.PH && px < g.PW) {
+                const int64_t o = ((int64_t)pz * g.PH + py) * g.PW + px;
+                ybase[o] = mine;
+                if constexpr (TRAIN) abase[o] = (uint8_t)(kmine | (mine > 0.0f ? 8 : 0));
             }
         }
     });
@@ -332,14 +367,14 @@ struct DgradParams {
 // dX[ci][p] = sum_{co, t} W[co][ci][t] dY[co][p - t]: the forward main loop over
 // the zero-padded dY region with flipped, transposed weights
 template <int G, int PZB, int PYB>
-__global__ __launch_bounds__(kThreads) void k_conv_dgrad(DgradParams P) {
+__global__ __launch_bounds__(conv_threads<16>()) void k_conv_dgrad(DgradParams P) {
     extern __shared__ float xs[];
     constexpr int NS = nsteps<16>();
     const Geom& g = P.g;
     const int b = blockIdx.z, z0 = blockIdx.y * 2 * PZB, y0 = blockIdx.x * 2 * PYB;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, gq = lane >> 4;
     // stage dY[co][z0-2 .., y0-2 .., -2 ..] into LDS (zero outside)
-    for (int r = wave; r < CO * g.ZL * g.YL; r += kThreads / 64) {
+    for (int r = wave; r < CO * g.ZL * g.YL; r += conv_threads<16>() / 64) {
         const int co = r / (g.ZL * g.YL), zz = (r / g.YL) % g.ZL, yy = r % g.YL;
         const int64_t plane = ((int64_t)b * CO + co) * g.PD * g.PH * g.PW;
         float* dst = xs + co * g.CS + zz * g.ZS + yy * g.YS;
@@ -430,7 +465,8 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad(WgradParams P) {
         const int pz0 = rz * PZB, py0 = ry * PYB;
         const int64_t srow = P.rows ? P.rows[b] : b;
         __syncthreads();  // the previous item's reads of xs are done
-        load_tile<CIN>(xs, P.x + srow * (int64_t)CIN * g.D * g.H * g.W, g, 2 * pz0 - g.pd, 2 * py0 - g.ph, -g.pw);
+        load_tile<CIN, kThreads>(xs, P.x + srow * (int64_t)CIN * g.D * g.H * g.W, g, 2 * pz0 - g.pd, 2 * py0 - g.ph,
+                                 -g.pw);
         __syncthreads();
         const int64_t plane = ((int64_t)b * CO + c) * g.PD * g.PH * g.PW;
         for (int t = (WP == 4 ? wave : 0); t < ntile; t += WP) {
@@ -502,6 +538,12 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* part, int nbl
         db[co] = a;
 }
 
+template <class K>
+void allow_big_lds(K* kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+
 template <int CIN, int G, int PZB, int PYB>
 int launch_fwd(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
                const float* bias, float* y, uint8_t* amax, hipStream_t st) {
@@ -517,12 +559,15 @@ int launch_fwd(const rt_conv_layer* L, int32_t B, const float* x, const int64_t*
     if (lds > 160 * 1024) return rt_internal_fail(RT_ELIMIT, "rt_conv: input tile exceeds LDS (grid too wide)");
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv_relu_pool<CIN, G, PZB, PYB>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        allow_big_lds(&k_conv_relu_pool<CIN, G, PZB, PYB, true>);
+        allow_big_lds(&k_conv_relu_pool<CIN, G, PZB, PYB, false>);
         attr = true;
     }
     dim3 grid((P.g.PH + PYB - 1) / PYB, (P.g.PD + PZB - 1) / PZB, B);
-    hipLaunchKernelGGL((k_conv_relu_pool<CIN, G, PZB, PYB>), grid, dim3(kThreads), lds, st, P);
+    if (amax)
+        hipLaunchKernelGGL((k_conv_relu_pool<CIN, G, PZB, PYB, true>), grid, dim3(conv_threads<CIN>()), lds, st, P);
+    else
+        hipLaunchKernelGGL((k_conv_relu_pool<CIN, G, PZB, PYB, false>), grid, dim3(conv_threads<CIN>()), lds, st, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
@@ -539,11 +584,6 @@ Geom make_dgrad_geom(const rt_conv_layer* L) {
     return g;
 }
 
-template <class K>
-void allow_big_lds(K* kern) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-}
 
 template <int G, int PZB, int PYB>
 int launch_dgrad(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am, float* dx,
@@ -562,7 +602,7 @@ int launch_dgrad(const rt_conv_layer* L, int32_t B, const float* w, const float*
         attr = true;
     }
     dim3 grid((P.g.H + 2 * PYB - 1) / (2 * PYB), (P.g.D + 2 * PZB - 1) / (2 * PZB), B);
-    hipLaunchKernelGGL((k_conv_dgrad<G, PZB, PYB>), grid, dim3(kThreads), lds, st, P);
+    hipLaunchKernelGGL((k_conv_dgrad<G, PZB, PYB>), grid, dim3(conv_threads<16>()), lds, st, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
