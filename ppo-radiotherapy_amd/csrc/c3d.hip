@@ -29,6 +29,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <algorithm>
 #include <type_traits>
 
 #include "rtenv.h"
@@ -38,7 +39,7 @@ extern "C" int rt_internal_fail(int code, const char* msg);
 namespace {
 
 constexpr int CO = 16;
-constexpr int kThreads = 256;      // weight-gradient kernel
+constexpr int kThreads = 512;      // weight-gradient kernel: 8 waves = position groups x column groups
 // forward / data-gradient kernels: conv1 (4 input channels, 95 VGPRs) runs
 // 8-wave blocks (4 waves per SIMD at 2 blocks per CU) on 9-step register
 // batches; the 16-channel stages (108 A fragments in registers) 4-wave blocks
@@ -342,20 +343,6 @@ __global__ __launch_bounds__(conv_threads<CIN>()) void k_conv_relu_pool(FwdParam
 }
 
 // ---------------------------------------------------------------------------
-// Gradient of the conv-output (pre-pool, post-ReLU-mask) at conv position
-// (cz, cy, cx) of channel co: the pooled gradient if that position is its
-// window's recorded maximum and the ReLU was active, else 0.
-__device__ __forceinline__ float dy_at(const float* dP, const uint8_t* am, const Geom& g, int64_t plane, int cz,
-                                       int cy, int cx) {
-    if (cz < 0 || cz >= g.cd || cy < 0 || cy >= g.ch || cx < 0 || cx >= g.cw) return 0.0f;
-    const int qz = cz + g.pd, qy = cy + g.ph, qx = cx + g.pw;
-    const int pz = qz >> 1, py = qy >> 1, px = qx >> 1;
-    if (pz >= g.PD || py >= g.PH || px >= g.PW) return 0.0f;  // dropped by the floor of the pooled size
-    const int64_t o = plane + ((int64_t)pz * g.PH + py) * g.PW + px;
-    const int byte = am[o];
-    return ((byte & 8) && (byte & 7) == ((qz & 1) * 4 + (qy & 1) * 2 + (qx & 1))) ? dP[o] : 0.0f;
-}
-
 struct DgradParams {
     const float* w;    // stage weights [16][16/G][27]
     const float* dP;   // [B][16][PD][PH][PW]
@@ -373,12 +360,31 @@ __global__ __launch_bounds__(conv_threads<16>()) void k_conv_dgrad(DgradParams P
     const Geom& g = P.g;
     const int b = blockIdx.z, z0 = blockIdx.y * 2 * PZB, y0 = blockIdx.x * 2 * PYB;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, gq = lane >> 4;
-    // stage dY[co][z0-2 .., y0-2 .., -2 ..] into LDS (zero outside)
-    for (int r = wave; r < CO * g.ZL * g.YL; r += conv_threads<16>() / 64) {
-        const int co = r / (g.ZL * g.YL), zz = (r / g.YL) % g.ZL, yy = r % g.YL;
-        const int64_t plane = ((int64_t)b * CO + co) * g.PD * g.PH * g.PW;
-        float* dst = xs + co * g.CS + zz * g.ZS + yy * g.YS;
-        for (int xx = lane; xx < g.XL; xx += 64) dst[xx] = dy_at(P.dP, P.am, g, plane, z0 + zz - 2, y0 + yy - 2, xx - 2);
+    // stage dY[co][z0-2 .., y0-2 .., -2 ..] into LDS: zero the tile, then each
+    // pooling window that overlaps it scatters its gradient to its recorded
+    // maximum (one argmax byte + one gradient load per window, not per position)
+    constexpr int NT = conv_threads<16>();
+    for (int i = threadIdx.x; i < CO * g.CS; i += NT) xs[i] = 0.0f;
+    __syncthreads();
+    {
+        const int cz0 = z0 - 2, cy0 = y0 - 2, cx0 = -2;  // conv coordinates of LDS (0, 0, 0)
+        const int pz_lo = max((cz0 + g.pd) >> 1, 0), pz_hi = min((cz0 + g.ZL - 1 + g.pd) >> 1, g.PD - 1);
+        const int py_lo = max((cy0 + g.ph) >> 1, 0), py_hi = min((cy0 + g.YL - 1 + g.ph) >> 1, g.PH - 1);
+        const int px_hi = min((cx0 + g.XL - 1 + g.pw) >> 1, g.PW - 1);
+        const int nz = pz_hi - pz_lo + 1, ny = py_hi - py_lo + 1, nx = px_hi + 1;
+        const int nwin = CO * nz * ny * nx;
+        for (int i = threadIdx.x; i < nwin; i += NT) {
+            const int px = i % nx, py = py_lo + (i / nx) % ny, pz = pz_lo + (i / (nx * ny)) % nz,
+                      co = i / (nx * ny * nz);
+            const int64_t o = (((int64_t)b * CO + co) * g.PD + pz) * g.PH * g.PW + (int64_t)py * g.PW + px;
+            const int byte = P.am[o];
+            if (!(byte & 8)) continue;
+            const int k = byte & 7;
+            const int cz = 2 * pz - g.pd + (k >> 2), cy = 2 * py - g.ph + ((k >> 1) & 1), cx = 2 * px - g.pw + (k & 1);
+            const int zz = cz - cz0, yy = cy - cy0, xx = cx - cx0;
+            if (zz >= 0 && zz < g.ZL && yy >= 0 && yy < g.YL && xx >= 0 && xx < g.XL)
+                xs[co * g.CS + zz * g.ZS + yy * g.YS + xx] = P.dP[o];
+        }
     }
     float af[NS];
     constexpr int cpg = CO / G;
@@ -434,12 +440,13 @@ template <int CIN, int PZB, int PYB>
 __global__ __launch_bounds__(kThreads) void k_conv_wgrad(WgradParams P) {
     extern __shared__ float xs[];
     constexpr int NCT = ncol_tiles<CIN>();
-    constexpr int WP = CIN == 4 ? 4 : 1;  // waves splitting the positions
-    static_assert(CIN != 4 || NCT == kWgradTiles, "conv1 columns");
-    static_assert(CIN != 16 || NCT == 4 * kWgradTiles, "conv2/3 columns");
+    constexpr int WC = NCT / kWgradTiles;      // column groups (1 for conv1, 4 for conv2/3)
+    constexpr int WP = (kThreads / 64) / WC;   // position groups
+    static_assert(NCT % kWgradTiles == 0, "column tiles");
     const Geom& g = P.g;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, gq = lane >> 4;
-    const int t0c = WP == 4 ? 0 : wave * kWgradTiles;  // first column tile of this wave
+    const int wc = wave % WC, wp = wave / WC;
+    const int t0c = wc * kWgradTiles;  // first column tile of this wave
     // per column tile: LDS offset of (ci, tap) of column 16T + c, or a constant
     int koff[kWgradTiles];
     float kconst[kWgradTiles];  // -1: gather; else the constant B value
@@ -469,49 +476,83 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad(WgradParams P) {
                                  -g.pw);
         __syncthreads();
         const int64_t plane = ((int64_t)b * CO + c) * g.PD * g.PH * g.PW;
-        for (int t = (WP == 4 ? wave : 0); t < ntile; t += WP) {
-            const int tz = t / (PYB * nxt), ty = (t / nxt) % PYB, tx = t % nxt;
-            const int pz = pz0 + tz, py = py0 + ty, px = 2 * tx + (gq >> 1);
-            float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (pz < g.PD && py < g.PH && px < g.PW) {
-                const int64_t o = plane + ((int64_t)pz * g.PH + py) * g.PW + px;
-                const int byte = P.am[o];
-                if (byte & 8) {
-                    const float d = P.dP[o];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)  // position n = 4q + g: zc = q >> 1, yc = q & 1, xc = g
-                        a[q] = (byte & 7) == ((q >> 1) * 4 + (q & 1) * 2 + (gq & 1)) ? d : 0.0f;
+        // tiles t = t0, t0 + WP, ...: (tz, ty, tx) advanced incrementally; the
+        // next tile's pooled gradient + argmax byte are loaded before this
+        // tile's MFMAs, its 28 B values are gathered before the first MFMA
+        int tz = 0, ty = 0, tx = wp;
+        auto advance = [&](int& z, int& y, int& x) {
+            x += WP;
+            while (x >= nxt) {
+                x -= nxt;
+                if (++y == PYB) {
+                    y = 0;
+                    ++z;
                 }
             }
+        };
+        while (tx >= nxt) {
+            tx -= nxt;
+            if (++ty == PYB) {
+                ty = 0;
+                ++tz;
+            }
+        }
+        auto load_a = [&](int z, int y, int x, int& byte, float& d) {
+            const int pz = pz0 + z, py = py0 + y, px = 2 * x + (gq >> 1);
+            byte = 0;
+            d = 0.0f;
+            if (z < PZB && pz < g.PD && py < g.PH && px < g.PW) {
+                const int64_t o = plane + ((int64_t)pz * g.PH + py) * g.PW + px;
+                byte = P.am[o];
+                d = P.dP[o];
+            }
+        };
+        int byte, nbyte;
+        float d, nd;
+        load_a(tz, ty, tx, byte, d);
+        for (int t = wp; t < ntile; t += WP) {
+            int nz = tz, ny = ty, nx = tx;
+            advance(nz, ny, nx);
             const int tb = 2 * tz * g.ZS + 2 * ty * g.YS + 4 * tx + gq;
+            float bv[4][kWgradTiles];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int pb = tb + (q >> 1) * g.ZS + (q & 1) * g.YS;
 #pragma unroll
-                for (int T = 0; T < kWgradTiles; ++T) {
-                    const float bv = kconst[T] < 0.0f ? xs[pb + koff[T]] : kconst[T];
-                    acc[T] = mfma4(a[q], bv, acc[T]);
-                }
+                for (int T = 0; T < kWgradTiles; ++T) bv[q][T] = kconst[T] < 0.0f ? xs[pb + koff[T]] : kconst[T];
             }
+            load_a(nz, ny, nx, nbyte, nd);
+            float a[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)  // position n = 4q + g: zc = q >> 1, yc = q & 1, xc = g
+                a[q] = ((byte & 8) && (byte & 7) == ((q >> 1) * 4 + (q & 1) * 2 + (gq & 1))) ? d : 0.0f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int T = 0; T < kWgradTiles; ++T) acc[T] = mfma4(a[q], bv[q][T], acc[T]);
+            tz = nz;
+            ty = ny;
+            tx = nx;
+            byte = nbyte;
+            d = nd;
         }
     }
-    // D (lane (c, g)): rows co = 4g + r, column 16T + c
+    // D (lane (c, g)): rows co = 4g + r, column 16T + c; the WP position
+    // groups are summed through LDS in a fixed order
     float* out = P.part + (size_t)blockIdx.x * (CO * NCT * 16);
-    if constexpr (WP == 1) {
+    constexpr int REG = CO * NCT * 16;
+    __syncthreads();
+    float* R = xs;  // WP regions of 16 x NCT*16 (after the last item)
 #pragma unroll
-        for (int T = 0; T < kWgradTiles; ++T)
+    for (int T = 0; T < kWgradTiles; ++T)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) out[(4 * gq + r) * (NCT * 16) + 16 * (t0c + T) + c] = acc[T][r];
-    } else {
-        __syncthreads();
-        float* R = xs;  // 4 wave regions of 16 x 112 (after the last item)
+        for (int r = 0; r < 4; ++r) R[wp * REG + (4 * gq + r) * (NCT * 16) + 16 * (t0c + T) + c] = acc[T][r];
+    __syncthreads();
+    for (int i = threadIdx.x; i < REG; i += kThreads) {
+        float v = R[i];
 #pragma unroll
-        for (int T = 0; T < kWgradTiles; ++T)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) R[wave * (CO * NCT * 16) + (4 * gq + r) * (NCT * 16) + 16 * T + c] = acc[T][r];
-        __syncthreads();
-        for (int i = threadIdx.x; i < CO * NCT * 16; i += kThreads)
-            out[i] = (R[i] + R[CO * NCT * 16 + i]) + (R[2 * CO * NCT * 16 + i] + R[3 * CO * NCT * 16 + i]);
+        for (int k = 1; k < WP; ++k) v += R[k * REG + i];
+        out[i] = v;
     }
 }
 
@@ -633,7 +674,8 @@ int launch_wgrad(const rt_conv_layer* L, int32_t B, const float* x, const int64_
     constexpr int NCT = ncol_tiles<CIN>();
     const int nblk = wgrad_blocks<CIN, PZB, PYB>(L, B);
     if ((int64_t)nblk * CO * NCT * 16 > ws_floats) return rt_internal_fail(RT_EINVAL, "rt_conv_wgrad: workspace too small");
-    const size_t lds = (size_t)CIN * P.g.CS * sizeof(float);
+    constexpr int WC = NCT / kWgradTiles, WP = (kThreads / 64) / WC;
+    const size_t lds = std::max((size_t)CIN * P.g.CS, (size_t)WP * CO * NCT * 16) * sizeof(float);
     if (lds > 160 * 1024) return rt_internal_fail(RT_ELIMIT, "rt_conv_wgrad: tile exceeds LDS");
     static bool attr = false;
     if (!attr) {
