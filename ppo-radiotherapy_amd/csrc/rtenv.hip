@@ -178,8 +178,14 @@ __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
 // ---------------------------------------------------------------------------
 // libm sin/cos of the rotation half-angle (scipy from_rotvec): correctly
 // rounded in double-double on the range the env produces (<= 1.361).
-__device__ __forceinline__ double half_sin(double x) { return x <= 1.6 ? rtdd::sin_cr(x) : sin(x); }
-__device__ __forceinline__ double half_cos(double x) { return x <= 1.6 ? rtdd::cos_cr(x) : cos(x); }
+__device__ __forceinline__ void half_sincos(double x, double* s, double* c) {
+    if (x <= 1.6) {
+        rtdd::sincos_cr(x, s, c);
+    } else {
+        *s = sin(x);
+        *c = cos(x);
+    }
+}
 
 struct PoseOut {
     double pos[3], dir[3], os_t[3], os_r;
@@ -209,14 +215,16 @@ __device__ void pose_update(const Geom& G, const Consts& C, const double pos[3],
     double n0 = ddot_norm3(dir[0], dir[1], dir[2]);
     double d0 = dir[0] / n0, d1 = dir[1] / n0, d2 = dir[2] / n0;
     double ang = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    double sh, ch;
+    half_sincos(ang / 2.0, &sh, &ch);
     double s;
     if (ang <= 1e-3) {
         double a2 = ang * ang;
         s = 0.5 - a2 / 48.0 + a2 * a2 / 3840.0;
     } else {
-        s = half_sin(ang / 2.0) / ang;
+        s = sh / ang;
     }
-    double qx = s * r[0], qy = s * r[1], qz = s * r[2], qw = half_cos(ang / 2.0);
+    double qx = s * r[0], qy = s * r[1], qz = s * r[2], qw = ch;
     double x2 = qx * qx, y2 = qy * qy, z2 = qz * qz, w2 = qw * qw;
     double xy = qx * qy, zw = qz * qw, xz = qx * qz, yw = qy * qw, yz = qy * qz, xw = qx * qw;
     double m00 = x2 - y2 - z2 + w2, m01 = 2.0 * (xy - zw), m02 = 2.0 * (xz + yw);
@@ -1310,8 +1318,12 @@ int rt_host_tumour_sum(int64_t V, int32_t n, const int32_t* idx_h, const float* 
 int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h) {
     if (n < 0 || (n && (!x_h || !sin_h || !cos_h))) return fail(RT_EINVAL, "bad argument");
     for (int32_t i = 0; i < n; ++i) {
-        sin_h[i] = x_h[i] <= 1.6 ? rtdd::sin_cr(x_h[i]) : std::sin(x_h[i]);
-        cos_h[i] = x_h[i] <= 1.6 ? rtdd::cos_cr(x_h[i]) : std::cos(x_h[i]);
+        if (x_h[i] <= 1.6) {
+            rtdd::sincos_cr(x_h[i], &sin_h[i], &cos_h[i]);
+        } else {
+            sin_h[i] = std::sin(x_h[i]);
+            cos_h[i] = std::cos(x_h[i]);
+        }
     }
     return RT_OK;
 }

@@ -117,3 +117,20 @@ def test_exact_tumour_sum_plan(V):
         out = np.zeros(1, np.float32)
         assert L.rt_host_tumour_sum(V, idx.size, idx.ctypes.data, vals.ctypes.data, out.ctypes.data) == 0
         assert out[0] == np.sum(dense.reshape(-1)), (V, trial)
+
+
+def test_fast_sincos_matches_plain_double_double(tmp_path):
+    """rtdd::sincos_cr (the device path of scipy's from_rotvec half angle)
+    returns the bits of the plain 18-term double-double sin/cos
+    (tools/check_sincos.cpp; 5e7 arguments were checked when it was written)."""
+    import shutil
+    import subprocess
+
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = tmp_path / "check_sincos"
+    subprocess.run([gxx, "-O2", "-ffp-contract=off", "-I", os.path.join(REPO, "ppo-radiotherapy_amd", "csrc"),
+                    os.path.join(REPO, "tools", "check_sincos.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "1000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
