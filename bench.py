@@ -24,7 +24,10 @@ Also reported:
                          library records around it on the env stream over
                          the timed region; traffic from profiles/k_dense_pmc.json
   cpu_baseline           op-for-op NumPy port of the reference step on one
-                         host core, same 64^3 workload (bounded sample)
+                         host core, same 64^3 workload (bounded sample); beside
+                         it the same on all host cores and the scalar C port
+  roofline.measured_copy_ceiling_GBps
+                         device copy bandwidth measured in the same run
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       (N > 1 under torch.distributed.run, one rank per GPU)
@@ -72,7 +75,8 @@ def parse():
     ap.add_argument("--num-steps", type=int, default=64)
     ap.add_argument("--num-minibatches", type=int, default=8)
     ap.add_argument("--update-epochs", type=int, default=10)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="CPU-baseline sample budget per leg (4 legs: numpy/C x 1/all cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-update", action="store_true")
     ap.add_argument("--env-only", action="store_true", help="time rt_env_step alone (profiling)")
@@ -103,27 +107,51 @@ def trainer_cfg(a):
                            micro_batch=a.micro_batch)
 
 
-def cpu_baseline(lib, seconds: float):
-    """One-core NumPy port of the reference step on the same 64^3 workload."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    from numpy_env import NumpyEnv
+def cpu_baseline(grid: int, seconds: float):
+    """The reference's single-env step on the host cores (oracle/cpu_bench.py,
+    run as a child process): the op-for-op NumPy port on one core is `value`;
+    the same on every available core (one pinned process each, capped at 16)
+    and the scalar C restatement are reported beside it."""
+    import subprocess
 
-    rng = np.random.default_rng(0)
-    env = NumpyEnv(lib.lungs, lib.tumour_dense(0))
-    env.reset()
-    n, t0 = 0, time.perf_counter()
-    while True:
-        a = rng.uniform(-1, 1, 6).astype(np.float32)
-        _, _, done = env.step(a)
-        n += 1
-        if done:
-            env.reset(lib.tumour_dense(int(rng.integers(lib.n_tumours))))
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            break
-    return {"value": n / dt, "unit": "env steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} visionless steps of one env at {lib.shape[0]}x{lib.shape[1]}x{lib.shape[2]} "
-                      f"(oracle/numpy_env.py, U(-1,1) actions, autoreset), {dt:.1f} s on 1 host core"}
+    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_bench.py"), "--grid", str(grid),
+           "--seconds", str(seconds), "--kinds", "numpy,c"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=20 * seconds + 300)
+    if r.returncode != 0:
+        return {"error": r.stderr[-2000:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    one = d["numpy"]["one_core"]
+    out = {"value": one["value"], "unit": "env steps/s", "cores": 1, "kind": "port",
+           "sample": f"{one['steps']} visionless steps of one env at {grid}^3 (oracle/numpy_env.py, "
+                     f"U(-1,1) actions, autoreset), {one['seconds']:.1f} s on 1 host core ({d['cpu_model']})",
+           "cpu_model": d["cpu_model"], "cores_available": d["cores_available"]}
+    if "all_cores" in d["numpy"]:
+        out["all_cores"] = {k: d["numpy"]["all_cores"][k] for k in ("value", "cores", "steps")}
+    out["c_port"] = {"one_core": d["c"]["one_core"]["value"],
+                     "all_cores": d["c"].get("all_cores", {}).get("value"),
+                     "cores": d["c"].get("all_cores", {}).get("cores", 1)}
+    return out
+
+
+def copy_ceiling(dev, gib: float = 2.0, reps: int = 10) -> float:
+    """Measured device-to-device copy bandwidth (STREAM copy: read + write
+    bytes / time), the achievable HBM ceiling beside the 8 TB/s spec."""
+    import torch
+
+    n = int(gib * (1 << 30)) // 4
+    src = torch.ones(n, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    bw = 2 * 4 * n * reps / (e0.elapsed_time(e1) * 1e-3)
+    del src, dst
+    torch.cuda.empty_cache()
+    return bw
 
 
 def load_pmc(grid, envs):
@@ -209,7 +237,6 @@ def main():
 
     # ---------------- timed rollout (or env-only)
     K = a.steps
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     actions = torch.rand((a.envs, 6), device=dev, generator=gen) * 2 - 1
     env.kernel_timing(K)  # HIP events around k_beam / k_dense / k_finish on the env stream
     barrier()
@@ -217,19 +244,17 @@ def main():
     t0 = time.perf_counter()
     if a.env_only:
         for i in range(K):
-            evs[i][0].record()
             env.step(actions, info_out=tr.infos[i % T])
-            evs[i][1].record()
     else:
         for i in range(K):
-            tr.rollout_step(i % T, evs[i])
+            tr.rollout_step(i % T)
     torch.cuda.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
-    env_ms = max_over_ranks(float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs])))
     kms, kcalls = env.kernel_timing_read()
     env.kernel_timing(0)
     kms = {k: max_over_ranks(v) for k, v in kms.items()}
+    env_ms = sum(kms.values())  # k_beam start -> k_finish end, per step
     total_envs = a.envs * world
     steps_per_s = total_envs * K / dt
 
@@ -276,6 +301,10 @@ def main():
             "env_step_frac_of_hbm": a.envs * 4 * V / (env_ms * 1e-3) / HBM_PEAK,
             "survey_model_bytes_per_env_step": 8 * V,
             "survey_model_frac": a.envs * 8 * V / (env_ms * 1e-3) / HBM_PEAK}
+    if rank == 0 and not a.env_only:
+        cbw = copy_ceiling(dev)
+        roof["measured_copy_ceiling_GBps"] = cbw / 1e9
+        roof["frac_of_measured_ceiling"] = achieved / cbw
 
     # ---------------- the other step formulation, same workload (policy in the loop)
     other = None
@@ -347,7 +376,7 @@ def main():
         out["other_step_mode"] = other
     out["roofline"] = roof
     if rank == 0 and world == 1 and not a.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(lib, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(a.grid, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     env.close()

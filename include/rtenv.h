@@ -15,6 +15,7 @@
  *   apply_rotation/translation transforms.py:7,62| rt_debug_pose (parity hook)
  *   GAE loop                  train.py:163-181  | rt_gae
  *   agent.get_action_and_value train.py:143-149 | rt_policy_sample (visionless agent)
+ *   rollout step (policy + env) train.py:143-158 | rt_env_step_policy (fused)
  *   PPO minibatch step        train.py:197-246  | rt_ppo_grad + rt_adam_step / rt_ppo_update
  *   FeaturesExtractor3D.cnn   networks.py:8-45  | rt_conv_relu_pool_fwd (+ backward kernels)
  *
@@ -186,6 +187,31 @@ int rt_policy_sample(const float* const* params_d, int32_t n_params_tensors, int
                      const float* obs_d, const uint8_t* done_d, float* obs_out_d, float* done_out_d,
                      float* act_out_d, float* logp_out_d, float* value_out_d, uint64_t seed,
                      uint64_t counter, int64_t env_id_base, void* stream);
+
+/* Fused rollout step of the visionless agent (train.py:143-158): the
+ * policy sample of rt_policy_sample (same arithmetic, same bits) and
+ * rt_env_step in ONE launch per step in incremental step mode (policy, pose
+ * update, beam march and finish on one wave per env), two more (k_dense,
+ * k_finish) in dense mode.  The env acts on the sampled actions
+ * (act_store_d); outputs as rt_env_step.  obs_in_d may be obs_d (the env's
+ * observation buffer of the previous step). */
+typedef struct rt_policy_step {
+    const float* const* params;   /* 13 device pointers, rt_policy_sample order (host array) */
+    int32_t n_params;             /* 13 */
+    const float* obs_in;          /* [N][9] observation acted on (next_obs) */
+    const uint8_t* done_in;       /* [N] next_done (env terminated) or NULL */
+    float* obs_store;             /* [N][9] storage obs[step] */
+    float* done_store;            /* [N]    storage dones[step] */
+    float* act_store;             /* [N][6] storage actions[step] */
+    float* logp_store;            /* [N]    storage logprobs[step] */
+    float* value_store;           /* [N]    storage values[step] */
+    uint64_t seed;                /* Philox key */
+    uint64_t counter;             /* Philox call counter (one per step) */
+    int64_t env_id_base;          /* global id of env 0 (rank * N) */
+} rt_policy_step;
+
+int rt_env_step_policy(rt_env* env, const rt_policy_step* step, float* obs_d, float* reward_d,
+                       uint8_t* terminated_d, float* info_d, void* stream);
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */

@@ -32,6 +32,7 @@ EXPORTS = [
     "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
+    "rt_env_step_policy",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
     "rt_ppo_shuffle", "rt_ppo_adv_stats",
     "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
@@ -88,6 +89,13 @@ class RtPpoHparams(ctypes.Structure):
     ]
 
 
+class RtPolicyStep(ctypes.Structure):
+    _fields_ = [("params", ctypes.POINTER(ctypes.c_void_p)), ("n_params", ctypes.c_int32)] + [
+        (k, ctypes.c_void_p) for k in ("obs_in", "done_in", "obs_store", "done_store", "act_store", "logp_store",
+                                       "value_store")] + [
+        ("seed", ctypes.c_uint64), ("counter", ctypes.c_uint64), ("env_id_base", ctypes.c_int64)]
+
+
 class RtConvLayer(ctypes.Structure):
     _fields_ = [("cin", ctypes.c_int32), ("groups", ctypes.c_int32), ("in_dims", ctypes.c_int32 * 3),
                 ("pool_pad", ctypes.c_int32 * 3)]
@@ -136,6 +144,7 @@ def load(build_if_missing: bool = True):
         "rt_gae": ([i32, i32, vp, vp, vp, vp, vp, f64, f64, vp, vp, vp], ctypes.c_int),
         "rt_policy_sample": ([ctypes.POINTER(vp), i32, i32, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint64,
                               ctypes.c_uint64, i64, vp], ctypes.c_int),
+        "rt_env_step_policy": ([vp, ctypes.POINTER(RtPolicyStep), vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_ppo_workspace_floats": ([i32], i64),
         "rt_ppo_num_params": ([], i32),
         "rt_ppo_grad": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, vp,

@@ -38,7 +38,7 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = (*SRCS, HDR, os.path.join(PKG, "csrc", "rt_ddmath.h"), __file__)
+    deps = (*SRCS, HDR, os.path.join(PKG, "csrc", "rt_ddmath.h"), os.path.join(PKG, "csrc", "rt_trace.h"), __file__)
     return any(os.path.getmtime(p) > t for p in deps)
 
 

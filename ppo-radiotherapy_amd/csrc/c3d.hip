@@ -359,7 +359,7 @@ __global__ __launch_bounds__(conv_threads<16>()) void k_conv_dgrad(DgradParams P
     constexpr int NS = nsteps<16>();
     const Geom& g = P.g;
     const int b = blockIdx.z, z0 = blockIdx.y * 2 * PZB, y0 = blockIdx.x * 2 * PYB;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, gq = lane >> 4;
+    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
     // stage dY[co][z0-2 .., y0-2 .., -2 ..] into LDS: zero the tile, then each
     // pooling window that overlaps it scatters its gradient to its recorded
     // maximum (one argmax byte + one gradient load per window, not per position)

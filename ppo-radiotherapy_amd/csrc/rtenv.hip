@@ -33,6 +33,8 @@
 
 #include "rtenv.h"
 #include "rt_ddmath.h"
+#include "rt_trace.h"
+#include "policy_core.h"
 
 namespace {
 
@@ -41,6 +43,7 @@ constexpr int kUnroll = 8;               // float4 loads in flight per thread
 constexpr int kSliceVec = 8192;          // k_dense slice: 8192 float4 = 128 KiB of dose
 constexpr int kMaxTumourVoxels = 16384;  // tumour voxels (op slots n + n-1 < 2^16; k_finish LDS per wave)
 constexpr int kMaxGridDim = 1024;
+constexpr int kMaxPlanLevels = 64;       // levels of a tumour's sum plan (LDS copy in k_finish)
 constexpr float kEpsF = 1e-6f;           // draw_line.py:4 (f32 under NEP 50)
 
 enum : int32_t { MODE_NOOP = 0, MODE_STEP = 1, MODE_RESET = 2 };
@@ -129,11 +132,15 @@ struct EnvState {
 struct Library {
     const uint32_t* lung_bits;
     const int32_t* vox;
+    const uint32_t* coord;   // per tumour voxel: x << 20 | y << 10 | z (no divisions in k_finish)
     const uint32_t* ops;     // packed (a | b << 16); dst = n + op index
     const int32_t* lvl_end;  // per level: op index end (relative to op_base)
     const TumourMeta* meta;
     int32_t K;
 };
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* glb_ptr_t;
 
 // ---------------------------------------------------------------------------
 // Device numerics helpers
@@ -345,9 +352,12 @@ __device__ int beam_setup(const int32_t g[3], const double pos_d[3], const doubl
 }
 
 // Splats of march iteration k given its intery/interz (draw_line.py:69-100).
-// Writes up to 4 in-bounds (flat idx, weight) in reference order; returns count.
-__device__ __forceinline__ int march_splats(const int32_t g[3], const BeamSetup& s, int k, float y,
-                                            float z, int32_t idx[4], float w[4]) {
+// Slot q = 2*dy + dz (the reference's order) holds the flat index and weight,
+// or index -1 when the voxel is outside the grid.  Fixed slots keep the
+// arrays in registers (a compacted list would be indexed dynamically and
+// spill to scratch).
+__device__ __forceinline__ void march_splats(const int32_t g[3], const BeamSetup& s, int k, float y, float z,
+                                             int32_t idx[4], float w[4]) {
     int x = s.start + k * s.stepdir;
     int yf = (int)floorf(y), zf = (int)floorf(z);
     float yfr = y - (float)yf;
@@ -356,7 +366,6 @@ __device__ __forceinline__ int march_splats(const int32_t g[3], const BeamSetup&
     const int b0 = s.dom == 0 ? x : yf;
     const int b1 = s.dom == 1 ? x : (s.dom == 0 ? yf : zf);
     const int b2 = s.dom == 2 ? x : zf;
-    int n = 0;
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
 #pragma unroll
@@ -365,14 +374,16 @@ __device__ __forceinline__ int march_splats(const int32_t g[3], const BeamSetup&
             float ww = wy * (dz == 0 ? (1.0f - zfr) : zfr);
             // draw_line.py:88-90: +dy/+dz always on axes 1/2
             int ix = b0, iy = b1 + dy, iz = b2 + dz;
-            if (ix >= 0 && ix < g[0] && iy >= 0 && iy < g[1] && iz >= 0 && iz < g[2]) {
-                idx[n] = (ix * g[1] + iy) * g[2] + iz;
-                w[n] = ww;
-                ++n;
-            }
+            const bool in = ix >= 0 && ix < g[0] && iy >= 0 && iy < g[1] && iz >= 0 && iz < g[2];
+            idx[2 * dy + dz] = in ? (ix * g[1] + iy) * g[2] + iz : -1;
+            w[2 * dy + dz] = ww;
         }
     }
-    return n;
+}
+
+__device__ __forceinline__ void no_splats(int32_t idx[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) idx[q] = -1;
 }
 
 struct BeamParams {
@@ -395,7 +406,7 @@ struct BeamParams {
 // tumour sampling on reset (environment.py:86-105), f64 pose update
 // (environment.py:196-210) and the f32 beam setup (draw_line.py:17-66).
 // ---------------------------------------------------------------------------
-__device__ BeamSetup pose_step(const BeamParams& P, int e) {
+__device__ BeamSetup pose_step(const BeamParams& P, int e, const float* act) {
     const EnvState& st = P.st;
     BeamSetup s{};
     int32_t flags = st.flags[e];
@@ -435,11 +446,19 @@ __device__ BeamSetup pose_step(const BeamParams& P, int e) {
         s.tumour = st.tumour[e];
         float a[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) a[i] = P.actions[(size_t)e * 6 + i];
+        for (int i = 0; i < 6; ++i) a[i] = act ? act[i] : P.actions[(size_t)e * 6 + i];
         double pos[3] = {pose[0], pose[1], pose[2]};
         double dir[3] = {pose[3], pose[4], pose[5]};
+#ifdef RT_TRACE
+        if (pos[0] + dir[0] + a[0] == 12345.0) pose[0] = 0.0;  // consume the loads before the stamp
+#endif
+        RT_STAMP(e, 10);
         PoseOut o;
         pose_update(P.G, P.C, pos, dir, a, o);
+#ifdef RT_TRACE
+        if (o.dir[0] == 12345.0) pose[0] = 0.0;
+#endif
+        RT_STAMP(e, 11);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             pose[i] = o.pos[i];
@@ -472,15 +491,19 @@ __device__ __forceinline__ float rfl_f(float x) {
 // owns the voxel and adds its neighbour's weight: fl32(w_k + w_k+1) is exactly
 // the reference's `output[...] += weight` sequence (IEEE add commutes).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_beam(BeamParams P) {
-    const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (e >= P.N) return;  // wave-uniform
+// act: the env's 6 action floats in registers (fused policy step) or null
+// (read from P.actions).
+// act: the env's 6 action floats in registers (fused policy step) or null
+// (read from P.actions).
+__device__ void beam_env(const BeamParams& P, int e, int lane, const float* act) {
     BeamSetup s{};
     if (lane == 0) {
-        s = pose_step(P, e);
+        RT_STAMP(e, 2);
+        s = pose_step(P, e, act);
         P.st.setup[e] = s;
+        RT_STAMP(e, 3);
     }
+    if (lane == 0) RT_STAMP(e, 12);
     const int mode = rfl_i(s.mode);
     if (P.incremental && mode == MODE_RESET) {
         // reset_dose (environment.py:104) for the incremental step: k_dense is not run
@@ -529,17 +552,22 @@ __global__ __launch_bounds__(256) void k_beam(BeamParams P) {
         }
         int32_t ci[4], pi[4], ni[4];
         float cw[4], pw[4], nw[4];
-        int nc = march_splats(P.G.g, b, k, yk, zk, ci, cw);
-        int np = 0, nn = 0;
-        if (pairs && k > 0) np = march_splats(P.G.g, b, k - 1, ya, za, pi, pw);
-        if (pairs && k + 1 < niter) nn = march_splats(P.G.g, b, k + 1, yk + b.sgy, zk + b.sgz, ni, nw);
-        for (int i = 0; i < nc; ++i) {
+        march_splats(P.G.g, b, k, yk, zk, ci, cw);
+        if (pairs && k > 0) march_splats(P.G.g, b, k - 1, ya, za, pi, pw);
+        else no_splats(pi);
+        if (pairs && k + 1 < niter) march_splats(P.G.g, b, k + 1, yk + b.sgy, zk + b.sgz, ni, nw);
+        else no_splats(ni);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
             const int32_t v = ci[i];
+            if (v < 0) continue;
             bool owned = true;
-            for (int j = 0; j < np; ++j) owned = owned && (pi[j] != v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) owned = owned && (pi[j] != v);
             if (!owned) continue;
             float w = cw[i];
-            for (int j = 0; j < nn; ++j)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
                 if (ni[j] == v) w = w + nw[j];
             const float old_d = dose[v];
             const float new_d = clip01(old_d + w * bd);
@@ -567,6 +595,14 @@ __global__ __launch_bounds__(256) void k_beam(BeamParams P) {
             P.st.lung_sum[e] += dsum;
         }
     }
+    if (lane == 0) RT_STAMP(e, 4);
+}
+
+__global__ __launch_bounds__(256) void k_beam(BeamParams P) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (e >= P.N) return;  // wave-uniform
+    beam_env(P, e, lane, nullptr);
 }
 
 __device__ __forceinline__ float wave_sum_f(float v) {
@@ -835,8 +871,10 @@ __device__ void hash_beam(const Geom& G, const BeamSetup& b, int lane, int32_t* 
         }
         int32_t idx[4];
         float w[4];
-        const int n = march_splats(G.g, b, k, y, z, idx, w);
-        for (int i = 0; i < n; ++i) hash_add(keys, vals, mask, idx[i], w[i]);
+        march_splats(G.g, b, k, y, z, idx, w);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (idx[i] >= 0) hash_add(keys, vals, mask, idx[i], w[i]);
     }
 }
 
@@ -900,13 +938,9 @@ __device__ void vision_scatter(const FinishParams& P, int e, int lane, const dou
 //  - combine k_dense slices; rewards (environment.py:164-191), termination,
 //    obs (environment.py:259-268), info, episode statistics
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_finish(FinishParams P) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int e = blockIdx.x * P.wpb + w;
-    if (e >= P.N) return;
-    extern __shared__ __attribute__((aligned(16))) unsigned char fsm_raw[];
-    unsigned char* wave_lds = fsm_raw + (size_t)w * P.wave_lds;
+__device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char* wave_lds) {
     float* tvals = reinterpret_cast<float*>(wave_lds);
+    if (lane == 0) RT_STAMP(e, 5);
     const BeamSetup s = P.st.setup[e];
     const TumourMeta m = P.lib.meta[s.tumour];
     const double* pose = P.st.pose + (size_t)e * 6;
@@ -926,18 +960,34 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
     const float* dose = P.st.dose + (size_t)e * P.G.Vpad;
     const int nt = m.n;
     const int32_t* tv = P.lib.vox + m.vox_base;
+    const uint32_t* tc = P.lib.coord + m.vox_base;
     const double px = pose[0], py = pose[1], pz = pose[2];
     const int W = P.G.g[2], H = P.G.g[1], HW = H * W;
+    // the sum plan's operands and level ends -> LDS by async copies (no VGPRs),
+    // in flight during the gather; the plan below then touches only LDS
+    uint32_t* ops_s = reinterpret_cast<uint32_t*>(tvals + 2 * P.max_tvox);
+    int32_t* lev_s = reinterpret_cast<int32_t*>(ops_s + P.max_tvox);
+    {
+        const uint32_t* ops = P.lib.ops + m.op_base;
+        const int32_t* lend = P.lib.lvl_end + m.lvl_base;
+        const int nops = nt - 1;  // a binary sum tree over nt leaves (checked at create)
+        for (int o = 0; o < nops; o += 64)
+            if (lane < nops - o)
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(ops + o + lane), (lds_ptr_t)(ops_s + o), 4, 0, 0);
+        if (lane < m.nlev)
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(lend + lane), (lds_ptr_t)lev_s, 4, 0, 0);
+    }
     int ctum = 0;
     double best = INFINITY;
     int bidx = 0x7fffffff;
     for (int i = lane; i < nt; i += 64) {
         const int v = tv[i];
+        const uint32_t c = tc[i];
         const float x = dose[v];
         tvals[i] = x;
         const bool lung = (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u;
         ctum += (lung && x > P.C.lung_thr) ? 1 : 0;
-        const int ix = v / HW, iy = (v / W) % H, iz = v % W;
+        const int ix = (int)(c >> 20), iy = (int)((c >> 10) & 1023u), iz = (int)(c & 1023u);
         const double d0 = (double)ix - px, d1 = (double)iy - py, d2 = (double)iz - pz;
         const double nn = sqrt((d0 * d0 + d1 * d1) + d2 * d2);  // np.linalg.norm(axis=1) order
         if (nn < best) {
@@ -955,22 +1005,23 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
             bidx = oi;
         }
     }
+    if (lane == 0) RT_STAMP(e, 6);
     // exact np.sum(dose * tumours): level plan (slots: leaves 0..n-1, op o -> n+o)
     {
-        const uint32_t* ops = P.lib.ops + m.op_base;
-        const int32_t* lend = P.lib.lvl_end + m.lvl_base;
+        __builtin_amdgcn_s_waitcnt(0);  // the async copies above have landed
         int lo = 0;
         for (int l = 0; l < m.nlev; ++l) {
             lds_wave_sync();
-            const int hi = lend[l];
+            const int hi = lev_s[l];
             for (int o = lo + lane; o < hi; o += 64) {
-                const uint32_t ab = ops[o];
+                const uint32_t ab = ops_s[o];
                 tvals[nt + o] = tvals[ab & 0xffffu] + tvals[ab >> 16];
             }
             lo = hi;
         }
         lds_wave_sync();
     }
+    if (lane == 0) RT_STAMP(e, 7);
     int cnt = 0;
     double dl = 0.0;
     if (P.incremental) {
@@ -1024,8 +1075,89 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
             inf[RT_INFO_EP_RETURN] = (float)ret;
             inf[RT_INFO_EP_LENGTH] = (float)len;
         }
+        RT_STAMP(e, 8);
     }
     if (P.vision) vision_scatter(P, e, lane, pose, m, wave_lds);
+}
+
+__global__ __launch_bounds__(256) void k_finish(FinishParams P) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int e = blockIdx.x * P.wpb + w;
+    if (e >= P.N) return;
+    extern __shared__ __attribute__((aligned(16))) unsigned char fsm_raw[];
+    finish_env(P, e, lane, fsm_raw + (size_t)w * P.wave_lds);
+}
+
+// ---------------------------------------------------------------------------
+// k_step_policy: the rollout step of the visionless agent fused with the env
+// step (train.py:143-158): one wave per env, `wpb` envs per block.  The block
+// stages the policy parameters in LDS, each wave samples its env's action
+// (policy_core.h: the same arithmetic as k_policy_sample, so the same bits),
+// writes the step's rollout storage, then runs the env's pose update + beam
+// march (beam_env) on that action from registers.  FINISH (incremental step
+// mode, no dense pass in between): the same wave then finishes the env
+// (finish_env), so the whole step is one launch.  The finish reuses the LDS
+// of the parameters after a block barrier.
+// ---------------------------------------------------------------------------
+struct PolicyStepParams {
+    rtpol::Weights w;
+    const float* obs_in;       // [N][9]  the observation the policy acts on
+    const uint8_t* done_in;    // [N]     next_done or null
+    float* obs_store;          // [N][9]  storage obs[step]
+    float* done_store;         // [N]
+    float* act_store;          // [N][6]
+    float* logp_store;         // [N]
+    float* value_store;        // [N]
+    uint64_t seed;
+    uint64_t counter;
+    int64_t id_base;
+    int32_t wpb;
+};
+
+template <bool FINISH>
+__global__ __launch_bounds__(1024) void k_step_policy(BeamParams B, FinishParams F, PolicyStepParams Q) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+    rtpol::Lds& L = *reinterpret_cast<rtpol::Lds*>(psm);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int e = blockIdx.x * Q.wpb + w;
+    const bool live = e < B.N;
+    if (lane == 0) RT_STAMP(e, 0);
+    rtpol::stage(L, Q.w, tid, (int)blockDim.x);
+    __syncthreads();
+    float act = 0.0f;
+    if (live) {
+        if (lane == 0) RT_STAMP(e, 9);
+        float* h1 = reinterpret_cast<float*>(psm + sizeof(rtpol::Lds)) + w * rtpol::H;
+        float x[rtpol::NOBS];
+#pragma unroll
+        for (int i = 0; i < rtpol::NOBS; ++i) x[i] = Q.obs_in[(size_t)e * rtpol::NOBS + i];
+        const rtpol::Sample smp = rtpol::policy_env(L, h1, x, lane, Q.seed, Q.counter, (uint64_t)(Q.id_base + e));
+        if (lane < rtpol::NOBS) {
+            float xi = x[0];
+#pragma unroll
+            for (int i = 1; i < rtpol::NOBS; ++i) xi = lane == i ? x[i] : xi;
+            Q.obs_store[(size_t)e * rtpol::NOBS + lane] = xi;
+        }
+        if (lane == rtpol::NOBS) Q.done_store[e] = Q.done_in ? (float)Q.done_in[e] : 0.0f;
+        if (lane < rtpol::NACT) Q.act_store[(size_t)e * rtpol::NACT + lane] = smp.action;
+        if (lane == 0) {
+            Q.logp_store[e] = smp.logp;
+            Q.value_store[e] = smp.value;
+            RT_STAMP(e, 1);
+        }
+        act = smp.action;
+    }
+    if (FINISH) __syncthreads();  // every wave is done with the parameters' LDS
+    if (!live) return;
+    float a6[rtpol::NACT];
+#pragma unroll
+    for (int i = 0; i < rtpol::NACT; ++i) a6[i] = rtpol::lane_f(act, i);
+    beam_env(B, e, lane, a6);
+    if (FINISH) {
+        // this wave's dose stores are visible to its own lanes' loads below
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        finish_env(F, e, lane, psm + (size_t)w * F.wave_lds);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1047,12 +1179,14 @@ __global__ void k_debug_beam(Geom G, int m, const double* pos, const double* dir
     for (int k = 0; k < s.niter; ++k) {
         int32_t ii[4];
         float ww[4];
-        int q = march_splats(G.g, s, k, y, z, ii, ww);
-        for (int i = 0; i < q; ++i, ++n) {
+        march_splats(G.g, s, k, y, z, ii, ww);
+        for (int i = 0; i < 4; ++i) {
+            if (ii[i] < 0) continue;
             if (n < cap) {
                 idx_out[(size_t)c * cap + n] = ii[i];
                 w_out[(size_t)c * cap + n] = ww[i];
             }
+            ++n;
         }
         y = y + s.sgy;
         z = z + s.sgz;
@@ -1210,6 +1344,8 @@ struct rt_env {
     size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
     int finish_wave_lds = 0; // bytes per wave
     int finish_wpb = 4;      // k_finish envs per block
+    int fused_wpb = 16;      // k_step_policy envs (waves) per block
+    size_t fused_smem = 0;   // k_step_policy dynamic LDS
     uint32_t view_hash_mask = 0;
     int32_t* part_cnt = nullptr;
     double* part_sum = nullptr;
@@ -1285,6 +1421,8 @@ Consts make_consts(const rt_env_config& c) {
 }
 
 }  // namespace
+
+RT_TRACE_READ_FN(rt_trace_read_env)
 
 extern "C" {
 
@@ -1390,6 +1528,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     }
     std::vector<TumourMeta> meta(K);
     std::vector<int32_t> vox;
+    std::vector<uint32_t> coord;
     std::vector<uint32_t> ops;
     std::vector<int32_t> lvl_end;
     int max_n = 0;
@@ -1423,6 +1562,11 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
             m.obs_c[i] = (float)(c / G.S[i] * 2.0 - 1.0);
         }
         vox.insert(vox.end(), iv, iv + n);
+        for (int i = 0; i < n; ++i) {
+            const int64_t v = iv[i];
+            coord.push_back((uint32_t)(v / ((int64_t)G.g[1] * G.g[2])) << 20 |
+                            (uint32_t)((v / G.g[2]) % G.g[1]) << 10 | (uint32_t)(v % G.g[2]));
+        }
         PlanBuilder pb{iv, n, (int64_t)G.V};
         int res = pb.build();
         // order ops by level; op at sorted position o writes slot n + o
@@ -1445,6 +1589,10 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
                 ++nlev;
             }
         }
+        if (nops != n - 1 || nlev > kMaxPlanLevels) {
+            free_env(env);
+            return fail(RT_ELIMIT, "tumour sum plan: unexpected shape");
+        }
         m.nlev = nlev;
         m.result = res < 0 ? -1 : slot(res);
     }
@@ -1455,23 +1603,38 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     env->slices = (nvec + env->vec_per_slice - 1) / env->vec_per_slice;
     const int maxdim = std::max(G.g[0], std::max(G.g[1], G.g[2]));
     env->view_hash_mask = env->visionless ? 0u : next_pow2((uint32_t)(8 * (maxdim + 2))) - 1;
-    size_t wave_bytes = (size_t)2 * max_n * sizeof(float);
-    if (!env->visionless) wave_bytes += (size_t)(env->view_hash_mask + 1) * 8;
+    // per wave: plan slots (2 n floats), then either the plan's operands and
+    // level ends (STEP) or the vision beam-view hash (used after the plan)
+    size_t plan_bytes = (size_t)max_n * sizeof(uint32_t) + kMaxPlanLevels * sizeof(int32_t);
+    size_t hash_bytes = env->visionless ? 0 : (size_t)(env->view_hash_mask + 1) * 8;
+    size_t wave_bytes = (size_t)2 * max_n * sizeof(float) + std::max(plan_bytes, hash_bytes);
     wave_bytes = (wave_bytes + 15) / 16 * 16;
     env->finish_wave_lds = (int)wave_bytes;
     env->finish_wpb = 4;
     while (env->finish_wpb > 1 && (size_t)env->finish_wpb * wave_bytes > 160 * 1024) env->finish_wpb /= 2;
     env->finish_smem = (size_t)env->finish_wpb * wave_bytes;
     if (env->finish_smem > 160 * 1024) { free_env(env); return fail(RT_ELIMIT, "LDS budget exceeded"); }
+    // k_step_policy: parameters + per-wave h1, or (incremental, after the
+    // barrier) the per-wave finish scratch in the same bytes
+    auto fused_bytes = [&](int wpb) {
+        size_t pol = sizeof(rtpol::Lds) + (size_t)wpb * rtpol::H * sizeof(float);
+        size_t fin = env->incremental ? (size_t)wpb * wave_bytes : 0;
+        return std::max(pol, fin);
+    };
+    env->fused_wpb = 16;
+    while (env->fused_wpb > 1 && fused_bytes(env->fused_wpb) > 160 * 1024) env->fused_wpb /= 2;
+    env->fused_smem = fused_bytes(env->fused_wpb);
 
     // ---- device allocations ----
     const int N = env->N;
     uint32_t* d_lbits;
+    uint32_t* d_coord;
     int32_t *d_vox, *d_lvl;
     uint32_t* d_ops;
     TumourMeta* d_meta;
     EnvState& st = env->st;
     if ((rc = dev_alloc(env, &d_lbits, lbits.size())) || (rc = dev_alloc(env, &d_vox, vox.size())) ||
+        (rc = dev_alloc(env, &d_coord, coord.size())) ||
         (rc = dev_alloc(env, &d_ops, ops.size())) || (rc = dev_alloc(env, &d_lvl, lvl_end.size())) ||
         (rc = dev_alloc(env, &d_meta, meta.size())) ||
         (rc = dev_alloc(env, &st.dose, (size_t)N * G.Vpad)) || (rc = dev_alloc(env, &st.pose, (size_t)N * 6)) ||
@@ -1493,6 +1656,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         pose0[(size_t)e * 6 + 4] = 1.0;
     }
     if (h2d(d_lbits, lbits.data(), lbits.size() * 4) || h2d(d_vox, vox.data(), vox.size() * 4) ||
+        h2d(d_coord, coord.data(), coord.size() * 4) ||
         (ops.size() && h2d(d_ops, ops.data(), ops.size() * 4)) ||
         (lvl_end.size() && h2d(d_lvl, lvl_end.data(), lvl_end.size() * 4)) ||
         h2d(d_meta, meta.data(), meta.size() * sizeof(TumourMeta)) ||
@@ -1508,6 +1672,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     }
     env->lib.lung_bits = d_lbits;
     env->lib.vox = d_vox;
+    env->lib.coord = d_coord;
     env->lib.ops = d_ops;
     env->lib.lvl_end = d_lvl;
     env->lib.meta = d_meta;
@@ -1525,13 +1690,8 @@ float* rt_env_dose(rt_env* env, int64_t* stride) {
     return env->st.dose;
 }
 
-static int launch_step(rt_env* env, bool reset_call, const float* actions, const uint8_t* mask,
-                       const int32_t* ids, float* obs, float* reward, uint8_t* term, float* info,
-                       hipStream_t stream) {
-    const int N = env->N;
-    hipEvent_t* ev = nullptr;
-    if (env->timing_cap > 0 && env->timing_n < env->timing_cap) ev = &env->tev[(size_t)4 * env->timing_n++];
-    if (ev) (void)hipEventRecord(ev[0], stream);
+BeamParams beam_params(const rt_env* env, bool reset_call, const float* actions, const uint8_t* mask,
+                       const int32_t* ids) {
     BeamParams bp{};
     bp.G = env->G;
     bp.C = env->C;
@@ -1540,13 +1700,46 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
     bp.actions = actions;
     bp.reset_mask = mask;
     bp.reset_ids = ids;
-    bp.N = N;
+    bp.N = env->N;
     bp.is_reset_call = reset_call ? 1 : 0;
     bp.incremental = env->incremental;
     bp.seed = env->seed;
     bp.env_id_base = env->env_id_base;
-    hipLaunchKernelGGL(k_beam, dim3((N + 3) / 4), dim3(256), 0, stream, bp);
-    RT_LAUNCH_CHECK("k_beam");
+    return bp;
+}
+
+FinishParams finish_params(const rt_env* env, float* obs, float* reward, uint8_t* term, float* info) {
+    FinishParams fp{};
+    fp.G = env->G;
+    fp.C = env->C;
+    fp.st = env->st;
+    fp.lib = env->lib;
+    fp.obs = obs;
+    fp.reward = reward;
+    fp.terminated = term;
+    fp.info = info;
+    fp.part_cnt = env->part_cnt;
+    fp.part_sum = env->part_sum;
+    fp.slices = env->slices;
+    fp.max_tvox = env->max_tvox;
+    fp.N = env->N;
+    fp.vision = env->visionless ? 0 : 1;
+    fp.incremental = env->incremental;
+    fp.hash_mask = env->view_hash_mask;
+    fp.wave_lds = env->finish_wave_lds;
+    fp.wpb = env->finish_wpb;
+    return fp;
+}
+
+void allow_lds(const void* kernel, size_t bytes) {
+    if (bytes > 64 * 1024)
+        (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+// k_dense / k_dense_vis (skipped in incremental mode) then k_finish
+int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, float* info, hipStream_t stream,
+                        hipEvent_t* ev) {
+    const int N = env->N;
     DenseParams dp{};
     dp.G = env->G;
     dp.lung_thr = env->C.lung_thr;
@@ -1568,35 +1761,32 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
         RT_LAUNCH_CHECK("k_dense_vis");
     }
     if (ev) (void)hipEventRecord(ev[2], stream);
-    FinishParams fp{};
-    fp.G = env->G;
-    fp.C = env->C;
-    fp.st = env->st;
-    fp.lib = env->lib;
-    fp.obs = obs;
-    fp.reward = reward;
-    fp.terminated = term;
-    fp.info = info;
-    fp.part_cnt = env->part_cnt;
-    fp.part_sum = env->part_sum;
-    fp.slices = env->slices;
-    fp.max_tvox = env->max_tvox;
-    fp.N = N;
-    fp.vision = env->visionless ? 0 : 1;
-    fp.incremental = env->incremental;
-    fp.hash_mask = env->view_hash_mask;
-    fp.wave_lds = env->finish_wave_lds;
-    fp.wpb = env->finish_wpb;
+    FinishParams fp = finish_params(env, obs, reward, term, info);
     static bool big_lds = false;
-    if (!big_lds && env->finish_smem > 64 * 1024) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_finish),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (!big_lds) {
+        allow_lds(reinterpret_cast<const void*>(&k_finish), env->finish_smem);
         big_lds = true;
     }
     hipLaunchKernelGGL(k_finish, dim3((N + fp.wpb - 1) / fp.wpb), dim3(64 * fp.wpb), env->finish_smem, stream, fp);
     RT_LAUNCH_CHECK("k_finish");
     if (ev) (void)hipEventRecord(ev[3], stream);
     return RT_OK;
+}
+
+hipEvent_t* next_timing_slot(rt_env* env) {
+    if (env->timing_cap > 0 && env->timing_n < env->timing_cap) return &env->tev[(size_t)4 * env->timing_n++];
+    return nullptr;
+}
+
+static int launch_step(rt_env* env, bool reset_call, const float* actions, const uint8_t* mask,
+                       const int32_t* ids, float* obs, float* reward, uint8_t* term, float* info,
+                       hipStream_t stream) {
+    hipEvent_t* ev = next_timing_slot(env);
+    if (ev) (void)hipEventRecord(ev[0], stream);
+    BeamParams bp = beam_params(env, reset_call, actions, mask, ids);
+    hipLaunchKernelGGL(k_beam, dim3((env->N + 3) / 4), dim3(256), 0, stream, bp);
+    RT_LAUNCH_CHECK("k_beam");
+    return launch_dense_finish(env, obs, reward, term, info, stream, ev);
 }
 
 int rt_env_reset(rt_env* env, const uint8_t* mask_d, const int32_t* tumour_ids_d, float* obs_d,
@@ -1611,6 +1801,57 @@ int rt_env_step(rt_env* env, const float* actions_d, float* obs_d, float* reward
     if (!env || !actions_d || !obs_d || !reward_d || !terminated_d) return fail(RT_EINVAL, "NULL argument");
     return launch_step(env, false, actions_d, nullptr, nullptr, obs_d, reward_d, terminated_d, info_d,
                        as_stream(stream));
+}
+
+int rt_env_step_policy(rt_env* env, const rt_policy_step* ps, float* obs_d, float* reward_d,
+                       uint8_t* terminated_d, float* info_d, void* stream) {
+    if (!env || !ps || !ps->params || !ps->obs_in || !ps->obs_store || !ps->done_store || !ps->act_store ||
+        !ps->logp_store || !ps->value_store || !obs_d || !reward_d || !terminated_d)
+        return fail(RT_EINVAL, "NULL argument");
+    if (!env->visionless) return fail(RT_EINVAL, "rt_env_step_policy: the fused policy is the visionless MLP");
+    if (ps->n_params != rtpol::kTensors) return fail(RT_EINVAL, "rt_env_step_policy: expected 13 parameter tensors");
+    PolicyStepParams Q{};
+    for (int i = 0; i < rtpol::kTensors; ++i) {
+        if (!ps->params[i]) return fail(RT_EINVAL, "rt_env_step_policy: NULL parameter");
+        Q.w.p[i] = ps->params[i];
+    }
+    Q.obs_in = ps->obs_in;
+    Q.done_in = ps->done_in;
+    Q.obs_store = ps->obs_store;
+    Q.done_store = ps->done_store;
+    Q.act_store = ps->act_store;
+    Q.logp_store = ps->logp_store;
+    Q.value_store = ps->value_store;
+    Q.seed = ps->seed;
+    Q.counter = ps->counter;
+    Q.id_base = ps->env_id_base;
+    Q.wpb = env->fused_wpb;
+    hipStream_t s = as_stream(stream);
+    hipEvent_t* ev = next_timing_slot(env);
+    if (ev) (void)hipEventRecord(ev[0], s);
+    BeamParams bp = beam_params(env, false, Q.act_store, nullptr, nullptr);
+    FinishParams fp = finish_params(env, obs_d, reward_d, terminated_d, info_d);
+    const dim3 grid((env->N + Q.wpb - 1) / Q.wpb), block(64 * Q.wpb);
+    if (env->incremental) {
+        static bool big = false;
+        if (!big) {
+            allow_lds(reinterpret_cast<const void*>(&k_step_policy<true>), env->fused_smem);
+            big = true;
+        }
+        hipLaunchKernelGGL(k_step_policy<true>, grid, block, env->fused_smem, s, bp, fp, Q);
+        RT_LAUNCH_CHECK("k_step_policy");
+        if (ev)
+            for (int k = 1; k < 4; ++k) (void)hipEventRecord(ev[k], s);
+        return RT_OK;
+    }
+    static bool big = false;
+    if (!big) {
+        allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), env->fused_smem);
+        big = true;
+    }
+    hipLaunchKernelGGL(k_step_policy<false>, grid, block, env->fused_smem, s, bp, fp, Q);
+    RT_LAUNCH_CHECK("k_step_policy");
+    return launch_dense_finish(env, obs_d, reward_d, terminated_d, info_d, s, ev);
 }
 
 int rt_env_kernel_timing(rt_env* env, int32_t capacity) {

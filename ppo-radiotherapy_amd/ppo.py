@@ -17,6 +17,7 @@ device-resident env:
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import time
 from dataclasses import dataclass
@@ -136,6 +137,11 @@ class PPOTrainer:
         # MLP agent on the HIP env; otherwise the torch path below
         self.fused_policy = (bool(getattr(cfg, "fused_policy", True)) and self.device.type == "cuda"
                              and self._fusable(agent, env))
+        # the policy fused into the env step (rt_env_step_policy): one launch per
+        # step in incremental mode; same bits as rt_policy_sample + rt_env_step
+        self.fused_env_step = (self.fused_policy and bool(getattr(cfg, "fused_env_step", True))
+                               and getattr(env, "visionless", False))
+        self._step_structs = None
         self._policy_counter = 0
         self._policy_seed = int(getattr(cfg, "seed", 0)) * 1_000_003 + 7919 * rank + 1
         self._done_valid = False
@@ -195,6 +201,26 @@ class PPOTrainer:
         obs/done/action/logprob/value of this step into the storage, then the
         env steps on storage actions[step] and writes rewards[step]/infos[step]."""
         env = self.env
+        if self.fused_env_step and getattr(env, "visionless", False):
+            if self._step_structs is None:
+                self._step_structs = [_lib.RtPolicyStep(
+                    params=ctypes.cast(self._policy_ptrs, ctypes.POINTER(ctypes.c_void_p)), n_params=13,
+                    obs_store=self.obs[t].data_ptr(), done_store=self.dones[t].data_ptr(),
+                    act_store=self.actions[t].data_ptr(), logp_store=self.logprobs[t].data_ptr(),
+                    value_store=self.values[t].data_ptr(), seed=self._policy_seed, env_id_base=self.rank * self.N)
+                    for t in range(self.T)]
+            st = self._step_structs[step]
+            st.obs_in = env.obs.data_ptr()
+            st.done_in = env.terminated.data_ptr() if self._done_valid else None
+            st.counter = self._policy_counter
+            self._policy_counter += 1
+            if env_events is not None:
+                env_events[0].record()
+            env.step_policy(st, info_out=self.infos[step], reward_out=self.rewards[step])
+            if env_events is not None:
+                env_events[1].record()
+            self._done_valid = True
+            return
         L = _lib.load()
         stream = _lib.stream_handle()
         _lib.check(L.rt_policy_sample(self._policy_ptrs, 13, self.N, env.obs.data_ptr(),

@@ -19,6 +19,7 @@ equivalent of `"episode" in infos` (train.py:160).
 """
 from __future__ import annotations
 
+import ctypes
 import time
 
 import numpy as np
@@ -128,6 +129,21 @@ class RadiotherapyVecEnv:
         _lib.check(self._L.rt_env_step(self._h, _lib.ptr(a), _lib.ptr(self.obs), _lib.ptr(rew),
                                        _lib.ptr(self.terminated), _lib.ptr(info), _lib.stream_handle()),
                    "rt_env_step")
+        return self.obs, rew, self.terminated.view(torch.bool), self.truncated, LazyInfos(self._infos, info)
+
+    def step_policy(self, step, info_out: torch.Tensor | None = None, reward_out: torch.Tensor | None = None):
+        """Fused rollout step (rt_env_step_policy): the visionless MLP policy
+        samples the actions described by `step` (an _lib.RtPolicyStep whose
+        pointers name the policy parameters, the observation acted on and the
+        rollout-storage slices) and the env steps on them, in one launch per
+        step in incremental mode.  Outputs as `step`."""
+        if not self.visionless:
+            raise ValueError("step_policy: the fused policy is the visionless agent")
+        info = self.info if info_out is None else info_out
+        rew = self.reward if reward_out is None else reward_out
+        _lib.check(self._L.rt_env_step_policy(self._h, ctypes.byref(step), _lib.ptr(self.obs), _lib.ptr(rew),
+                                              _lib.ptr(self.terminated), _lib.ptr(info), _lib.stream_handle()),
+                   "rt_env_step_policy")
         return self.obs, rew, self.terminated.view(torch.bool), self.truncated, LazyInfos(self._infos, info)
 
     def set_next_tumours(self, ids):
