@@ -16,6 +16,7 @@
  *   GAE loop                  train.py:163-181  | rt_gae
  *   agent.get_action_and_value train.py:143-149 | rt_policy_sample (visionless agent)
  *   rollout step (policy + env) train.py:143-158 | rt_env_step_policy (fused)
+ *   rollout loop              train.py:138-161  | rt_env_rollout_policy (persistent)
  *   PPO minibatch step        train.py:197-246  | rt_ppo_grad + rt_adam_step / rt_ppo_update
  *   FeaturesExtractor3D.cnn   networks.py:8-45  | rt_conv_relu_pool_fwd (+ backward kernels)
  *
@@ -212,6 +213,29 @@ typedef struct rt_policy_step {
 
 int rt_env_step_policy(rt_env* env, const rt_policy_step* step, float* obs_d, float* reward_d,
                        uint8_t* terminated_d, float* info_d, void* stream);
+
+/* n_steps consecutive rollout steps (train.py:138-161) in ONE persistent
+ * launch, incremental step mode only: each env's wave runs its policy sample,
+ * env step and finish n_steps times back to back, with no grid-wide
+ * synchronisation between steps (envs are independent).  Step s (0-based)
+ * writes the storage slices step.X_store + s * (row floats * N) -- i.e.
+ * step.X_store is row `first` of contiguous [T][N][...] storage -- plus
+ * reward_store[s * N + e] and info_store[(s * N + e) * RT_INFO_W] (info_store
+ * may be NULL), with Philox counter step.counter + s.  Step 0 acts on
+ * step.obs_in / step.done_in; later steps on the env's own outputs, which
+ * are left in obs_d / terminated_d after the last step.  Same bits as
+ * n_steps calls of rt_env_step_policy.  RT_EINVAL in dense step mode;
+ * RT_ELIMIT if the kernel's LDS layout cannot be built (callers then step
+ * with rt_env_step_policy; not reached for the visionless MLP). */
+typedef struct rt_policy_rollout {
+    rt_policy_step step;          /* storage row of the first step, its counter */
+    int32_t n_steps;
+    float* reward_store;          /* [n_steps][N] */
+    float* info_store;            /* [n_steps][N][RT_INFO_W] or NULL */
+} rt_policy_rollout;
+
+int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* obs_d, uint8_t* terminated_d,
+                          void* stream);
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */

@@ -23,6 +23,7 @@ INFO_NAMES = {
 INFO_W = 20
 STEP_DENSE, STEP_INCREMENTAL = 0, 1
 
+RT_ELIMIT = -5
 RT_ERRORS = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EDEVICE", -4: "RT_ELAUNCH", -5: "RT_ELIMIT"}
 
 # every symbol include/rtenv.h declares (checked by tests/test_abi.py)
@@ -32,7 +33,7 @@ EXPORTS = [
     "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
-    "rt_env_step_policy",
+    "rt_env_step_policy", "rt_env_rollout_policy",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
     "rt_ppo_shuffle", "rt_ppo_adv_stats",
     "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
@@ -96,6 +97,11 @@ class RtPolicyStep(ctypes.Structure):
         ("seed", ctypes.c_uint64), ("counter", ctypes.c_uint64), ("env_id_base", ctypes.c_int64)]
 
 
+class RtPolicyRollout(ctypes.Structure):
+    _fields_ = [("step", RtPolicyStep), ("n_steps", ctypes.c_int32), ("reward_store", ctypes.c_void_p),
+                ("info_store", ctypes.c_void_p)]
+
+
 class RtConvLayer(ctypes.Structure):
     _fields_ = [("cin", ctypes.c_int32), ("groups", ctypes.c_int32), ("in_dims", ctypes.c_int32 * 3),
                 ("pool_pad", ctypes.c_int32 * 3)]
@@ -145,6 +151,7 @@ def load(build_if_missing: bool = True):
         "rt_policy_sample": ([ctypes.POINTER(vp), i32, i32, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint64,
                               ctypes.c_uint64, i64, vp], ctypes.c_int),
         "rt_env_step_policy": ([vp, ctypes.POINTER(RtPolicyStep), vp, vp, vp, vp, vp], ctypes.c_int),
+        "rt_env_rollout_policy": ([vp, ctypes.POINTER(RtPolicyRollout), vp, vp, vp], ctypes.c_int),
         "rt_ppo_workspace_floats": ([i32], i64),
         "rt_ppo_num_params": ([], i32),
         "rt_ppo_grad": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, vp,

@@ -20,11 +20,18 @@ OUT = os.path.join(PKG, "librtenv.so")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 
 HIPCC_FLAGS = [
-    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
     # every f32/f64 operation must round where the reference rounds
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-Wall", "-Wno-unused-function",
 ]
+# per-source extra flags.  rtenv.hip: machine LICM hoists the f64 series
+# constants of the pose update out of k_rollout_policy's step loop and spills
+# them to scratch (reloaded serially inside the sincos chain); without it the
+# kernel fits 128 VGPRs with no spill, and the other kernels' loops are unchanged
+# (register renaming only).
+EXTRA_FLAGS = {SRC: ["-mllvm", "-disable-machine-licm"]}
+OBJ_DIR = os.path.join(PKG, "_obj")
 
 
 def hipcc() -> str:
@@ -38,14 +45,28 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = (*SRCS, HDR, os.path.join(PKG, "csrc", "rt_ddmath.h"), os.path.join(PKG, "csrc", "rt_trace.h"), __file__)
+    deps = (*SRCS, HDR, *(os.path.join(PKG, "csrc", h) for h in ("rt_ddmath.h", "rt_trace.h", "policy_core.h")),
+            __file__)
     return any(os.path.getmtime(p) > t for p in deps)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return OUT
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), *SRCS, "-o", OUT + ".tmp"]
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    procs, objs = [], []
+    for src in SRCS:
+        obj = os.path.join(OBJ_DIR, os.path.splitext(os.path.basename(src))[0] + ".o")
+        cmd = [hipcc(), *HIPCC_FLAGS, *EXTRA_FLAGS.get(src, []), "-I", os.path.join(REPO, "include"), "-c", src,
+               "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((subprocess.Popen(cmd), cmd))
+        objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

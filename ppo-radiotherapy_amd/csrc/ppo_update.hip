@@ -986,15 +986,31 @@ __global__ __launch_bounds__(256) void k_shuffle(int64_t n, int h, uint64_t key,
 }
 
 // [n_mb][2] = (mean, unbiased std) of adv over each minibatch of perm
-// (train.py:215-218), sums in f64
-__global__ __launch_bounds__(256) void k_adv_stats(const float* adv, const int64_t* perm, int mb, float* stats) {
-    __shared__ double ps[4], pq[4];
+// (train.py:215-218), sums in f64.  One 1024-thread block per minibatch; each
+// thread issues its 16 index loads, then its 16 gathers, before accumulating,
+// so a block has 16K independent loads in flight (the gathers hit a ~1 MB
+// array that lives in L2).
+constexpr int kAdvThreads = 1024, kAdvBatch = 16;
+__global__ __launch_bounds__(kAdvThreads) void k_adv_stats(const float* adv, const int64_t* perm, int mb,
+                                                          float* stats) {
+    __shared__ double ps[kAdvThreads / 64], pq[kAdvThreads / 64];
     const int64_t base = (int64_t)blockIdx.x * mb;
     double s = 0.0, q = 0.0;
-    for (int j = threadIdx.x; j < mb; j += 256) {
-        const double a = adv[perm[base + j]];
-        s += a;
-        q += a * a;
+    for (int j0 = 0; j0 < mb; j0 += kAdvThreads * kAdvBatch) {
+        int64_t ix[kAdvBatch];
+        float a[kAdvBatch];
+#pragma unroll
+        for (int u = 0; u < kAdvBatch; ++u) {
+            const int j = j0 + u * kAdvThreads + (int)threadIdx.x;
+            ix[u] = j < mb ? perm[base + j] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kAdvBatch; ++u) a[u] = ix[u] >= 0 ? adv[ix[u]] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < kAdvBatch; ++u) {
+            s += (double)a[u];
+            q += (double)a[u] * (double)a[u];
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -1007,7 +1023,11 @@ __global__ __launch_bounds__(256) void k_adv_stats(const float* adv, const int64
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const double S = (ps[0] + ps[1]) + (ps[2] + ps[3]), Q = (pq[0] + pq[1]) + (pq[2] + pq[3]);
+        double S = 0.0, Q = 0.0;
+        for (int w = 0; w < kAdvThreads / 64; ++w) {
+            S += ps[w];
+            Q += pq[w];
+        }
         const double mean = S / mb;
         const double var = mb > 1 ? (Q - S * mean) / (mb - 1) : 0.0;
         stats[2 * blockIdx.x] = (float)mean;
@@ -1182,7 +1202,7 @@ extern "C" int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32
                                 float* stats_d, void* stream) {
     if (!adv_d || !perm_d || mb_size < 1 || n_minibatches < 1 || !stats_d)
         return rt_internal_fail(RT_EINVAL, "rt_ppo_adv_stats: bad argument");
-    hipLaunchKernelGGL(k_adv_stats, dim3(n_minibatches), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), adv_d,
+    hipLaunchKernelGGL(k_adv_stats, dim3(n_minibatches), dim3(kAdvThreads), 0, reinterpret_cast<hipStream_t>(stream), adv_d,
                        perm_d, mb_size, stats_d);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));

@@ -835,7 +835,9 @@ struct FinishParams {
     const int32_t* part_cnt;
     const double* part_sum;
     int32_t slices;
-    int32_t max_tvox;    // per-wave LDS holds 2 * max_tvox floats
+    int32_t max_tvox;    // per-wave LDS holds the sum plan of tumours up to max_tvox voxels
+    float* gscratch;     // larger tumours (k_rollout_policy's smaller LDS share): plan slots
+    int64_t gscratch_stride;  //   here, gscratch + e * stride, operands read from the library
     int32_t N;
     int32_t vision;      // obs is f32 [N][4][V]
     int32_t incremental; // lung count / sum from the k_beam-maintained counters
@@ -938,6 +940,25 @@ __device__ void vision_scatter(const FinishParams& P, int e, int lane, const dou
 //  - combine k_dense slices; rewards (environment.py:164-191), termination,
 //    obs (environment.py:259-268), info, episode statistics
 // ---------------------------------------------------------------------------
+// Executes a tumour's exact-order sum plan over the slots `tv` (leaves
+// 0..n-1 filled; op o writes slot n+o) level by level; returns the final sum
+// (0 for an empty tumour).  Every lane returns it.
+__device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const int32_t* lev, int nt, int nlev,
+                                          int result, int lane) {
+    int lo = 0;
+    for (int l = 0; l < nlev; ++l) {
+        lds_wave_sync();
+        const int hi = lev[l];
+        for (int o = lo + lane; o < hi; o += 64) {
+            const uint32_t ab = ops[o];
+            tv[nt + o] = tv[ab & 0xffffu] + tv[ab >> 16];
+        }
+        lo = hi;
+    }
+    lds_wave_sync();
+    return result >= 0 ? tv[result] : 0.0f;
+}
+
 __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char* wave_lds) {
     float* tvals = reinterpret_cast<float*>(wave_lds);
     if (lane == 0) RT_STAMP(e, 5);
@@ -963,11 +984,15 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     const uint32_t* tc = P.lib.coord + m.vox_base;
     const double px = pose[0], py = pose[1], pz = pose[2];
     const int W = P.G.g[2], H = P.G.g[1], HW = H * W;
+    // plan slots (leaves 0..n-1, op o -> n+o): the wave's LDS, or for a
+    // tumour above the LDS capacity a global scratch row (L2)
+    const bool in_lds = nt <= P.max_tvox;
+    float* tg = in_lds ? nullptr : P.gscratch + (size_t)e * P.gscratch_stride;
     // the sum plan's operands and level ends -> LDS by async copies (no VGPRs),
     // in flight during the gather; the plan below then touches only LDS
     uint32_t* ops_s = reinterpret_cast<uint32_t*>(tvals + 2 * P.max_tvox);
     int32_t* lev_s = reinterpret_cast<int32_t*>(ops_s + P.max_tvox);
-    {
+    if (in_lds) {
         const uint32_t* ops = P.lib.ops + m.op_base;
         const int32_t* lend = P.lib.lvl_end + m.lvl_base;
         const int nops = nt - 1;  // a binary sum tree over nt leaves (checked at create)
@@ -984,7 +1009,8 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
         const int v = tv[i];
         const uint32_t c = tc[i];
         const float x = dose[v];
-        tvals[i] = x;
+        if (in_lds) tvals[i] = x;
+        else tg[i] = x;
         const bool lung = (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u;
         ctum += (lung && x > P.C.lung_thr) ? 1 : 0;
         const int ix = (int)(c >> 20), iy = (int)((c >> 10) & 1023u), iz = (int)(c & 1023u);
@@ -1006,20 +1032,13 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
         }
     }
     if (lane == 0) RT_STAMP(e, 6);
-    // exact np.sum(dose * tumours): level plan (slots: leaves 0..n-1, op o -> n+o)
-    {
+    // exact np.sum(dose * tumours): level plan
+    float S;
+    if (in_lds) {
         __builtin_amdgcn_s_waitcnt(0);  // the async copies above have landed
-        int lo = 0;
-        for (int l = 0; l < m.nlev; ++l) {
-            lds_wave_sync();
-            const int hi = lev_s[l];
-            for (int o = lo + lane; o < hi; o += 64) {
-                const uint32_t ab = ops_s[o];
-                tvals[nt + o] = tvals[ab & 0xffffu] + tvals[ab >> 16];
-            }
-            lo = hi;
-        }
-        lds_wave_sync();
+        S = run_plan(tvals, ops_s, lev_s, nt, m.nlev, m.result, lane);
+    } else {
+        S = run_plan(tg, P.lib.ops + m.op_base, P.lib.lvl_end + m.lvl_base, nt, m.nlev, m.result, lane);
     }
     if (lane == 0) RT_STAMP(e, 7);
     int cnt = 0;
@@ -1037,7 +1056,6 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     }
     if (lane == 0) {
         const long long c = (long long)cnt - ctum;  // lungs * (1 - tumours)
-        const float S = m.result >= 0 ? tvals[m.result] : 0.0f;
         const float ratio = S / m.T;
         const float r_tum = ratio * P.C.tum_reward;
         const double r_lung = (double)c / m.lung_total * P.C.lung_reward;
@@ -1158,6 +1176,114 @@ __global__ __launch_bounds__(1024) void k_step_policy(BeamParams B, FinishParams
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         finish_env(F, e, lane, psm + (size_t)w * F.wave_lds);
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_rollout_policy: n_steps rollout steps of the visionless agent in ONE
+// persistent launch (incremental step mode).  Envs never interact, so a wave
+// can run its env's whole step chain -- policy sample, pose update, march,
+// finish -- n_steps times back to back without any grid- or block-wide
+// synchronisation after the one-time parameter staging: the waves of a CU
+// drift into different phases (f64 pose ALU, random-line dose RMW, LDS sum
+// plan) and hide each other's latency, and the per-launch costs of the
+// stepwise path (launch, parameter staging, the tail of the slowest env) are
+// paid once per rollout.  LDS: the parameters (once per block) and one region
+// per wave, 16 waves per block so a CU holds 16 envs: the wave's h1 during
+// its policy, its finish scratch after it.  A tumour whose sum plan exceeds
+// the region keeps its plan slots in a global scratch row.  The step body is
+// k_step_policy<true>'s, so the bits are the same.
+// ---------------------------------------------------------------------------
+struct RolloutParams {
+    PolicyStepParams q;  // storage rows of the first step, its Philox counter
+    float* reward_store; // [n][N]
+    float* info_store;   // [n][N][RT_INFO_W] or null
+    int32_t n_steps;
+    int32_t fin_off;     // byte offset of the finish scratch in dynamic LDS
+};
+
+struct RolloutArgs {
+    BeamParams B;
+    FinishParams F;
+    RolloutParams R;
+};
+
+__global__ __launch_bounds__(1024) void k_rollout_policy(RolloutArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+    rtpol::Lds& L = *reinterpret_cast<rtpol::Lds*>(rsm);
+    const int tid = threadIdx.x, lane0 = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int e0 = blockIdx.x * A.R.q.wpb + w;
+    rtpol::stage(L, A.R.q.w, tid, (int)blockDim.x);
+    __syncthreads();
+    if (e0 >= A.B.N) return;  // wave-uniform; no block barrier follows
+    // the wave's region: h1 during the policy, the finish scratch after it
+    unsigned char* const fin_0 = rsm + A.R.fin_off + (size_t)w * A.F.wave_lds;
+    float* const h1_0 = reinterpret_cast<float*>(fin_0);
+    const int n_steps = A.R.n_steps;
+    if (lane0 == 0) RT_STAMP(e0, 13);
+    for (int t = 0; t < n_steps; ++t) {
+        // Re-derive the loop-invariant inputs (kernel arguments through a
+        // laundered kernarg pointer, lane, env, LDS bases) every step: hoisted
+        // out of the loop they stay live across the whole step body and push
+        // it past 128 VGPRs into scratch.  Scalar loads from the kernarg
+        // segment are cheap.
+        typedef const __attribute__((address_space(4))) RolloutArgs* KPtr;
+        KPtr ap = (KPtr)(__builtin_amdgcn_kernarg_segment_ptr());
+        asm volatile("" : "+s"(ap));
+        const RolloutArgs& K = *(const RolloutArgs*)ap;
+        const BeamParams& B = K.B;
+        const FinishParams& F = K.F;
+        const RolloutParams& R = K.R;
+        const PolicyStepParams& Q = R.q;
+        int lane = lane0, e = e0;
+        asm volatile("" : "+v"(lane));
+        asm volatile("" : "+s"(e));
+        float* h1 = h1_0;
+        unsigned char* fin = fin_0;
+        asm volatile("" : "+s"(h1));
+        asm volatile("" : "+s"(fin));
+        const size_t N = (size_t)B.N;
+        const float* obs_in = t == 0 ? Q.obs_in : F.obs;
+        const uint8_t* done_in = t == 0 ? Q.done_in : F.terminated;
+        if (lane == 0) {
+            RT_STAMP(e, 0);
+            RT_STAMP(e, 9);
+        }
+        float x[rtpol::NOBS];
+#pragma unroll
+        for (int i = 0; i < rtpol::NOBS; ++i) x[i] = obs_in[(size_t)e * rtpol::NOBS + i];
+        const rtpol::Sample smp =
+            rtpol::policy_env(L, h1, x, lane, Q.seed, Q.counter + (uint64_t)t, (uint64_t)(Q.id_base + e));
+        if (lane == 0) RT_STAMP(e, 1);
+        const size_t r9 = (size_t)t * N * rtpol::NOBS + (size_t)e * rtpol::NOBS;
+        const size_t r6 = (size_t)t * N * rtpol::NACT + (size_t)e * rtpol::NACT;
+        const size_t r1 = (size_t)t * N + (size_t)e;
+        if (lane < rtpol::NOBS) {
+            float xi = x[0];
+#pragma unroll
+            for (int i = 1; i < rtpol::NOBS; ++i) xi = lane == i ? x[i] : xi;
+            Q.obs_store[r9 + lane] = xi;
+        }
+        if (lane == rtpol::NOBS) Q.done_store[r1] = done_in ? (float)done_in[e] : 0.0f;
+        if (lane < rtpol::NACT) Q.act_store[r6 + lane] = smp.action;
+        if (lane == 0) {
+            Q.logp_store[r1] = smp.logp;
+            Q.value_store[r1] = smp.value;
+        }
+        float a6[rtpol::NACT];
+#pragma unroll
+        for (int i = 0; i < rtpol::NACT; ++i) a6[i] = rtpol::lane_f(smp.action, i);
+        beam_env(B, e, lane, a6);
+        // this wave's dose stores are visible to its own lanes' loads below
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        FinishParams Ft = F;
+        Ft.reward = R.reward_store + (size_t)t * N;
+        Ft.info = R.info_store ? R.info_store + (size_t)t * N * RT_INFO_W : nullptr;
+        finish_env(Ft, e, lane, fin);
+        // obs / terminated / dose of this step -> every lane of the next
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane0 == 0) RT_STAMP(e0, 14);
 }
 
 // ---------------------------------------------------------------------------
@@ -1346,6 +1472,12 @@ struct rt_env {
     int finish_wpb = 4;      // k_finish envs per block
     int fused_wpb = 16;      // k_step_policy envs (waves) per block
     size_t fused_smem = 0;   // k_step_policy dynamic LDS
+    int rollout_wpb = 0;     // k_rollout_policy envs per block (0: does not fit LDS)
+    size_t rollout_smem = 0; // k_rollout_policy dynamic LDS
+    int rollout_fin_off = 0; // offset of its per-wave regions
+    int rollout_wave_lds = 0;// bytes per wave region
+    int rollout_cap = 0;     // largest tumour whose sum plan fits a region
+    float* rollout_gscratch = nullptr;  // [N][2 * max_tvox] plan slots of larger tumours
     uint32_t view_hash_mask = 0;
     int32_t* part_cnt = nullptr;
     double* part_sum = nullptr;
@@ -1624,6 +1756,22 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     env->fused_wpb = 16;
     while (env->fused_wpb > 1 && fused_bytes(env->fused_wpb) > 160 * 1024) env->fused_wpb /= 2;
     env->fused_smem = fused_bytes(env->fused_wpb);
+    // k_rollout_policy: the parameters once per block, then 16 per-wave
+    // regions (h1 during the policy, the finish scratch after it); tumours
+    // above the region's plan capacity keep their plan slots in gscratch
+    {
+        const size_t off = (sizeof(rtpol::Lds) + 15) / 16 * 16;
+        const int wpb = 16;
+        const size_t per_wave = (160 * 1024 - off) / wpb / 16 * 16;
+        const int cap = (int)((per_wave - kMaxPlanLevels * sizeof(int32_t)) / (3 * sizeof(float)));
+        if (env->incremental && env->visionless && per_wave >= rtpol::H * sizeof(float) && cap >= 1) {
+            env->rollout_wpb = wpb;
+            env->rollout_fin_off = (int)off;
+            env->rollout_wave_lds = (int)per_wave;
+            env->rollout_cap = std::min(cap, max_n);
+            env->rollout_smem = off + (size_t)wpb * per_wave;
+        }
+    }
 
     // ---- device allocations ----
     const int N = env->N;
@@ -1644,7 +1792,9 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         (rc = dev_alloc(env, &st.next_tumour, N)) || (rc = dev_alloc(env, &st.setup, N)) ||
         (rc = dev_alloc(env, &env->part_cnt, (size_t)N * env->slices)) ||
         (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices)) ||
-        (rc = dev_alloc(env, &st.lung_cnt, N)) || (rc = dev_alloc(env, &st.lung_sum, N))) {
+        (rc = dev_alloc(env, &st.lung_cnt, N)) || (rc = dev_alloc(env, &st.lung_sum, N)) ||
+        (env->rollout_wpb && env->rollout_cap < max_n &&
+         (rc = dev_alloc(env, &env->rollout_gscratch, (size_t)N * 2 * max_n)))) {
         free_env(env);
         return rc;
     }
@@ -1722,6 +1872,8 @@ FinishParams finish_params(const rt_env* env, float* obs, float* reward, uint8_t
     fp.part_sum = env->part_sum;
     fp.slices = env->slices;
     fp.max_tvox = env->max_tvox;
+    fp.gscratch = nullptr;
+    fp.gscratch_stride = 0;
     fp.N = env->N;
     fp.vision = env->visionless ? 0 : 1;
     fp.incremental = env->incremental;
@@ -1852,6 +2004,63 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* ps, float* obs_d, floa
     hipLaunchKernelGGL(k_step_policy<false>, grid, block, env->fused_smem, s, bp, fp, Q);
     RT_LAUNCH_CHECK("k_step_policy");
     return launch_dense_finish(env, obs_d, reward_d, terminated_d, info_d, s, ev);
+}
+
+int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
+                          void* stream) {
+    if (!env || !r || !obs_d || !terminated_d || !r->reward_store) return fail(RT_EINVAL, "NULL argument");
+    const rt_policy_step* ps = &r->step;
+    if (!ps->params || !ps->obs_in || !ps->obs_store || !ps->done_store || !ps->act_store || !ps->logp_store ||
+        !ps->value_store)
+        return fail(RT_EINVAL, "NULL argument");
+    if (!env->visionless || !env->incremental)
+        return fail(RT_EINVAL, "rt_env_rollout_policy: visionless env in incremental step mode only");
+    if (ps->n_params != rtpol::kTensors) return fail(RT_EINVAL, "rt_env_rollout_policy: expected 13 parameter tensors");
+    if (r->n_steps < 1) return fail(RT_EINVAL, "rt_env_rollout_policy: n_steps < 1");
+    if (env->rollout_wpb == 0)
+        return fail(RT_ELIMIT, "rt_env_rollout_policy: policy + finish scratch exceed LDS (largest tumour too big)");
+    RolloutParams R{};
+    PolicyStepParams& Q = R.q;
+    for (int i = 0; i < rtpol::kTensors; ++i) {
+        if (!ps->params[i]) return fail(RT_EINVAL, "rt_env_rollout_policy: NULL parameter");
+        Q.w.p[i] = ps->params[i];
+    }
+    Q.obs_in = ps->obs_in;
+    Q.done_in = ps->done_in;
+    Q.obs_store = ps->obs_store;
+    Q.done_store = ps->done_store;
+    Q.act_store = ps->act_store;
+    Q.logp_store = ps->logp_store;
+    Q.value_store = ps->value_store;
+    Q.seed = ps->seed;
+    Q.counter = ps->counter;
+    Q.id_base = ps->env_id_base;
+    Q.wpb = env->rollout_wpb;
+    R.reward_store = r->reward_store;
+    R.info_store = r->info_store;
+    R.n_steps = r->n_steps;
+    R.fin_off = env->rollout_fin_off;
+    hipStream_t s = as_stream(stream);
+    hipEvent_t* ev = next_timing_slot(env);
+    if (ev) (void)hipEventRecord(ev[0], s);
+    BeamParams bp = beam_params(env, false, nullptr, nullptr, nullptr);
+    FinishParams fp = finish_params(env, obs_d, nullptr, terminated_d, nullptr);
+    fp.max_tvox = env->rollout_cap;
+    fp.wave_lds = env->rollout_wave_lds;
+    fp.gscratch = env->rollout_gscratch;
+    fp.gscratch_stride = 2 * (int64_t)env->max_tvox;
+    static bool big = false;
+    if (!big) {
+        allow_lds(reinterpret_cast<const void*>(&k_rollout_policy), env->rollout_smem);
+        big = true;
+    }
+    const dim3 grid((env->N + Q.wpb - 1) / Q.wpb), block(64 * Q.wpb);
+    RolloutArgs A{bp, fp, R};
+    hipLaunchKernelGGL(k_rollout_policy, grid, block, env->rollout_smem, s, A);
+    RT_LAUNCH_CHECK("k_rollout_policy");
+    if (ev)
+        for (int k = 1; k < 4; ++k) (void)hipEventRecord(ev[k], s);
+    return RT_OK;
 }
 
 int rt_env_kernel_timing(rt_env* env, int32_t capacity) {

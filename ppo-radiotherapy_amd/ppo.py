@@ -142,6 +142,10 @@ class PPOTrainer:
         self.fused_env_step = (self.fused_policy and bool(getattr(cfg, "fused_env_step", True))
                                and getattr(env, "visionless", False))
         self._step_structs = None
+        # ... and the whole rollout as ONE persistent launch (rt_env_rollout_policy)
+        # whenever the env runs the incremental step mode: same bits as the
+        # stepwise launches
+        self.fused_rollout = self.fused_env_step and bool(getattr(cfg, "fused_rollout", True))
         self._policy_counter = 0
         self._policy_seed = int(getattr(cfg, "seed", 0)) * 1_000_003 + 7919 * rank + 1
         self._done_valid = False
@@ -264,9 +268,46 @@ class PPOTrainer:
     @torch.no_grad()
     def rollout(self):
         """train.py:138-161 for all envs of this rank; no host synchronisation."""
-        for step in range(self.T):
-            self.rollout_step(step)
+        self.rollout_steps(0, self.T)
         self.global_step += self.N * self.T * self.world
+
+    @torch.no_grad()
+    def rollout_steps(self, first: int, count: int):
+        """Rollout steps first .. first+count-1 (storage rows): one persistent
+        launch when the env supports it (rt_env_rollout_policy), otherwise
+        step by step."""
+        if not (self.fused_rollout and getattr(self.env, "step_mode", "dense") == "incremental"
+                and getattr(self.env, "visionless", False)):
+            for step in range(first, first + count):
+                self.rollout_step(step)
+            return
+        if self.env.rollout_policy(self._rollout_struct(first, count)) == _lib.RT_ELIMIT:
+            self.fused_rollout = False  # library too large for the persistent kernel's LDS
+            return self.rollout_steps(first, count)
+        self._policy_counter += count
+        self._done_valid = True
+
+    def _rollout_struct(self, first: int, count: int):
+        """rt_policy_rollout for storage rows first .. first+count-1."""
+        env = self.env
+        ro = _lib.RtPolicyRollout()
+        st = ro.step
+        st.params = ctypes.cast(self._policy_ptrs, ctypes.POINTER(ctypes.c_void_p))
+        st.n_params = 13
+        st.obs_in = env.obs.data_ptr()
+        st.done_in = env.terminated.data_ptr() if self._done_valid else None
+        st.obs_store = self.obs[first].data_ptr()
+        st.done_store = self.dones[first].data_ptr()
+        st.act_store = self.actions[first].data_ptr()
+        st.logp_store = self.logprobs[first].data_ptr()
+        st.value_store = self.values[first].data_ptr()
+        st.seed = self._policy_seed
+        st.counter = self._policy_counter
+        st.env_id_base = self.rank * self.N
+        ro.n_steps = count
+        ro.reward_store = self.rewards[first].data_ptr()
+        ro.info_store = self.infos[first].data_ptr()
+        return ro
 
     def _sync_next(self):
         """Fused rollout keeps next_obs/next_done in the env's buffers."""

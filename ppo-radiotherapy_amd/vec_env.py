@@ -146,6 +146,18 @@ class RadiotherapyVecEnv:
                    "rt_env_step_policy")
         return self.obs, rew, self.terminated.view(torch.bool), self.truncated, LazyInfos(self._infos, info)
 
+    def rollout_policy(self, rollout) -> int:
+        """`rollout.n_steps` fused rollout steps in one persistent launch
+        (rt_env_rollout_policy; incremental step mode).  `rollout` is an
+        _lib.RtPolicyRollout naming the storage rows of its first step.
+        Returns the library's status (RT_ELIMIT: the tumour library is too
+        large for the kernel's LDS budget -- step with step_policy instead)."""
+        rc = self._L.rt_env_rollout_policy(self._h, ctypes.byref(rollout), _lib.ptr(self.obs),
+                                           _lib.ptr(self.terminated), _lib.stream_handle())
+        if rc not in (0, _lib.RT_ELIMIT):
+            _lib.check(rc, "rt_env_rollout_policy")
+        return rc
+
     def set_next_tumours(self, ids):
         t = torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
         _lib.check(self._L.rt_env_set_next_tumours(self._h, _lib.ptr(t), _lib.stream_handle()),

@@ -42,19 +42,24 @@ def test_library_has_gfx950_code_object():
     assert b"amdgcn-amd-amdhsa--gfx942" not in data
 
 
-def test_config_struct_layout_matches_header(tmp_path):
-    fields = [f[0] for f in _lib.RtEnvConfig._fields_]
+@pytest.mark.parametrize("cname,pyname", [("rt_env_config", "RtEnvConfig"), ("rt_policy_step", "RtPolicyStep"),
+                                           ("rt_policy_rollout", "RtPolicyRollout"), ("rt_ppo_batch", "RtPpoBatch"),
+                                           ("rt_ppo_hparams", "RtPpoHparams"), ("rt_conv_layer", "RtConvLayer")])
+def test_struct_layout_matches_header(tmp_path, cname, pyname):
+    """Every ctypes mirror of a header struct has its size and field offsets."""
+    cls = getattr(_lib, pyname)
+    fields = [f[0] for f in cls._fields_]
     probe = tmp_path / "probe.c"
-    body = "\n".join(f'    printf("{f} %zu\\n", offsetof(rt_env_config, {f}));' for f in fields)
+    body = "\n".join(f'    printf("{f} %zu\\n", offsetof({cname}, {f}));' for f in fields)
     probe.write_text(f'#include <stddef.h>\n#include <stdio.h>\n#include "rtenv.h"\nint main(void) {{\n'
-                     f'    printf("sizeof %zu\\n", sizeof(rt_env_config));\n{body}\n    return 0;\n}}\n')
+                     f'    printf("sizeof %zu\\n", sizeof({cname}));\n{body}\n    return 0;\n}}\n')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(probe), "-o", str(exe)], check=True)
     got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                        check=True).stdout.splitlines())
-    assert int(got["sizeof"]) == ctypes.sizeof(_lib.RtEnvConfig)
+    assert int(got["sizeof"]) == ctypes.sizeof(cls)
     for f in fields:
-        assert int(got[f]) == getattr(_lib.RtEnvConfig, f).offset, f
+        assert int(got[f]) == getattr(cls, f).offset, f
 
 
 def test_config_defaults_are_reference_constants():

@@ -24,6 +24,7 @@ SLOTS, CAP = 16, 8192
 PHASES = {  # name: (start slot, end slot)
     "policy": (0, 1), "policy.stage": (0, 9), "policy.mlp+sample": (9, 1), "beam.pose": (2, 3), "pose.loads": (2, 10), "pose.update": (10, 11), "pose.setup": (11, 3), "pose->march": (3, 12), "beam.march": (12, 4), "finish.gather": (5, 6),
     "finish.plan": (6, 7), "finish.tail": (7, 8), "policy->beam": (1, 2), "beam->finish": (4, 5),
+    "step": (0, 8),
 }
 
 
@@ -31,7 +32,8 @@ def build():
     sys.path.insert(0, os.path.join(REPO, "ppo-radiotherapy_amd"))
     import build as b
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [b.hipcc(), *b.HIPCC_FLAGS, "-DRT_TRACE", "-I", os.path.join(REPO, "include"), *b.SRCS, "-o", OUT]
+    cmd = [b.hipcc(), *b.HIPCC_FLAGS, "-shared", *b.EXTRA_FLAGS[b.SRC], "-DRT_TRACE", "-I", os.path.join(REPO, "include"),
+           *b.SRCS, "-o", OUT]
     subprocess.run(cmd, check=True)
 
 
@@ -42,6 +44,8 @@ def main():
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--two-call", action="store_true", help="rt_policy_sample + rt_env_step instead of the fused step")
+    ap.add_argument("--persistent", action="store_true",
+                    help="the steps as one persistent k_rollout_policy launch (incremental); stamps of the last step")
     a = ap.parse_args()
     if a.build_only or not os.path.exists(OUT):
         build()
@@ -62,8 +66,13 @@ def main():
     lib = assets.synthetic_library((64,) * 3, 1000, 0)
     cfg.fused_env_step = not a.two_call
     tr = ps.make(a.envs, 0, lib, dev, cfg, a.mode)
-    for i in range(a.steps):
-        tr.rollout_step(i % tr.T)
+    if a.persistent:
+        tr.fused_rollout = True
+        tr.rollout_steps(0, min(a.steps, tr.T))
+    else:
+        tr.fused_rollout = False
+        for i in range(a.steps):
+            tr.rollout_step(i % tr.T)
     torch.cuda.synchronize()
     tabs = []
     for fn in ("rt_trace_read_policy", "rt_trace_read_env"):
@@ -76,7 +85,7 @@ def main():
         t[:, 0:2] = tabs[0][:, 0:2]
         t[:, 9] = tabs[0][:, 9]
     t = t.astype(np.int64)
-    t0 = t[:, 0].min()
+    t0 = t[:, 13].min() if a.persistent else t[:, 0].min()
     us = (t - t0) * 0.01  # 100 MHz
     out = {"mode": a.mode, "envs": a.envs, "phases_us": {}, "kernel_span_us": {}}
     stepped = t[:, 8] > t[:, 5]
@@ -87,6 +96,14 @@ def main():
     for k, (s0, s1) in {"k_policy_sample": (0, 1), "k_beam": (2, 4), "k_finish": (5, 8)}.items():
         out["kernel_span_us"][k] = {"first_start": float(us[:, s0].min()), "last_start": float(us[:, s0].max()),
                                     "first_end": float(us[stepped, s1].min()), "last_end": float(us[:, s1].max())}
+    if a.persistent:  # slots 13/14: each wave's kernel entry / exit
+        blk = np.arange(a.envs) // 16
+        ent, ext = us[:, 13], us[:, 14]
+        out["persistent"] = {"entry_us_pct": [float(np.percentile(ent, q)) for q in (0, 25, 50, 75, 100)],
+                             "exit_us_pct": [float(np.percentile(ext, q)) for q in (0, 25, 50, 75, 100)],
+                             "life_us_pct": [float(np.percentile(ext - ent, q)) for q in (0, 25, 50, 75, 100)],
+                             "blocks_entered_by_us": {str(x): int(np.unique(blk[ent <= x]).size)
+                                                      for x in (5, 20, 100, 500, 1000, 2000, 3000)}}
     print(json.dumps(out, indent=1))
     tr.env.close()
 
