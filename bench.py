@@ -174,7 +174,8 @@ def load_pmc(grid, envs):
     try:
         with open(p) as f:
             d = json.load(f)
-        if tuple(d.get("grid", ())) == tuple(grid) and int(d.get("envs", -1)) == envs:
+        if (tuple(d.get("grid", ())) == tuple(grid) and int(d.get("envs", -1)) == envs
+                and d.get("layout") == "lung_first"):
             return d.get("hbm_bytes_per_launch")
     except Exception:
         pass
@@ -302,7 +303,14 @@ def main():
 
     # ---------------- roofline of the dominant kernel, k_dense
     V = int(np.prod(grid))
-    bytes_launch = a.envs * 4 * V  # k_dense reads each env's f32 dose row once
+    Vl = int(np.count_nonzero(lib.lungs))
+    # k_dense reads each env's lung segment (the first Vl floats of its
+    # lung-first dose row) once: the voxels the lung reductions sum over
+    bytes_launch = a.envs * 4 * Vl
+    bytes_model = f"4 B x {Vl} lung voxels x envs (lung-first dose rows; {Vl / V:.3f} of the volume)"
+    if a.vision:  # k_dense_vis: read the C-order dose row, write the lungs and dose channels
+        bytes_launch = a.envs * 12 * V
+        bytes_model = "12 B x V x envs (k_dense_vis: dose read, two observation channels written)"
     dense_ms = kms["k_dense"]
     achieved = bytes_launch / (dense_ms * 1e-3)
     traffic = load_pmc(grid, a.envs)
@@ -310,7 +318,8 @@ def main():
             "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
             "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch, "kernel_ms": dense_ms,
             "kernel_calls_timed": kcalls, "kernel_ms_all": kms, "env_step_ms": env_ms,
-            "env_step_frac_of_hbm": a.envs * 4 * V / (env_ms * 1e-3) / HBM_PEAK,
+            "bytes_model": bytes_model,
+            "env_step_frac_of_hbm": bytes_launch / (env_ms * 1e-3) / HBM_PEAK,
             "survey_model_bytes_per_env_step": 8 * V,
             "survey_model_frac": a.envs * 8 * V / (env_ms * 1e-3) / HBM_PEAK}
     if rank == 0 and not a.env_only:

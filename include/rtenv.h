@@ -134,9 +134,13 @@ int rt_env_step(rt_env* env, const float* actions_d, float* obs_d, float* reward
 int rt_env_set_next_tumours(rt_env* env, const int32_t* tumour_ids_d, void* stream);
 
 /* State access (device pointers into library-owned memory; valid until
- * rt_env_destroy).  dose is f32[N][dose_stride] with the first D*H*W floats
- * of each row used. */
+ * rt_env_destroy).  dose is f32[N][dose_stride]; the first D*H*W floats of a
+ * row hold the env's dose volume, in C order or -- dense-mode visionless
+ * handles, whose k_dense streams only the lung voxels -- lung-first: voxel v
+ * (C-order flat index) sits at row position rt_env_dose_index(env)[v]
+ * (device i32[D*H*W]); rt_env_dose_index returns NULL for C-order rows. */
 float* rt_env_dose(rt_env* env, int64_t* dose_stride);
+const int32_t* rt_env_dose_index(rt_env* env);
 int rt_env_get_state(rt_env* env, double* pose_d /* f64[N,6] pos,dir */, int32_t* t_d,
                      int32_t* tumour_d, void* stream);
 int rt_env_set_pose(rt_env* env, const double* pose_d /* f64[N,6] */, void* stream);

@@ -17,7 +17,10 @@
 // written out where OpenBLAS fuses.  See DESIGN.md "Numerics".
 //
 // Data layout in HBM (per handle = one GPU):
-//   dose      f32[N][Vpad]   Vpad = round_up(D*H*W, 1024): rows 4 KiB aligned
+//   dose      f32[N][Vpad]   Vpad = round_up(D*H*W, 1024): rows 4 KiB aligned;
+//                            dense visionless: lung-first rows (the lung voxels in
+//                            C order, then the rest), so k_dense streams only the
+//                            lung segment; otherwise C order
 //   pose      f64[N][6]      beam position + direction
 //   lung_bits u32[Vpad/32]   shared lung mask, 1 bit per voxel (L2-resident)
 //   tumour library: sorted C-order voxel lists + per-tumour sum plans
@@ -131,7 +134,9 @@ struct EnvState {
 
 struct Library {
     const uint32_t* lung_bits;
+    const int32_t* dose_pos;  // voxel -> position in a dose row (lung-first layout), null = C order
     const int32_t* vox;
+    const int32_t* vpos;      // per tumour voxel: its dose-row position (= vox in C order)
     const uint32_t* coord;   // per tumour voxel: x << 20 | y << 10 | z (no divisions in k_finish)
     const uint32_t* ops;     // packed (a | b << 16); dst = n + op index
     const int32_t* lvl_end;  // per level: op index end (relative to op_base)
@@ -569,9 +574,10 @@ __device__ void beam_env(const BeamParams& P, int e, int lane, const float* act)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (ni[j] == v) w = w + nw[j];
-            const float old_d = dose[v];
+            const int32_t pv = P.lib.dose_pos ? P.lib.dose_pos[v] : v;
+            const float old_d = dose[pv];
             const float new_d = clip01(old_d + w * bd);
-            dose[v] = new_d;
+            dose[pv] = new_d;
             if (P.incremental && ((lbits[v >> 5] >> (v & 31)) & 1u)) {
                 dcnt += (new_d > thr ? 1 : 0) - (old_d > thr ? 1 : 0);
                 dsum += (double)new_d - (double)old_d;
@@ -629,7 +635,9 @@ struct DenseParams {
     int32_t* part_cnt;     // [N][slices]
     double* part_sum;      // [N][slices]
     int32_t slices;
-    int32_t vec_per_slice; // float4 per slice, multiple of 256
+    int32_t vec_per_slice; // float4 per slice (of the streamed segment), multiple of 256
+    int32_t lung_n;        // lung-first rows: # lung voxels (the segment k_dense streams)
+    int32_t zero_per;      // RESET: float4 of the whole row zeroed per slice
 };
 
 #define LUNG_VOXEL(comp, bit)                                                      \
@@ -642,9 +650,11 @@ struct DenseParams {
 // k_dense: the full-volume reductions of lungs_dose_reward
 // (environment.py:173-182) and info doses.lung (environment.py:235):
 // count(dose > 0.2 over lung voxels) and sum(dose over lung voxels) for every
-// env, as a read-only float4 stream of each env's dose row split in 128 KiB
-// slices (grid = slices x N).  Tumour voxels are corrected in k_finish.
-// A RESET env's slices are zeroed instead (reset_dose, environment.py:104).
+// env.  Only lung voxels contribute, and the rows are laid out lung-first, so
+// the reduction is a read-only float4 stream of each row's lung segment
+// (the first lung_n floats), split in 128 KiB slices (grid = slices x N); no
+// per-voxel mask.  Tumour voxels are corrected in k_finish.  A RESET env's
+// slices zero the whole row instead (reset_dose, environment.py:104).
 // ---------------------------------------------------------------------------
 // Non-temporal 16-B load: the 4 GiB dose stream is read once per step and
 // far exceeds L2 / Infinity Cache; the nt policy lifts k_dense from 6.1 to
@@ -661,14 +671,14 @@ __global__ __launch_bounds__(256) void k_dense(DenseParams P) {
     const int mode = P.st.setup[e].mode;
     if (mode == MODE_NOOP) return;
     float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
-    const int nvec = P.G.Vpad >> 2;
-    const int q0 = sl * P.vec_per_slice;
-    const int q1 = min(q0 + P.vec_per_slice, nvec);  // (q1 - q0) % 256 == 0
     if (mode == MODE_RESET) {
-        for (int q = q0 + tid; q < q1; q += kStepThreads) d4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int z0 = sl * P.zero_per, z1 = min(z0 + P.zero_per, P.G.Vpad >> 2);
+        for (int q = z0 + tid; q < z1; q += kStepThreads) d4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
     }
-    const uint32_t* lbits = P.lung_bits;
+    const int n = P.lung_n;
+    const int q0 = sl * P.vec_per_slice;
+    const int q1 = min(q0 + P.vec_per_slice, (n + 3) >> 2);
     const float thr = P.lung_thr;
     int cnt = 0;
     double lsum = 0.0;
@@ -681,15 +691,18 @@ __global__ __launch_bounds__(256) void k_dense(DenseParams P) {
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            int q = base + u * kStepThreads + tid;
+            const int q = base + u * kStepThreads + tid;
             if (base + u * kStepThreads >= q1) break;  // block-uniform tail
-            uint32_t lb = (lbits[q >> 3] >> ((q & 7) << 2)) & 0xFu;
-            float part = 0.0f;
-            LUNG_VOXEL(v[u].x, 0)
-            LUNG_VOXEL(v[u].y, 1)
-            LUNG_VOXEL(v[u].z, 2)
-            LUNG_VOXEL(v[u].w, 3)
-            lsum += (double)part;
+            // the segment's last float4 may hold non-lung voxels: zero them
+            // (a zero adds nothing and is never above the threshold)
+            float4 x = v[u];
+            if (4 * q + 3 >= n) {
+                if (4 * q + 1 >= n) x.y = 0.0f;
+                if (4 * q + 2 >= n) x.z = 0.0f;
+                if (4 * q + 3 >= n) x.w = 0.0f;
+            }
+            cnt += (x.x > thr ? 1 : 0) + (x.y > thr ? 1 : 0) + (x.z > thr ? 1 : 0) + (x.w > thr ? 1 : 0);
+            lsum += (((double)x.x + (double)x.y) + (double)x.z) + (double)x.w;
         }
     }
     __shared__ int s_cnt[kStepThreads / 64];
@@ -981,6 +994,7 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     const float* dose = P.st.dose + (size_t)e * P.G.Vpad;
     const int nt = m.n;
     const int32_t* tv = P.lib.vox + m.vox_base;
+    const int32_t* tp = P.lib.vpos + m.vox_base;
     const uint32_t* tc = P.lib.coord + m.vox_base;
     const double px = pose[0], py = pose[1], pz = pose[2];
     const int W = P.G.g[2], H = P.G.g[1], HW = H * W;
@@ -1008,7 +1022,7 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     for (int i = lane; i < nt; i += 64) {
         const int v = tv[i];
         const uint32_t c = tc[i];
-        const float x = dose[v];
+        const float x = dose[tp[i]];
         if (in_lds) tvals[i] = x;
         else tg[i] = x;
         const bool lung = (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u;
@@ -1467,6 +1481,10 @@ struct rt_env {
     int max_tvox = 0;
     int slices = 0;          // k_dense slices per env
     int vec_per_slice = 0;   // float4 per slice
+    int lung_first = 0;      // dose rows lung-first (dense visionless), else C order
+    int lung_n = 0;          // lung voxels (the lung-first segment)
+    int zero_per = 0;        // k_dense RESET: float4 zeroed per slice
+    int32_t* dose_pos_d = nullptr;  // voxel -> row position (lung_first)
     size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
     int finish_wave_lds = 0; // bytes per wave
     int finish_wpb = 4;      // k_finish envs per block
@@ -1477,7 +1495,7 @@ struct rt_env {
     int rollout_fin_off = 0; // offset of its per-wave regions
     int rollout_wave_lds = 0;// bytes per wave region
     int rollout_cap = 0;     // largest tumour whose sum plan fits a region
-    float* rollout_gscratch = nullptr;  // [N][2 * max_tvox] plan slots of larger tumours
+    float* gscratch = nullptr;  // [N][2 * max_tvox] plan slots of tumours above a kernel's LDS capacity
     uint32_t view_hash_mask = 0;
     int32_t* part_cnt = nullptr;
     double* part_sum = nullptr;
@@ -1658,8 +1676,17 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
             ++lung_count;
         }
     }
+    // dense visionless: lung-first dose rows (k_dense streams the lung segment)
+    env->lung_first = env->visionless && !env->incremental;
+    env->lung_n = (int)lung_count;
+    std::vector<int32_t> dpos;
+    if (env->lung_first) {
+        dpos.resize(G.V);
+        int64_t a = 0, b = lung_count;
+        for (int64_t v = 0; v < G.V; ++v) dpos[v] = (int32_t)(cfg->lungs_h[v] ? a++ : b++);
+    }
     std::vector<TumourMeta> meta(K);
-    std::vector<int32_t> vox;
+    std::vector<int32_t> vox, vpos;
     std::vector<uint32_t> coord;
     std::vector<uint32_t> ops;
     std::vector<int32_t> lvl_end;
@@ -1694,6 +1721,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
             m.obs_c[i] = (float)(c / G.S[i] * 2.0 - 1.0);
         }
         vox.insert(vox.end(), iv, iv + n);
+        for (int i = 0; i < n; ++i) vpos.push_back(env->lung_first ? dpos[iv[i]] : iv[i]);
         for (int i = 0; i < n; ++i) {
             const int64_t v = iv[i];
             coord.push_back((uint32_t)(v / ((int64_t)G.g[1] * G.g[2])) << 20 |
@@ -1731,8 +1759,11 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     env->lib.K = K;
     env->max_tvox = max_n;
     const int nvec = G.Vpad / 4;
-    env->vec_per_slice = std::min(nvec, kSliceVec);
-    env->slices = (nvec + env->vec_per_slice - 1) / env->vec_per_slice;
+    // k_dense streams the lung segment (lung-first rows); k_dense_vis whole rows
+    const int svec = env->lung_first ? std::max(1, (env->lung_n + 3) / 4) : nvec;
+    env->vec_per_slice = std::min(svec, kSliceVec);
+    env->slices = (svec + env->vec_per_slice - 1) / env->vec_per_slice;
+    env->zero_per = (nvec + env->slices - 1) / env->slices;
     const int maxdim = std::max(G.g[0], std::max(G.g[1], G.g[2]));
     env->view_hash_mask = env->visionless ? 0u : next_pow2((uint32_t)(8 * (maxdim + 2))) - 1;
     // per wave: plan slots (2 n floats), then either the plan's operands and
@@ -1777,11 +1808,13 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     const int N = env->N;
     uint32_t* d_lbits;
     uint32_t* d_coord;
-    int32_t *d_vox, *d_lvl;
+    int32_t *d_vox, *d_lvl, *d_vpos = nullptr;
     uint32_t* d_ops;
     TumourMeta* d_meta;
     EnvState& st = env->st;
     if ((rc = dev_alloc(env, &d_lbits, lbits.size())) || (rc = dev_alloc(env, &d_vox, vox.size())) ||
+        (env->lung_first && ((rc = dev_alloc(env, &d_vpos, vpos.size())) ||
+                              (rc = dev_alloc(env, &env->dose_pos_d, dpos.size())))) ||
         (rc = dev_alloc(env, &d_coord, coord.size())) ||
         (rc = dev_alloc(env, &d_ops, ops.size())) || (rc = dev_alloc(env, &d_lvl, lvl_end.size())) ||
         (rc = dev_alloc(env, &d_meta, meta.size())) ||
@@ -1794,7 +1827,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices)) ||
         (rc = dev_alloc(env, &st.lung_cnt, N)) || (rc = dev_alloc(env, &st.lung_sum, N)) ||
         (env->rollout_wpb && env->rollout_cap < max_n &&
-         (rc = dev_alloc(env, &env->rollout_gscratch, (size_t)N * 2 * max_n)))) {
+         (rc = dev_alloc(env, &env->gscratch, (size_t)N * 2 * max_n)))) {
         free_env(env);
         return rc;
     }
@@ -1806,6 +1839,8 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         pose0[(size_t)e * 6 + 4] = 1.0;
     }
     if (h2d(d_lbits, lbits.data(), lbits.size() * 4) || h2d(d_vox, vox.data(), vox.size() * 4) ||
+        (env->lung_first && (h2d(d_vpos, vpos.data(), vpos.size() * 4) ||
+                             h2d(env->dose_pos_d, dpos.data(), dpos.size() * 4))) ||
         h2d(d_coord, coord.data(), coord.size() * 4) ||
         (ops.size() && h2d(d_ops, ops.data(), ops.size() * 4)) ||
         (lvl_end.size() && h2d(d_lvl, lvl_end.data(), lvl_end.size() * 4)) ||
@@ -1821,7 +1856,9 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         return fail(RT_EDEVICE, "initial upload failed");
     }
     env->lib.lung_bits = d_lbits;
+    env->lib.dose_pos = env->dose_pos_d;
     env->lib.vox = d_vox;
+    env->lib.vpos = env->lung_first ? d_vpos : d_vox;
     env->lib.coord = d_coord;
     env->lib.ops = d_ops;
     env->lib.lvl_end = d_lvl;
@@ -1833,6 +1870,8 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
 void rt_env_destroy(rt_env* env) { free_env(env); }
 
 int rt_env_num_envs(const rt_env* env) { return env ? env->N : 0; }
+
+const int32_t* rt_env_dose_index(rt_env* env) { return env ? env->dose_pos_d : nullptr; }
 
 float* rt_env_dose(rt_env* env, int64_t* stride) {
     if (!env) return nullptr;
@@ -1901,6 +1940,8 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
     dp.part_sum = env->part_sum;
     dp.slices = env->slices;
     dp.vec_per_slice = env->vec_per_slice;
+    dp.lung_n = env->lung_n;
+    dp.zero_per = env->zero_per;
     if (ev) (void)hipEventRecord(ev[1], stream);
     if (env->incremental) {
         // no dense pass: k_beam maintains the lung count and sum
@@ -2047,7 +2088,7 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d,
     FinishParams fp = finish_params(env, obs_d, nullptr, terminated_d, nullptr);
     fp.max_tvox = env->rollout_cap;
     fp.wave_lds = env->rollout_wave_lds;
-    fp.gscratch = env->rollout_gscratch;
+    fp.gscratch = env->gscratch;
     fp.gscratch_stride = 2 * (int64_t)env->max_tvox;
     static bool big = false;
     if (!big) {

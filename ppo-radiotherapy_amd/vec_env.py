@@ -222,11 +222,17 @@ class RadiotherapyVecEnv:
         return r.obs[:M]
 
     def dose(self) -> torch.Tensor:
-        """View [N, D, H, W] of the library-owned dose volumes."""
+        """[N, D, H, W] dose volumes: a view of the library-owned rows when
+        they are in C order, a C-order copy when the handle keeps them
+        lung-first (dense-mode visionless; rt_env_dose_index)."""
         stride = ctypes_int64()
         p = self._L.rt_env_dose(self._h, stride)
         V = int(np.prod(self.grid))
         flat = _tensor_from_ptr(p, (self.num_envs, stride.value), torch.float32, self.device)
+        ip = self._L.rt_env_dose_index(self._h)
+        if ip:
+            pos = _tensor_from_ptr(ip, (V,), torch.int32, self.device).long()
+            return flat[:, pos].reshape(self.num_envs, *self.grid)
         return flat[:, :V].reshape(self.num_envs, *self.grid)
 
     def kernel_timing(self, capacity: int):

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--grid", type=int, nargs=3, required=True)
     ap.add_argument("--envs", type=int, required=True)
+    ap.add_argument("--lung-voxels", type=int, default=0,
+                    help="lung-first rows: k_dense reads lung_voxels floats per env (0: the whole volume)")
     a = ap.parse_args()
     f = counter_values(a.fetch_dir, a.kernel, "FETCH_SIZE")
     w = counter_values(a.write_dir, a.kernel, "WRITE_SIZE")
@@ -43,7 +45,8 @@ def main():
         "FETCH_SIZE_KiB_median": fk, "WRITE_SIZE_KiB_median": wk,
         "read_bytes_per_launch": 2 * fk * 1024, "write_bytes_per_launch": wk * 1024,
         "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
-        "algorithmic_bytes_per_launch": 4 * V * a.envs,
+        "layout": "lung_first" if a.lung_voxels else "c_order",
+        "algorithmic_bytes_per_launch": 4 * (a.lung_voxels or V) * a.envs,
         "correction": "FETCH_SIZE x2 (gfx950 wide coalesced reads), KiB->B",
     }
     out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / out["algorithmic_bytes_per_launch"]
