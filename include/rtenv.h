@@ -307,10 +307,12 @@ int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_
 
 /* Per-epoch helpers of the update: perm_d[i] = a keyed pseudo-random
  * permutation of [0, n) (train.py:195's shuffle); stats_d[n_mb][2] = mean and
- * unbiased std of adv over each minibatch perm[i*mb, (i+1)*mb) (train.py:215-218). */
+ * unbiased std of adv over each minibatch perm[i*mb, (i+1)*mb) (train.py:215-218),
+ * using workspace_d (>= 128 * n_minibatches floats; rt_ppo_update's workspace
+ * serves). */
 int rt_ppo_shuffle(int64_t n, uint64_t key, int64_t* perm_d, void* stream);
 int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
-                     float* stats_d, void* stream);
+                     float* stats_d, float* workspace_d, int64_t workspace_floats, void* stream);
 
 /* ---- C3D feature extractor of the vision agent (networks.py:8-45) ----------
  * One stage = Conv3d(cin, 16, 3, groups) + ReLU + MaxPool3d(2, 2, pool_pad):

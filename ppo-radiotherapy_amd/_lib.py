@@ -162,7 +162,7 @@ def load(build_if_missing: bool = True):
                            ctypes.POINTER(RtPpoHparams), vp, vp, vp, vp, i64, i64, f64, vp, i64, vp, vp, vp],
                           ctypes.c_int),
         "rt_ppo_shuffle": ([i64, ctypes.c_uint64, vp, vp], ctypes.c_int),
-        "rt_ppo_adv_stats": ([vp, vp, i32, i32, vp, vp], ctypes.c_int),
+        "rt_ppo_adv_stats": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
         "rt_conv_out_dims": ([ctypes.POINTER(RtConvLayer), ctypes.POINTER(i32)], ctypes.c_int),
         "rt_conv_relu_pool_fwd": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_conv_wgrad_workspace_floats": ([ctypes.POINTER(RtConvLayer), i32], i64),

@@ -986,23 +986,25 @@ __global__ __launch_bounds__(256) void k_shuffle(int64_t n, int h, uint64_t key,
 }
 
 // [n_mb][2] = (mean, unbiased std) of adv over each minibatch of perm
-// (train.py:215-218), sums in f64.  One 1024-thread block per minibatch; each
-// thread issues its 16 index loads, then its 16 gathers, before accumulating,
-// so a block has 16K independent loads in flight (the gathers hit a ~1 MB
-// array that lives in L2).
-constexpr int kAdvThreads = 1024, kAdvBatch = 16;
-__global__ __launch_bounds__(kAdvThreads) void k_adv_stats(const float* adv, const int64_t* perm, int mb,
-                                                          float* stats) {
+// (train.py:215-218), sums in f64.  The gathers adv[perm[j]] are random 4-B
+// reads (one cache line each), so they are spread over kAdvParts workgroups
+// per minibatch (n_mb x 32 workgroups) instead of one: k_adv_partial writes
+// (sum, sum of squares) per part, k_adv_stats adds the parts in order.
+constexpr int kAdvParts = 32, kAdvThreads = 256, kAdvBatch = 4;
+__global__ __launch_bounds__(kAdvThreads) void k_adv_partial(const float* adv, const int64_t* perm, int mb,
+                                                            double* part) {
     __shared__ double ps[kAdvThreads / 64], pq[kAdvThreads / 64];
-    const int64_t base = (int64_t)blockIdx.x * mb;
+    const int chunk = (mb + kAdvParts - 1) / kAdvParts;
+    const int j0 = blockIdx.x * chunk, j1 = min(j0 + chunk, mb);
+    const int64_t base = (int64_t)blockIdx.y * mb;
     double s = 0.0, q = 0.0;
-    for (int j0 = 0; j0 < mb; j0 += kAdvThreads * kAdvBatch) {
+    for (int jb = j0; jb < j1; jb += kAdvThreads * kAdvBatch) {
         int64_t ix[kAdvBatch];
         float a[kAdvBatch];
 #pragma unroll
         for (int u = 0; u < kAdvBatch; ++u) {
-            const int j = j0 + u * kAdvThreads + (int)threadIdx.x;
-            ix[u] = j < mb ? perm[base + j] : -1;
+            const int j = jb + u * kAdvThreads + (int)threadIdx.x;
+            ix[u] = j < j1 ? perm[base + j] : -1;
         }
 #pragma unroll
         for (int u = 0; u < kAdvBatch; ++u) a[u] = ix[u] >= 0 ? adv[ix[u]] : 0.0f;
@@ -1028,11 +1030,24 @@ __global__ __launch_bounds__(kAdvThreads) void k_adv_stats(const float* adv, con
             S += ps[w];
             Q += pq[w];
         }
-        const double mean = S / mb;
-        const double var = mb > 1 ? (Q - S * mean) / (mb - 1) : 0.0;
-        stats[2 * blockIdx.x] = (float)mean;
-        stats[2 * blockIdx.x + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
+        double* o = part + ((size_t)blockIdx.y * kAdvParts + blockIdx.x) * 2;
+        o[0] = S;
+        o[1] = Q;
     }
+}
+
+__global__ __launch_bounds__(256) void k_adv_stats(const double* part, int mb, int n_mb, float* stats) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_mb) return;
+    double S = 0.0, Q = 0.0;
+    for (int k = 0; k < kAdvParts; ++k) {
+        S += part[((size_t)i * kAdvParts + k) * 2];
+        Q += part[((size_t)i * kAdvParts + k) * 2 + 1];
+    }
+    const double mean = S / mb;
+    const double var = mb > 1 ? (Q - S * mean) / (mb - 1) : 0.0;
+    stats[2 * i] = (float)mean;
+    stats[2 * i + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
 }
 
 // RT_PPO_GRAD_KERNEL=valu selects the VALU kernel (A/B comparisons); default MFMA
@@ -1199,11 +1214,16 @@ extern "C" int rt_ppo_shuffle(int64_t n, uint64_t key, int64_t* perm_d, void* st
 }
 
 extern "C" int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
-                                float* stats_d, void* stream) {
-    if (!adv_d || !perm_d || mb_size < 1 || n_minibatches < 1 || !stats_d)
+                                float* stats_d, float* workspace_d, int64_t workspace_floats, void* stream) {
+    if (!adv_d || !perm_d || !stats_d || !workspace_d || mb_size < 1 || n_minibatches < 1 ||
+        workspace_floats < (int64_t)n_minibatches * kAdvParts * 4)
         return rt_internal_fail(RT_EINVAL, "rt_ppo_adv_stats: bad argument");
-    hipLaunchKernelGGL(k_adv_stats, dim3(n_minibatches), dim3(kAdvThreads), 0, reinterpret_cast<hipStream_t>(stream), adv_d,
-                       perm_d, mb_size, stats_d);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    double* part = reinterpret_cast<double*>(workspace_d);
+    hipLaunchKernelGGL(k_adv_partial, dim3(kAdvParts, n_minibatches), dim3(kAdvThreads), 0, st, adv_d, perm_d,
+                       mb_size, part);
+    hipLaunchKernelGGL(k_adv_stats, dim3((n_minibatches + 255) / 256), dim3(256), 0, st, part, mb_size,
+                       n_minibatches, stats_d);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;

@@ -162,7 +162,8 @@ class PPOTrainer:
                 clip_coef=float(cfg.clip_coef), clip_vloss=int(bool(cfg.clip_vloss)), norm_adv=int(bool(cfg.norm_adv)),
                 ent_coef=float(cfg.ent_coef), vf_coef=float(cfg.vf_coef), max_grad_norm=float(cfg.max_grad_norm),
                 adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
-            self._ws = torch.empty(int(L.rt_ppo_workspace_floats(self.minibatch_size)), **kw)
+            n_mb = self.batch_size // self.minibatch_size  # rt_ppo_adv_stats shares the workspace
+            self._ws = torch.empty(max(int(L.rt_ppo_workspace_floats(self.minibatch_size)), 128 * n_mb), **kw)
             self._norm_ws = torch.empty(256, **kw)
             self._perm_buf = torch.empty(self.batch_size, dtype=torch.int64, **kw)
             self._adv_stats_buf = torch.empty((self.batch_size // self.minibatch_size, 2), **kw)
@@ -461,7 +462,8 @@ class PPOTrainer:
         if self.world > 1:
             return perm, self._epoch_adv_stats(self._b_adv, perm).contiguous()
         _lib.check(L.rt_ppo_adv_stats(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, n_mb,
-                                      self._adv_stats_buf.data_ptr(), stream), "rt_ppo_adv_stats")
+                                      self._adv_stats_buf.data_ptr(), self._ws.data_ptr(), self._ws.numel(),
+                                      stream), "rt_ppo_adv_stats")
         return perm, self._adv_stats_buf
 
     def _update_fused(self):

@@ -302,6 +302,8 @@ def test_shuffle_is_a_permutation_and_adv_stats(n):
         mb = n // 8
         adv = torch.randn(n, device=dev) * 3 + 1
         st = torch.empty((8, 2), device=dev)
-        _lib.check(L.rt_ppo_adv_stats(adv.data_ptr(), p1.data_ptr(), mb, 8, st.data_ptr(), None), "adv_stats")
+        ws = torch.empty(8 * 32 * 4, device=dev)
+        _lib.check(L.rt_ppo_adv_stats(adv.data_ptr(), p1.data_ptr(), mb, 8, st.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), None), "adv_stats")
         a = adv[p1].view(8, mb)
         torch.testing.assert_close(st, torch.stack([a.mean(1), a.std(1)], 1), rtol=1e-5, atol=1e-6)
