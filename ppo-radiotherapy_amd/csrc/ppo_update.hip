@@ -23,6 +23,7 @@
 // GEMM shapes per block are 64 x 64 x 64; tiles are mapped so that one
 // wavefront shares an 8-sample group (broadcast LDS reads) and each lane owns a
 // hidden unit (bank-distinct reads of 68-float padded rows).
+#include "rt_trace.h"
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -702,8 +703,13 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
     for (int k = 0; k < (int)(sizeof(acc.sc) / sizeof(float)); ++k) acc.sc[k] = 0.0f;
     const float inv_n = 1.0f / (float)P.mb;
     const int ntiles = (P.mb + 15) / 16;
-    for (int t = blockIdx.x * NPAIR + pair; t < ntiles; t += gridDim.x * NPAIR)
+    const int tw = blockIdx.x * (MT / 64) + 2 * pair + HEAD;  // trace row of this wave
+    int nt_done = 0;
+    for (int t = blockIdx.x * NPAIR + pair; t < ntiles; t += gridDim.x * NPAIR) {
         mf_tile<HEAD>(S, P, A, Bs, Xs, GMs, c, g, t, inv_n, acc);
+        if (lane == 0 && nt_done++ == 0) RT_STAMP(tw, 6);
+    }
+    if (lane == 0) RT_STAMP(tw, 2);
 
     // ---- per-lane partials reduced over the 16 samples c of each g-group
 #pragma unroll
@@ -716,6 +722,7 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
     }
 #pragma unroll
     for (int k = 0; k < (int)(sizeof(acc.sc) / sizeof(float)); ++k) acc.sc[k] = sum16(acc.sc[k]);
+    if (lane == 0) RT_STAMP(tw, 3);
     __syncthreads();
     // ---- phase 1: both W2 of every pair in its own region, summed in pair order
     float* R = reinterpret_cast<float*>(&S);
@@ -737,6 +744,7 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
         for (int pp = 1; pp < NPAIR; ++pp) v += R[pp * kW2Region + q];
         out[(q < H * H ? O_AW2 : O_CW2 - H * H) + q] = v;
     }
+    if (lane == 0) RT_STAMP(tw, 4);
     __syncthreads();
     // ---- phase 2: everything else (1875 values), same scheme
     {
@@ -784,11 +792,13 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
         const int p = q < O_AW2 ? q : (q < O_AW2 + (O_CW2 - O_AB2) ? q - O_AW2 + O_AB2 : q - O_AW2 - (O_CW2 - O_AB2) + O_CB2);
         out[p] = v;
     }
+    if (lane == 0) RT_STAMP(tw, 5);
 }
 
 __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
     __shared__ __attribute__((aligned(16))) MfmaLds S;
     const int tid = threadIdx.x;
+    if ((tid & 63) == 0) RT_STAMP(blockIdx.x * (MT / 64) + (tid >> 6), 0);
     for (int i = tid; i < H * H; i += MT) {
         S.w2[0][(i >> 6) * WP + (i & 63)] = P.w.p[2][i];
         S.w2[1][(i >> 6) * WP + (i & 63)] = P.w.p[9][i];
@@ -817,6 +827,7 @@ __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
     for (int i = tid; i < (MT / 64) * 6 * SP; i += MT) S.scr[i / (6 * SP)][(138 + (i / SP) % 6) * SP + i % SP] = 0.0f;
     __syncthreads();
     const int wave = tid >> 6, lane = tid & 63;
+    if (lane == 0) RT_STAMP(blockIdx.x * (MT / 64) + wave, 1);
     if (wave & 1)
         mf_wave<1>(S, P, wave >> 1, lane);
     else
@@ -1228,3 +1239,5 @@ extern "C" int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
 }
+
+RT_TRACE_READ_FN(rt_trace_read_update)
