@@ -9,7 +9,10 @@ remaining keys of configs/default.yaml.
 
 A bench "step" = one vectorised rollout step of every env on every GPU:
 policy forward + Gaussian sample + the HIP env step (k_beam + k_dense +
-k_finish), i.e. train.py:143-158.  `value` = envs x steps / max-over-ranks wall time.
+k_finish), i.e. train.py:143-158, issued by the trainer's rollout call
+(rt_env_rollout_policy; --rollout-groups 2 pipelines two env groups over
+two streams in dense mode).  `value` = envs x steps / max-over-ranks
+wall time.
 Also reported:
   ppo_updates_per_s      optimizer steps/s of the PPO update phase
                          (80 minibatch steps of 32768 samples per rank, flat
@@ -86,6 +89,8 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=0)
     ap.add_argument("--step-mode", choices=["dense", "incremental"], default="dense",
                     help="env step formulation measured as `value` (the other is reported beside it)")
+    ap.add_argument("--rollout-groups", type=int, default=1, choices=[1, 2],
+                    help="dense mode: env groups of the rollout call (2 = two pipelined streams)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
     ap.add_argument("--rehearse-same-device", action="store_true",
@@ -226,6 +231,8 @@ def main():
     lib = assets.synthetic_library(grid, 1000, 0)
     env = RadiotherapyVecEnv(a.envs, visionless=not a.vision, library=lib, device=dev, seed=a.seed + rank,
                              env_id_base=rank * a.envs, step_mode=a.step_mode)
+    if not a.vision and a.step_mode == "dense":
+        env.set_rollout_groups(a.rollout_groups)
     torch.manual_seed(a.seed)
     if a.vision:
         agent = PPO_3DCNN((4, *grid), (6,), 64).to(dev)
@@ -251,7 +258,7 @@ def main():
     # ---------------- timed rollout (or env-only)
     K = a.steps
     actions = torch.rand((a.envs, 6), device=dev, generator=gen) * 2 - 1
-    env.kernel_timing(K)  # HIP events around k_beam / k_dense / k_finish on the env stream
+    env.kernel_timing(2 * K)  # HIP events around k_beam / k_dense / k_finish (one slot per env group and step)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -311,12 +318,16 @@ def main():
     if a.vision:  # k_dense_vis: read the C-order dose row, write the lungs and dose channels
         bytes_launch = a.envs * 12 * V
         bytes_model = "12 B x V x envs (k_dense_vis: dose read, two observation channels written)"
-    dense_ms = kms["k_dense"]
-    achieved = bytes_launch / (dense_ms * 1e-3)
-    traffic = load_pmc(grid, a.envs)
+    dense_ms = kms["k_dense"]  # per step: the launches of all env groups
+    launches = max(kcalls, 1) / K  # k_dense launches per step (2: pipelined env groups)
+    achieved = bytes_launch / (dense_ms * 1e-3)  # = per-launch bytes / per-launch duration
+    traffic = load_pmc(grid, a.envs)  # measured on whole-handle launches (bench.py --env-only)
+    if traffic is not None:
+        traffic /= launches  # per launch of this run's env group
     roof = {"bound": "hbm", "kernel": "k_dense", "achieved": achieved / 1e9,
             "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
-            "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch, "kernel_ms": dense_ms,
+            "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch / launches,
+            "kernel_ms": dense_ms / launches, "launches_per_step": launches, "k_dense_ms_per_step": dense_ms,
             "kernel_calls_timed": kcalls, "kernel_ms_all": kms, "env_step_ms": env_ms,
             "bytes_model": bytes_model,
             "env_step_frac_of_hbm": bytes_launch / (env_ms * 1e-3) / HBM_PEAK,
@@ -337,7 +348,7 @@ def main():
         tr.env = env2
         tr.reset()
         run_steps(tr, a.warmup)
-        env2.kernel_timing(K)
+        env2.kernel_timing(2 * K)
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
@@ -392,6 +403,7 @@ def main():
            "env_only_kernel_steps_per_s": total_envs / (env_ms * 1e-3)}
     out.update(upd)
     out["step_mode"] = a.step_mode
+    out["rollout_groups"] = a.rollout_groups if a.step_mode == "dense" and not a.vision else 1
     if other is not None:
         out["other_step_mode"] = other
     out["roofline"] = roof

@@ -153,11 +153,13 @@ int rt_env_set_tumours(rt_env* env, const int32_t* tumour_d, void* stream);
 int rt_env_num_envs(const rt_env* env);
 
 /* Live kernel timing.  rt_env_kernel_timing(env, K) creates HIP events for
- * the next K step/reset calls (0 disables; not graph-capturable while on):
- * each call records events on the caller's stream around its three kernels.
+ * the next K step launches (0 disables; not graph-capturable while on): each
+ * step/reset call -- and each env group of each step of a dense-mode
+ * rt_env_rollout_policy -- takes one slot and records events on its stream
+ * around its three kernels (beam or policy+beam, k_dense, k_finish).
  * rt_env_kernel_timing_read waits for them and returns the summed
- * milliseconds of k_beam, k_dense and k_finish (ms_out[3]) over `steps`
- * calls, then clears the ring. */
+ * milliseconds of the three (ms_out[3]) over `steps` slots, then clears the
+ * ring. */
 int rt_env_kernel_timing(rt_env* env, int32_t capacity);
 int rt_env_kernel_timing_read(rt_env* env, double* ms_out /* [3] */, int32_t* steps);
 
@@ -218,19 +220,24 @@ typedef struct rt_policy_step {
 int rt_env_step_policy(rt_env* env, const rt_policy_step* step, float* obs_d, float* reward_d,
                        uint8_t* terminated_d, float* info_d, void* stream);
 
-/* n_steps consecutive rollout steps (train.py:138-161) in ONE persistent
- * launch, incremental step mode only: each env's wave runs its policy sample,
- * env step and finish n_steps times back to back, with no grid-wide
- * synchronisation between steps (envs are independent).  Step s (0-based)
+/* n_steps consecutive rollout steps (train.py:138-161).  Incremental step
+ * mode: ONE persistent launch -- each env's wave runs its policy sample, env
+ * step and finish n_steps times back to back, with no grid-wide
+ * synchronisation between steps (envs are independent).  Dense step mode:
+ * the three launches of rt_env_step_policy per step on `stream`; with
+ * rt_env_set_rollout_groups(env, 2) the envs are split in two groups on two
+ * library streams that take turns on the HBM-bound k_dense, so one group's
+ * latency-bound kernels run beside the other's dose stream (fork/join with
+ * `stream` by events).  Step s (0-based)
  * writes the storage slices step.X_store + s * (row floats * N) -- i.e.
  * step.X_store is row `first` of contiguous [T][N][...] storage -- plus
  * reward_store[s * N + e] and info_store[(s * N + e) * RT_INFO_W] (info_store
  * may be NULL), with Philox counter step.counter + s.  Step 0 acts on
  * step.obs_in / step.done_in; later steps on the env's own outputs, which
  * are left in obs_d / terminated_d after the last step.  Same bits as
- * n_steps calls of rt_env_step_policy.  RT_EINVAL in dense step mode;
- * RT_ELIMIT if the kernel's LDS layout cannot be built (callers then step
- * with rt_env_step_policy; not reached for the visionless MLP). */
+ * n_steps calls of rt_env_step_policy.  RT_EINVAL for a vision handle;
+ * RT_ELIMIT if the persistent kernel's LDS layout cannot be built (callers
+ * then step with rt_env_step_policy; not reached for the visionless MLP). */
 typedef struct rt_policy_rollout {
     rt_policy_step step;          /* storage row of the first step, its counter */
     int32_t n_steps;
@@ -240,6 +247,9 @@ typedef struct rt_policy_rollout {
 
 int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* obs_d, uint8_t* terminated_d,
                           void* stream);
+/* Env groups of the dense-mode rt_env_rollout_policy: 1 (default, every
+ * launch on the caller's stream) or 2 (two pipelined library streams). */
+int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */

@@ -33,7 +33,7 @@ EXPORTS = [
     "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
-    "rt_env_step_policy", "rt_env_rollout_policy",
+    "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
     "rt_ppo_shuffle", "rt_ppo_adv_stats",
     "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
@@ -153,6 +153,7 @@ def load(build_if_missing: bool = True):
                               ctypes.c_uint64, i64, vp], ctypes.c_int),
         "rt_env_step_policy": ([vp, ctypes.POINTER(RtPolicyStep), vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_env_rollout_policy": ([vp, ctypes.POINTER(RtPolicyRollout), vp, vp, vp], ctypes.c_int),
+        "rt_env_set_rollout_groups": ([vp, i32], ctypes.c_int),
         "rt_ppo_workspace_floats": ([i32], i64),
         "rt_ppo_num_params": ([], i32),
         "rt_ppo_grad": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, vp,

@@ -704,6 +704,7 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
     const float inv_n = 1.0f / (float)P.mb;
     const int ntiles = (P.mb + 15) / 16;
     const int tw = blockIdx.x * (MT / 64) + 2 * pair + HEAD;  // trace row of this wave
+    (void)tw;  // used by RT_STAMP in trace builds only
     int nt_done = 0;
     for (int t = blockIdx.x * NPAIR + pair; t < ntiles; t += gridDim.x * NPAIR) {
         mf_tile<HEAD>(S, P, A, Bs, Xs, GMs, c, g, t, inv_n, acc);

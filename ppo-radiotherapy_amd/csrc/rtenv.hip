@@ -30,6 +30,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -399,7 +400,8 @@ struct BeamParams {
     const float* actions;         // [N][6] (STEP)
     const uint8_t* reset_mask;    // RESET call: NULL = all
     const int32_t* reset_ids;     // RESET call: NULL = sample
-    int32_t N;
+    int32_t N;                    // envs [e_begin, N) of the handle take part
+    int32_t e_begin;              //   (an env group of the pipelined dense rollout)
     int32_t is_reset_call;
     int32_t incremental;          // RT_STEP_INCREMENTAL (visionless only)
     uint64_t seed;
@@ -606,7 +608,7 @@ __device__ void beam_env(const BeamParams& P, int e, int lane, const float* act)
 
 __global__ __launch_bounds__(256) void k_beam(BeamParams P) {
     const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int e = P.e_begin + blockIdx.x * 4 + (threadIdx.x >> 6);
     if (e >= P.N) return;  // wave-uniform
     beam_env(P, e, lane, nullptr);
 }
@@ -638,6 +640,7 @@ struct DenseParams {
     int32_t vec_per_slice; // float4 per slice (of the streamed segment), multiple of 256
     int32_t lung_n;        // lung-first rows: # lung voxels (the segment k_dense streams)
     int32_t zero_per;      // RESET: float4 of the whole row zeroed per slice
+    int32_t e_begin;       // env of blockIdx.y == 0 (env group of the pipelined rollout)
 };
 
 #define LUNG_VOXEL(comp, bit)                                                      \
@@ -666,7 +669,7 @@ __device__ __forceinline__ float4 load_nt(const float4* p) {
 }
 
 __global__ __launch_bounds__(256) void k_dense(DenseParams P) {
-    const int sl = blockIdx.x, e = blockIdx.y;
+    const int sl = blockIdx.x, e = P.e_begin + blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int mode = P.st.setup[e].mode;
     if (mode == MODE_NOOP) return;
@@ -754,7 +757,7 @@ struct DenseVisParams {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_dense_vis(DenseVisParams PV) {
     const DenseParams& P = PV.d;
-    const int sl = blockIdx.x, e = blockIdx.y;
+    const int sl = blockIdx.x, e = P.e_begin + blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int mode = P.st.setup[e].mode;
     float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
@@ -851,7 +854,8 @@ struct FinishParams {
     int32_t max_tvox;    // per-wave LDS holds the sum plan of tumours up to max_tvox voxels
     float* gscratch;     // larger tumours (k_rollout_policy's smaller LDS share): plan slots
     int64_t gscratch_stride;  //   here, gscratch + e * stride, operands read from the library
-    int32_t N;
+    int32_t N;           // envs [e_begin, N) take part
+    int32_t e_begin;
     int32_t vision;      // obs is f32 [N][4][V]
     int32_t incremental; // lung count / sum from the k_beam-maintained counters
     uint32_t hash_mask;  // vision: beam-view hash slots - 1
@@ -1114,7 +1118,7 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
 
 __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int e = blockIdx.x * P.wpb + w;
+    const int e = P.e_begin + blockIdx.x * P.wpb + w;
     if (e >= P.N) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm_raw[];
     finish_env(P, e, lane, fsm_raw + (size_t)w * P.wave_lds);
@@ -1151,7 +1155,7 @@ __global__ __launch_bounds__(1024) void k_step_policy(BeamParams B, FinishParams
     extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
     rtpol::Lds& L = *reinterpret_cast<rtpol::Lds*>(psm);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int e = blockIdx.x * Q.wpb + w;
+    const int e = B.e_begin + blockIdx.x * Q.wpb + w;
     const bool live = e < B.N;
     if (lane == 0) RT_STAMP(e, 0);
     rtpol::stage(L, Q.w, tid, (int)blockDim.x);
@@ -1489,6 +1493,8 @@ struct rt_env {
     int finish_wave_lds = 0; // bytes per wave
     int finish_wpb = 4;      // k_finish envs per block
     int fused_wpb = 16;      // k_step_policy envs (waves) per block
+    int pipe_wpb = 4;        // ... in the pipelined dense rollout
+    size_t pipe_smem = 0;
     size_t fused_smem = 0;   // k_step_policy dynamic LDS
     int rollout_wpb = 0;     // k_rollout_policy envs per block (0: does not fit LDS)
     size_t rollout_smem = 0; // k_rollout_policy dynamic LDS
@@ -1504,6 +1510,12 @@ struct rt_env {
     std::vector<hipEvent_t> tev;
     int timing_cap = 0;
     int timing_n = 0;
+    // pipelined dense rollout (rt_env_rollout_policy in dense step mode): env
+    // groups on two library streams; events fork, hand the k_dense turn from
+    // one group to the other, join
+    int rollout_groups = 1;  // 2: measured no faster
+    hipStream_t pipe[2] = {nullptr, nullptr};
+    hipEvent_t pev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // fork, dense[2], join[2]
     std::vector<void*> allocs;
 };
 
@@ -1533,6 +1545,10 @@ void free_env(rt_env* env) {
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(env->device);
     for (hipEvent_t e : env->tev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : env->pev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t q : env->pipe)
+        if (q) (void)hipStreamDestroy(q);
     for (void* p : env->allocs) (void)hipFree(p);
     (void)hipSetDevice(cur);
     delete env;
@@ -1787,6 +1803,16 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     env->fused_wpb = 16;
     while (env->fused_wpb > 1 && fused_bytes(env->fused_wpb) > 160 * 1024) env->fused_wpb /= 2;
     env->fused_smem = fused_bytes(env->fused_wpb);
+    // pipelined dense rollout: small policy blocks, so that they find room on
+    // CUs beside the other env group's k_dense blocks (a 16-wave block needs a
+    // whole CU's registers; RT_PIPE_WPB overrides, experiments)
+    {
+        const char* pw = std::getenv("RT_PIPE_WPB");
+        int w = pw ? std::atoi(pw) : 4;
+        if (w < 1 || w > 16) w = 4;
+        env->pipe_wpb = std::min(w, env->fused_wpb);
+        env->pipe_smem = fused_bytes(env->pipe_wpb);
+    }
     // k_rollout_policy: the parameters once per block, then 16 per-wave
     // regions (h1 during the policy, the finish scratch after it); tumours
     // above the region's plan capacity keep their plan slots in gscratch
@@ -1863,6 +1889,18 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     env->lib.ops = d_ops;
     env->lib.lvl_end = d_lvl;
     env->lib.meta = d_meta;
+    if (env->lung_first) {
+        for (hipStream_t& q : env->pipe)
+            if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) {
+                free_env(env);
+                return fail(RT_EDEVICE, "hipStreamCreateWithFlags failed");
+            }
+        for (hipEvent_t& ev : env->pev)
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+                free_env(env);
+                return fail(RT_EDEVICE, "hipEventCreateWithFlags failed");
+            }
+    }
     *out = env;
     return RT_OK;
 }
@@ -1928,9 +1966,13 @@ void allow_lds(const void* kernel, size_t bytes) {
 }
 
 // k_dense / k_dense_vis (skipped in incremental mode) then k_finish
+// envs [e0, e1) (e1 < 0: all).  wait_ev: k_dense starts after it (the other
+// env group's k_dense of the pipelined rollout); done_ev: recorded after k_dense.
 int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, float* info, hipStream_t stream,
-                        hipEvent_t* ev) {
-    const int N = env->N;
+                        hipEvent_t* ev, int e0 = 0, int e1 = -1, hipEvent_t wait_ev = nullptr,
+                        hipEvent_t done_ev = nullptr) {
+    if (e1 < 0) e1 = env->N;
+    const int n = e1 - e0;
     DenseParams dp{};
     dp.G = env->G;
     dp.lung_thr = env->C.lung_thr;
@@ -1942,25 +1984,30 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
     dp.vec_per_slice = env->vec_per_slice;
     dp.lung_n = env->lung_n;
     dp.zero_per = env->zero_per;
+    dp.e_begin = e0;
+    if (wait_ev) RT_HIP(hipStreamWaitEvent(stream, wait_ev, 0));
     if (ev) (void)hipEventRecord(ev[1], stream);
     if (env->incremental) {
         // no dense pass: k_beam maintains the lung count and sum
     } else if (env->visionless) {
-        hipLaunchKernelGGL(k_dense, dim3(env->slices, N), dim3(kStepThreads), 0, stream, dp);
+        hipLaunchKernelGGL(k_dense, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dp);
         RT_LAUNCH_CHECK("k_dense");
     } else {
         DenseVisParams dv{dp, obs};
-        hipLaunchKernelGGL(k_dense_vis, dim3(env->slices, N), dim3(kStepThreads), 0, stream, dv);
+        hipLaunchKernelGGL(k_dense_vis, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dv);
         RT_LAUNCH_CHECK("k_dense_vis");
     }
+    if (done_ev) RT_HIP(hipEventRecord(done_ev, stream));
     if (ev) (void)hipEventRecord(ev[2], stream);
     FinishParams fp = finish_params(env, obs, reward, term, info);
+    fp.e_begin = e0;
+    fp.N = e1;
     static bool big_lds = false;
     if (!big_lds) {
         allow_lds(reinterpret_cast<const void*>(&k_finish), env->finish_smem);
         big_lds = true;
     }
-    hipLaunchKernelGGL(k_finish, dim3((N + fp.wpb - 1) / fp.wpb), dim3(64 * fp.wpb), env->finish_smem, stream, fp);
+    hipLaunchKernelGGL(k_finish, dim3((n + fp.wpb - 1) / fp.wpb), dim3(64 * fp.wpb), env->finish_smem, stream, fp);
     RT_LAUNCH_CHECK("k_finish");
     if (ev) (void)hipEventRecord(ev[3], stream);
     return RT_OK;
@@ -2047,6 +2094,97 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* ps, float* obs_d, floa
     return launch_dense_finish(env, obs_d, reward_d, terminated_d, info_d, s, ev);
 }
 
+// ---------------------------------------------------------------------------
+// Dense step mode rollout: per step k_step_policy -> k_dense -> k_finish (the
+// launches of rt_env_step_policy, same bits), with the envs split in two
+// groups on two library streams.  k_dense is HBM-bound and needs the whole
+// chip; the policy/pose/march kernel and k_finish are latency-bound one wave
+// per env.  The groups take turns on k_dense (each group's k_dense waits for
+// the other's previous one), so while one group streams its dose rows the
+// other runs its latency-bound kernels beside it; only the first policy
+// kernel and the last finish are not hidden.  Fork and join with the
+// caller's stream are events; nothing synchronises the host.
+// ---------------------------------------------------------------------------
+static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
+                         hipStream_t s) {
+    const rt_policy_step* ps = &r->step;
+    const int N = env->N;
+    const bool two = env->rollout_groups > 1 && env->pipe[0] && N >= 32;
+    const int wpb = two ? env->pipe_wpb : env->fused_wpb;
+    const size_t smem = two ? env->pipe_smem : env->fused_smem;
+    const int h = two ? (N / 2 + wpb - 1) / wpb * wpb : N;  // group boundary on a block boundary
+    const int bounds[3] = {0, h, N};
+    const int G = two ? 2 : 1;
+    hipStream_t S[2] = {s, s};
+    if (two) {
+        RT_HIP(hipEventRecord(env->pev[0], s));
+        for (int g = 0; g < 2; ++g) {
+            S[g] = env->pipe[g];
+            RT_HIP(hipStreamWaitEvent(S[g], env->pev[0], 0));
+        }
+    }
+    static bool big = false;
+    if (!big) {
+        allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), env->fused_smem);
+        big = true;
+    }
+    PolicyStepParams Q{};
+    for (int i = 0; i < rtpol::kTensors; ++i) {
+        if (!ps->params[i]) return fail(RT_EINVAL, "rt_env_rollout_policy: NULL parameter");
+        Q.w.p[i] = ps->params[i];
+    }
+    Q.seed = ps->seed;
+    Q.id_base = ps->env_id_base;
+    Q.wpb = wpb;
+    const size_t Nn = (size_t)N;
+    for (int t = 0; t < r->n_steps; ++t) {
+        Q.obs_in = t == 0 ? ps->obs_in : obs_d;
+        Q.done_in = t == 0 ? ps->done_in : terminated_d;
+        Q.obs_store = ps->obs_store + (size_t)t * Nn * rtpol::NOBS;
+        Q.done_store = ps->done_store + (size_t)t * Nn;
+        Q.act_store = ps->act_store + (size_t)t * Nn * rtpol::NACT;
+        Q.logp_store = ps->logp_store + (size_t)t * Nn;
+        Q.value_store = ps->value_store + (size_t)t * Nn;
+        Q.counter = ps->counter + (uint64_t)t;
+        float* rew = r->reward_store + (size_t)t * Nn;
+        float* info = r->info_store ? r->info_store + (size_t)t * Nn * RT_INFO_W : nullptr;
+        for (int g = 0; g < G; ++g) {
+            const int e0 = bounds[g], e1 = bounds[g + 1];
+            hipEvent_t* ev = next_timing_slot(env);
+            if (ev) (void)hipEventRecord(ev[0], S[g]);
+            BeamParams bp = beam_params(env, false, Q.act_store, nullptr, nullptr);
+            FinishParams fp = finish_params(env, obs_d, rew, terminated_d, info);
+            bp.e_begin = e0;
+            bp.N = e1;
+            hipLaunchKernelGGL(k_step_policy<false>, dim3((e1 - e0 + wpb - 1) / wpb), dim3(64 * wpb), smem,
+                               S[g], bp, fp, Q);
+            RT_LAUNCH_CHECK("k_step_policy");
+            // k_dense turns: group 0 of step t after group 1 of step t-1, group 1 after group 0
+            static const bool serial = [] {
+                const char* v = std::getenv("RT_PIPE_SERIAL");  // experiments: 0 = no k_dense turns
+                return !(v && v[0] == '0');
+            }();
+            hipEvent_t wait = (two && serial && (t > 0 || g == 1)) ? env->pev[1 + (1 - g)] : nullptr;
+            int rc = launch_dense_finish(env, obs_d, rew, terminated_d, info, S[g], ev, e0, e1, wait,
+                                         two ? env->pev[1 + g] : nullptr);
+            if (rc) return rc;
+        }
+    }
+    if (two) {
+        for (int g = 0; g < 2; ++g) {
+            RT_HIP(hipEventRecord(env->pev[3 + g], S[g]));
+            RT_HIP(hipStreamWaitEvent(s, env->pev[3 + g], 0));
+        }
+    }
+    return RT_OK;
+}
+
+int rt_env_set_rollout_groups(rt_env* env, int32_t groups) {
+    if (!env || groups < 1 || groups > 2) return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups must be 1 or 2");
+    env->rollout_groups = groups;
+    return RT_OK;
+}
+
 int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
                           void* stream) {
     if (!env || !r || !obs_d || !terminated_d || !r->reward_store) return fail(RT_EINVAL, "NULL argument");
@@ -2054,10 +2192,10 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d,
     if (!ps->params || !ps->obs_in || !ps->obs_store || !ps->done_store || !ps->act_store || !ps->logp_store ||
         !ps->value_store)
         return fail(RT_EINVAL, "NULL argument");
-    if (!env->visionless || !env->incremental)
-        return fail(RT_EINVAL, "rt_env_rollout_policy: visionless env in incremental step mode only");
+    if (!env->visionless) return fail(RT_EINVAL, "rt_env_rollout_policy: the fused policy is the visionless MLP");
     if (ps->n_params != rtpol::kTensors) return fail(RT_EINVAL, "rt_env_rollout_policy: expected 13 parameter tensors");
     if (r->n_steps < 1) return fail(RT_EINVAL, "rt_env_rollout_policy: n_steps < 1");
+    if (!env->incremental) return rollout_dense(env, r, obs_d, terminated_d, as_stream(stream));
     if (env->rollout_wpb == 0)
         return fail(RT_ELIMIT, "rt_env_rollout_policy: policy + finish scratch exceed LDS (largest tumour too big)");
     RolloutParams R{};

@@ -142,9 +142,9 @@ class PPOTrainer:
         self.fused_env_step = (self.fused_policy and bool(getattr(cfg, "fused_env_step", True))
                                and getattr(env, "visionless", False))
         self._step_structs = None
-        # ... and the whole rollout as ONE persistent launch (rt_env_rollout_policy)
-        # whenever the env runs the incremental step mode: same bits as the
-        # stepwise launches
+        # ... and whole rollout runs in one call (rt_env_rollout_policy): one
+        # persistent launch in incremental step mode, the stepwise launches from
+        # C in dense mode; same bits as step_policy
         self.fused_rollout = self.fused_env_step and bool(getattr(cfg, "fused_rollout", True))
         self._policy_counter = 0
         self._policy_seed = int(getattr(cfg, "seed", 0)) * 1_000_003 + 7919 * rank + 1
@@ -274,11 +274,10 @@ class PPOTrainer:
 
     @torch.no_grad()
     def rollout_steps(self, first: int, count: int):
-        """Rollout steps first .. first+count-1 (storage rows): one persistent
-        launch when the env supports it (rt_env_rollout_policy), otherwise
-        step by step."""
-        if not (self.fused_rollout and getattr(self.env, "step_mode", "dense") == "incremental"
-                and getattr(self.env, "visionless", False)):
+        """Rollout steps first .. first+count-1 (storage rows): one library
+        call when the env supports it (rt_env_rollout_policy), otherwise step
+        by step."""
+        if not (self.fused_rollout and getattr(self.env, "visionless", False)):
             for step in range(first, first + count):
                 self.rollout_step(step)
             return

@@ -147,9 +147,11 @@ class RadiotherapyVecEnv:
         return self.obs, rew, self.terminated.view(torch.bool), self.truncated, LazyInfos(self._infos, info)
 
     def rollout_policy(self, rollout) -> int:
-        """`rollout.n_steps` fused rollout steps in one persistent launch
-        (rt_env_rollout_policy; incremental step mode).  `rollout` is an
-        _lib.RtPolicyRollout naming the storage rows of its first step.
+        """`rollout.n_steps` fused rollout steps (rt_env_rollout_policy): one
+        persistent launch in incremental step mode; in dense mode the stepwise
+        launches (optionally two env groups pipelined over two streams,
+        set_rollout_groups).  `rollout` is
+        an _lib.RtPolicyRollout naming the storage rows of its first step.
         Returns the library's status (RT_ELIMIT: the tumour library is too
         large for the kernel's LDS budget -- step with step_policy instead)."""
         rc = self._L.rt_env_rollout_policy(self._h, ctypes.byref(rollout), _lib.ptr(self.obs),
@@ -157,6 +159,10 @@ class RadiotherapyVecEnv:
         if rc not in (0, _lib.RT_ELIMIT):
             _lib.check(rc, "rt_env_rollout_policy")
         return rc
+
+    def set_rollout_groups(self, groups: int):
+        """Env groups of the dense-mode rollout_policy: 2 (pipelined streams) or 1."""
+        _lib.check(self._L.rt_env_set_rollout_groups(self._h, int(groups)), "rt_env_set_rollout_groups")
 
     def set_next_tumours(self, ids):
         t = torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
@@ -237,7 +243,8 @@ class RadiotherapyVecEnv:
 
     def kernel_timing(self, capacity: int):
         """Record HIP events around k_beam/k_dense/k_finish for the next
-        `capacity` step/reset calls (0 disables)."""
+        `capacity` step launches (0 disables); a dense-mode rollout_policy step
+        takes one slot per env group."""
         _lib.check(self._L.rt_env_kernel_timing(self._h, int(capacity)), "rt_env_kernel_timing")
 
     def kernel_timing_read(self):

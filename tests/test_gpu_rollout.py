@@ -1,10 +1,12 @@
-"""rt_env_rollout_policy (the whole rollout as ONE persistent launch, one wave
-per env running its steps back to back) produces the bits of stepwise
-rt_env_step_policy launches: rollout storage, rewards, infos, observations,
-dose volumes and poses, across episode ends (NEXT_STEP autoreset), a block
-tail (N not a multiple of 16), runs that start mid-storage, and libraries
-whose largest tumour's sum plan exceeds a wave's LDS region (plan slots in the
-global scratch row: 1000 and 12000 voxels)."""
+"""rt_env_rollout_policy produces the bits of stepwise rt_env_step_policy
+launches: rollout storage, rewards, infos, observations, dose volumes and
+poses, across episode ends (NEXT_STEP autoreset), a block tail (N not a
+multiple of 16), runs that start mid-storage, and libraries whose largest
+tumour's sum plan exceeds a wave's LDS region.  Incremental step mode: the
+whole rollout as ONE persistent launch (one wave per env running its steps
+back to back; plan slots in the global scratch row for 1000 and 12000 voxel
+tumours).  Dense step mode: the stepwise launches of two env groups
+pipelined over two library streams (and the one-group variant)."""
 import os
 import sys
 from types import SimpleNamespace
@@ -23,14 +25,14 @@ def _cfg(fused_rollout):
                            vf_coef=0.5, max_grad_norm=0.5, seed=3, fused_env_step=True, fused_rollout=fused_rollout)
 
 
-def _trainer(fused_rollout, lib, n):
+def _trainer(fused_rollout, lib, n, step_mode="incremental"):
     import _rtpkg  # noqa: F401
     from ppo_radiotherapy_amd.networks import PPO
     from ppo_radiotherapy_amd.ppo import PPOTrainer
     from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
 
     dev = torch.device("cuda")
-    env = RadiotherapyVecEnv(n, visionless=True, library=lib, device=dev, seed=11, step_mode="incremental")
+    env = RadiotherapyVecEnv(n, visionless=True, library=lib, device=dev, seed=11, step_mode=step_mode)
     torch.manual_seed(0)
     agent = PPO((9,), (6,), 64).to(dev)
     with torch.no_grad():
@@ -67,8 +69,10 @@ def _compare(a, b, it):
     assert torch.equal(a.env.dose(), b.env.dose())
 
 
-@pytest.mark.parametrize("big", [0, 1000, 12000])
-def test_persistent_rollout_is_bitwise_the_stepwise_rollout(big):
+@pytest.mark.parametrize("step_mode,big,groups", [("incremental", 0, 0), ("incremental", 1000, 0),
+                                                   ("incremental", 12000, 0), ("dense", 0, 2),
+                                                   ("dense", 1000, 2), ("dense", 0, 1)])
+def test_rollout_call_is_bitwise_the_stepwise_rollout(step_mode, big, groups):
     from ppo_radiotherapy_amd import assets
 
     if not torch.cuda.is_available():
@@ -77,8 +81,10 @@ def test_persistent_rollout_is_bitwise_the_stepwise_rollout(big):
     if big:
         lib = _with_big_tumour(lib, big)
     n = 1000
-    a = _trainer(True, lib, n)
-    b = _trainer(False, lib, n)
+    a = _trainer(True, lib, n, step_mode)
+    b = _trainer(False, lib, n, step_mode)
+    if groups:
+        a.env.set_rollout_groups(groups)
     assert a.fused_rollout and not b.fused_rollout
     T = a.T
     # runs of storage rows per iteration: whole rollouts and split ones
@@ -93,13 +99,13 @@ def test_persistent_rollout_is_bitwise_the_stepwise_rollout(big):
         ended += int(a.dones.sum().item())
         seen_big += int(a.env.get_state()[2].eq(lib.n_tumours - 1).sum().item())
     assert ended >= n  # every env's first episode ended inside the compared steps
-    assert a.fused_rollout  # the persistent kernel ran every run
+    assert a.fused_rollout  # the rollout call ran every run
     assert seen_big > 0  # some envs ran episodes on the largest tumour
     a.env.close()
     b.env.close()
 
 
-def test_rollout_policy_rejects_dense_mode():
+def test_rollout_policy_rejects_vision_and_bad_groups():
     import _rtpkg  # noqa: F401
     from ppo_radiotherapy_amd import _lib, assets
     from ppo_radiotherapy_amd.networks import PPO
@@ -112,6 +118,11 @@ def test_rollout_policy_rejects_dense_mode():
     env = RadiotherapyVecEnv(64, visionless=True, library=lib, device="cuda", seed=1, step_mode="dense")
     tr = PPOTrainer(_cfg(True), env, PPO((9,), (6,), 64).cuda(), torch.device("cuda"), 0, 1)
     tr.reset()
-    with pytest.raises(_lib.RtError, match="incremental"):
-        env.rollout_policy(tr._rollout_struct(0, 4))
+    ro = tr._rollout_struct(0, 4)
+    with pytest.raises(_lib.RtError, match="groups"):
+        env.set_rollout_groups(3)
     env.close()
+    venv = RadiotherapyVecEnv(4, visionless=False, library=lib, device="cuda", seed=1)
+    with pytest.raises(_lib.RtError, match="visionless"):
+        venv.rollout_policy(ro)
+    venv.close()
