@@ -13,7 +13,8 @@ import os
 
 from . import build as _build
 
-LIB_PATH = _build.OUT
+# RT_LIB_PATH: load another build of the library (kernel-variant experiments)
+LIB_PATH = os.environ.get("RT_LIB_PATH") or _build.OUT
 
 INFO_NAMES = {
     "total": 0, "tumour": 1, "lung": 2, "distance_to_tumour": 3, "dose_tumour": 4, "dose_lung": 5,
