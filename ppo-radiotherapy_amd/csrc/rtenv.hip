@@ -43,8 +43,14 @@
 namespace {
 
 constexpr int kStepThreads = 256;
-constexpr int kUnroll = 8;               // float4 loads in flight per thread
-constexpr int kSliceVec = 8192;          // k_dense slice: 8192 float4 = 128 KiB of dose
+#ifndef RT_DENSE_UNROLL
+#define RT_DENSE_UNROLL 8
+#endif
+#ifndef RT_SLICE_VEC
+#define RT_SLICE_VEC 8192
+#endif
+constexpr int kUnroll = RT_DENSE_UNROLL;  // float4 loads in flight per thread
+constexpr int kSliceVec = RT_SLICE_VEC;   // k_dense slice: 8192 float4 = 128 KiB of dose
 constexpr int kMaxTumourVoxels = 16384;  // tumour voxels (op slots n + n-1 < 2^16; k_finish LDS per wave)
 constexpr int kMaxGridDim = 1024;
 constexpr int kMaxPlanLevels = 64;       // levels of a tumour's sum plan (LDS copy in k_finish)
