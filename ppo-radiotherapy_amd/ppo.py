@@ -671,6 +671,46 @@ class PPOTrainer:
             else:
                 self.optimizer.param_groups[0]["lr"] = frac * float(self.cfg.learning_rate)
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self) -> dict:
+        """What a resumed run continues from (the reference saves
+        the agent's state_dict only, train.py:270-279): agent, optimizer
+        (torch Adam state and, for the fused update, the flat Adam moments and
+        step count), iteration, global step, the rollout policy's Philox
+        counter and the sampling/shuffle generator states.  The envs are not
+        part of it: a resumed run starts fresh episodes."""
+        d = {"agent": self.agent.state_dict(), "optimizer": self.optimizer.state_dict(),
+             "iteration": self.iteration, "global_step": self.global_step, "policy_counter": self._policy_counter,
+             "world": self.world}
+        if self.gen is not None:
+            d["gen"] = self.gen.get_state()
+        if self.fused_update:
+            d["adam"] = {"exp_avg": self._exp_avg.detach().clone(), "exp_avg_sq": self._exp_avg_sq.detach().clone(),
+                         "step": self._adam_step}
+            d["host_gen"] = self._host_gen.get_state()
+        return d
+
+    def load_state_dict(self, d: dict):
+        """Inverse of state_dict (parameters are copied in place, so the flat
+        parameter / gradient buffers of the fused update keep their views)."""
+        with torch.no_grad():
+            self.agent.load_state_dict(d["agent"])
+        self.optimizer.load_state_dict(d["optimizer"])
+        self.iteration = int(d["iteration"])
+        self.global_step = int(d["global_step"])
+        self._policy_counter = int(d["policy_counter"])
+        if self.gen is not None and "gen" in d and int(d.get("world", 1)) == self.world:
+            self.gen.set_state(d["gen"].cpu())
+        if self.fused_update:
+            a = d.get("adam")
+            if a is None:
+                raise ValueError("checkpoint has no fused-update Adam state")
+            self._exp_avg.copy_(a["exp_avg"])
+            self._exp_avg_sq.copy_(a["exp_avg_sq"])
+            self._adam_step = int(a["step"])
+            if "host_gen" in d and int(d.get("world", 1)) == self.world:
+                self._host_gen.set_state(d["host_gen"].cpu())
+
     def train_iteration(self, iteration: int, num_iterations: int) -> IterStats:
         self.anneal(iteration, num_iterations)
         t0 = time.perf_counter()

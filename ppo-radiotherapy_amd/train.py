@@ -4,6 +4,9 @@ Same CLI, same config keys, same output layout:
   {output_dir}/{run_name}/config.yaml
   {output_dir}/tensorboard/{run_name}/          (TensorBoard or scalars.jsonl)
   {output_dir}/models/{run_name}/{exp_name}_{iteration}.model   (agent.state_dict())
+plus, with `save_checkpoint` (default), a full trainer checkpoint beside each
+model in {output_dir}/checkpoints/{run_name}/{exp_name}_{iteration}.ckpt that
+`resume_from` continues (PPOTrainer.state_dict: agent, Adam state, counters).
 
 Multi-GPU: launch with `python -m torch.distributed.run --nproc-per-node N
 train.py ...`; `num_envs` is the global env count, sharded evenly over the
@@ -64,7 +67,14 @@ def train(cfg, writer, device, output_dir=None, run_name=None, rank=0, world=1):
     gen.manual_seed(int(cfg.seed) * 7919 + rank)
     tr = PPOTrainer(cfg, envs, agent, device, rank, world, gen)
     tr.reset(seed=int(cfg.seed))
-    iterator = range(1, int(cfg.num_iterations) + 1)
+    start = 1
+    if cfg.get("resume_from"):
+        ck = torch.load(cfg.resume_from, map_location=device, weights_only=True)
+        tr.load_state_dict(ck)
+        start = tr.iteration + 1
+        if rank == 0:
+            print(f"resumed from {cfg.resume_from} at iteration {start}")
+    iterator = range(start, int(cfg.num_iterations) + 1)
     if cfg.use_tqdm and rank == 0:
         try:
             from tqdm import tqdm
@@ -89,6 +99,9 @@ def train(cfg, writer, device, output_dir=None, run_name=None, rank=0, world=1):
             model_path = f"{output_dir}/models/{run_name}/{cfg.exp_name}_{iteration}.model"
             torch.save(agent.state_dict(), model_path)
             print(f"model saved to {model_path}")
+            if cfg.get("save_checkpoint", True):
+                os.makedirs(f"{output_dir}/checkpoints/{run_name}", exist_ok=True)
+                torch.save(tr.state_dict(), f"{output_dir}/checkpoints/{run_name}/{cfg.exp_name}_{iteration}.ckpt")
     envs.close()
     return agent
 

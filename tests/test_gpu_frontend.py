@@ -102,6 +102,35 @@ def test_train_cli_outputs(tmp_path):
     assert all(torch.isfinite(p).all() for p in agent.parameters())
 
 
+def test_train_checkpoint_resume(tmp_path):
+    """SURVEY §5 checkpoint/resume: every save writes a full trainer checkpoint
+    beside the model; resume_from continues at the next iteration with the
+    agent, Adam moments/step and counters of the checkpoint."""
+    import train as train_mod
+
+    out = tmp_path / "out"
+    train_mod.main(["--config-file", _tiny_cfg(tmp_path, num_saves=3), "--output-dir", str(out)])
+    run = os.listdir(out / "checkpoints")[0]
+    cks = sorted(os.listdir(out / "checkpoints" / run))
+    assert cks == ["tiny_1.ckpt", "tiny_2.ckpt", "tiny_3.ckpt"]
+    c1 = torch.load(out / "checkpoints" / run / "tiny_1.ckpt", weights_only=True)
+    assert c1["iteration"] == 1 and c1["global_step"] == 64 * 16
+    per_iter = 2 * 4  # update_epochs x num_minibatches optimizer steps
+    if "adam" in c1:
+        assert c1["adam"]["step"] == per_iter
+    out2 = tmp_path / "out2"
+    agent = train_mod.main(["--config-file", _tiny_cfg(tmp_path, num_saves=3,
+                                                         resume_from=str(out / "checkpoints" / run / "tiny_1.ckpt")),
+                            "--output-dir", str(out2)])
+    run2 = os.listdir(out2 / "models")[0]
+    assert sorted(os.listdir(out2 / "models" / run2)) == ["tiny_2.model", "tiny_3.model"]
+    c3 = torch.load(out2 / "checkpoints" / run2 / "tiny_3.ckpt", weights_only=True)
+    assert c3["iteration"] == 3 and c3["global_step"] == 3 * 64 * 16
+    if "adam" in c3:
+        assert c3["adam"]["step"] == 3 * per_iter
+    assert all(torch.isfinite(p).all() for p in agent.parameters())
+
+
 def test_evaluate_reference_checkpoint(tmp_path, golden):
     import ppo_eval
     from networks import PPO
