@@ -1,4 +1,4 @@
-"""Trainer host logic and the data-parallel path on CPU (gloo, world_size 2)."""
+"""Trainer host logic and the data-parallel path on CPU (gloo, world_size 2, 4, 8)."""
 import os
 import socket
 import sys
@@ -94,8 +94,8 @@ def _dp_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_data_parallel_gloo_world2():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_data_parallel_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -117,11 +117,12 @@ def test_data_parallel_gloo_world2():
         assert p.exitcode == 0
     assert len(res) == world
     res = sorted(res, key=lambda x: x[0])
-    (_, l0, g0, p0, e0), (_, l1, g1, p1, e1) = res
-    np.testing.assert_allclose(g0, (l0 + l1) / 2, rtol=1e-6, atol=1e-7)   # averaged bucket
-    np.testing.assert_array_equal(g0, g1)
-    np.testing.assert_array_equal(p0, p1)  # replicas stay identical through the update
-    assert e0 < 1e-5 and e1 < 1e-5
+    local = np.stack([r[1] for r in res])
+    np.testing.assert_allclose(res[0][2], local.mean(axis=0), rtol=1e-5, atol=1e-7)   # averaged bucket
+    for r in res[1:]:
+        np.testing.assert_array_equal(r[2], res[0][2])
+        np.testing.assert_array_equal(r[3], res[0][3])  # replicas stay identical through the update
+    assert all(r[4] < 1e-5 for r in res)
 
 
 def test_micro_batched_gradient_equals_full_minibatch():
