@@ -10,8 +10,10 @@ remaining keys of configs/default.yaml.
 A bench "step" = one vectorised rollout step of every env on every GPU:
 policy forward + Gaussian sample + the HIP env step (k_beam + k_dense +
 k_finish), i.e. train.py:143-158, issued by the trainer's rollout call
-(rt_env_rollout_policy; --rollout-groups 2 pipelines two env groups over
-two streams in dense mode).  `value` = envs x steps / max-over-ranks
+(rt_env_rollout_policy: in dense mode two env groups pipelined over two
+streams, taking turns on a persistent k_dense; --rollout-groups 1 issues
+every launch on one stream).  roofline.isolated: k_dense of a one-group
+pass over the same workload (the kernel alone on the chip).  `value` = envs x steps / max-over-ranks
 wall time.
 Also reported:
   ppo_updates_per_s      optimizer steps/s of the PPO update phase
@@ -89,7 +91,7 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=0)
     ap.add_argument("--step-mode", choices=["dense", "incremental"], default="dense",
                     help="env step formulation measured as `value` (the other is reported beside it)")
-    ap.add_argument("--rollout-groups", type=int, default=1, choices=[1, 2],
+    ap.add_argument("--rollout-groups", type=int, default=2, choices=[1, 2],
                     help="dense mode: env groups of the rollout call (2 = two pipelined streams)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
@@ -278,6 +280,19 @@ def main():
     total_envs = a.envs * world
     steps_per_s = total_envs * K / dt
 
+    # ---------------- k_dense alone on the chip (one env group), same workload
+    iso = None
+    if not a.vision and not a.env_only and a.step_mode == "dense" and a.rollout_groups > 1:
+        env.set_rollout_groups(1)
+        run_steps(tr, 4)
+        env.kernel_timing(2 * K)
+        run_steps(tr, K)
+        torch.cuda.synchronize()
+        ki, ci = env.kernel_timing_read()
+        env.kernel_timing(0)
+        env.set_rollout_groups(a.rollout_groups)
+        iso = {k: max_over_ranks(v) for k, v in ki.items()}  # per launch (one per step)
+
     # ---------------- PPO update phase + one full iteration
     upd = {}
     if not a.no_update and not a.env_only:
@@ -333,6 +348,12 @@ def main():
             "env_step_frac_of_hbm": bytes_launch / (env_ms * 1e-3) / HBM_PEAK,
             "survey_model_bytes_per_env_step": 8 * V,
             "survey_model_frac": a.envs * 8 * V / (env_ms * 1e-3) / HBM_PEAK}
+    if iso is not None:
+        iso_ach = a.envs * 4 * Vl / (iso["k_dense"] * 1e-3)
+        roof["isolated"] = {"kernel_ms": iso["k_dense"], "achieved": iso_ach / 1e9, "frac": iso_ach / HBM_PEAK,
+                            "kernel_ms_all": iso, "note": "k_dense over all envs, one launch per step, "
+                                                          "nothing co-running (one-group pass)"}
+    roof["step_frac_of_hbm"] = a.envs * 4 * Vl / (dt / K) / HBM_PEAK if not a.vision else None
     if rank == 0 and not a.env_only:
         cbw = copy_ceiling(dev)
         roof["measured_copy_ceiling_GBps"] = cbw / 1e9

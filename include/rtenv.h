@@ -224,11 +224,12 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* step, float* obs_d, fl
  * mode: ONE persistent launch -- each env's wave runs its policy sample, env
  * step and finish n_steps times back to back, with no grid-wide
  * synchronisation between steps (envs are independent).  Dense step mode:
- * the three launches of rt_env_step_policy per step on `stream`; with
- * rt_env_set_rollout_groups(env, 2) the envs are split in two groups on two
- * library streams that take turns on the HBM-bound k_dense, so one group's
- * latency-bound kernels run beside the other's dose stream (fork/join with
- * `stream` by events).  Step s (0-based)
+ * the envs are split in two groups on two library streams that take turns
+ * on the HBM-bound k_dense (a persistent variant that leaves CU slots free),
+ * so one group's latency-bound policy/beam and finish kernels run beside the
+ * other's dose stream (fork/join with `stream` by events);
+ * rt_env_set_rollout_groups(env, 1) issues the three launches of
+ * rt_env_step_policy per step on `stream` instead.  Step s (0-based)
  * writes the storage slices step.X_store + s * (row floats * N) -- i.e.
  * step.X_store is row `first` of contiguous [T][N][...] storage -- plus
  * reward_store[s * N + e] and info_store[(s * N + e) * RT_INFO_W] (info_store
@@ -247,8 +248,8 @@ typedef struct rt_policy_rollout {
 
 int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* obs_d, uint8_t* terminated_d,
                           void* stream);
-/* Env groups of the dense-mode rt_env_rollout_policy: 1 (default, every
- * launch on the caller's stream) or 2 (two pipelined library streams). */
+/* Env groups of the dense-mode rt_env_rollout_policy: 2 (default, two
+ * pipelined library streams) or 1 (every launch on the caller's stream). */
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:

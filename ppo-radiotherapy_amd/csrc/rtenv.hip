@@ -674,8 +674,7 @@ __device__ __forceinline__ float4 load_nt(const float4* p) {
     return make_float4(t.x, t.y, t.z, t.w);
 }
 
-__global__ __launch_bounds__(256) void k_dense(DenseParams P) {
-    const int sl = blockIdx.x, e = P.e_begin + blockIdx.y;
+__device__ __forceinline__ void dense_item(const DenseParams& P, int sl, int e) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int mode = P.st.setup[e].mode;
     if (mode == MODE_NOOP) return;
@@ -733,6 +732,21 @@ __global__ __launch_bounds__(256) void k_dense(DenseParams P) {
         P.part_cnt[(size_t)e * P.slices + sl] = c;
         P.part_sum[(size_t)e * P.slices + sl] = t;
     }
+    __syncthreads();  // s_cnt / s_sum are reused by the next item of a persistent block
+}
+
+__global__ __launch_bounds__(256) void k_dense(DenseParams P) {
+    dense_item(P, blockIdx.x, P.e_begin + blockIdx.y);
+}
+
+// k_dense with a fixed grid (a few blocks per CU) looping over the (env,
+// slice) items of envs [e_begin, e_begin + n_env): the pipelined dense
+// rollout's dose stream.  It leaves CU slots free for the other env group's
+// latency-bound kernels (the grid version fills every slot and has a launch
+// tail), and 6 blocks x 4 waves per CU keep ~16 MB of loads in flight.
+__global__ __launch_bounds__(256) void k_dense_persist(DenseParams P, int n_env) {
+    const int n_items = n_env * P.slices;
+    for (int it = blockIdx.x; it < n_items; it += gridDim.x) dense_item(P, it % P.slices, P.e_begin + it / P.slices);
 }
 
 // Store 4 consecutive voxels [v0, v0+4) of one obs channel row.
@@ -1499,7 +1513,9 @@ struct rt_env {
     int finish_wave_lds = 0; // bytes per wave
     int finish_wpb = 4;      // k_finish envs per block
     int fused_wpb = 16;      // k_step_policy envs (waves) per block
-    int pipe_wpb = 4;        // ... in the pipelined dense rollout
+    int pipe_wpb = 8;        // ... in the pipelined dense rollout
+    int pipe_dense_bpc = 6;  // its k_dense: persistent, blocks per CU
+    int num_cu = 256;        // compute units of the device
     size_t pipe_smem = 0;
     size_t fused_smem = 0;   // k_step_policy dynamic LDS
     int rollout_wpb = 0;     // k_rollout_policy envs per block (0: does not fit LDS)
@@ -1519,7 +1535,7 @@ struct rt_env {
     // pipelined dense rollout (rt_env_rollout_policy in dense step mode): env
     // groups on two library streams; events fork, hand the k_dense turn from
     // one group to the other, join
-    int rollout_groups = 1;  // 2: measured no faster
+    int rollout_groups = 2;  // DESIGN.md §3 "Pipelined dense rollout"
     hipStream_t pipe[2] = {nullptr, nullptr};
     hipEvent_t pev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // fork, dense[2], join[2]
     std::vector<void*> allocs;
@@ -1674,6 +1690,11 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
 
     rt_env* env = new rt_env();
     env->device = device;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            env->num_cu = prop.multiProcessorCount;
+    }
     env->N = cfg->num_envs;
     env->seed = cfg->seed;
     env->env_id_base = cfg->env_id_base;
@@ -1814,10 +1835,12 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     // whole CU's registers; RT_PIPE_WPB overrides, experiments)
     {
         const char* pw = std::getenv("RT_PIPE_WPB");
-        int w = pw ? std::atoi(pw) : 4;
-        if (w < 1 || w > 16) w = 4;
+        int w = pw ? std::atoi(pw) : 8;
+        if (w < 1 || w > 16) w = 8;
         env->pipe_wpb = std::min(w, env->fused_wpb);
         env->pipe_smem = fused_bytes(env->pipe_wpb);
+        const char* pb = std::getenv("RT_DENSE_PERSIST");  // experiments: 0 = grid k_dense
+        if (pb) env->pipe_dense_bpc = std::max(0, std::atoi(pb));
     }
     // k_rollout_policy: the parameters once per block, then 16 per-wave
     // regions (h1 during the policy, the finish scratch after it); tumours
@@ -1976,7 +1999,7 @@ void allow_lds(const void* kernel, size_t bytes) {
 // env group's k_dense of the pipelined rollout); done_ev: recorded after k_dense.
 int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, float* info, hipStream_t stream,
                         hipEvent_t* ev, int e0 = 0, int e1 = -1, hipEvent_t wait_ev = nullptr,
-                        hipEvent_t done_ev = nullptr) {
+                        hipEvent_t done_ev = nullptr, int persist_bpc = 0) {
     if (e1 < 0) e1 = env->N;
     const int n = e1 - e0;
     DenseParams dp{};
@@ -1996,7 +2019,12 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
     if (env->incremental) {
         // no dense pass: k_beam maintains the lung count and sum
     } else if (env->visionless) {
-        hipLaunchKernelGGL(k_dense, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dp);
+        if (persist_bpc > 0) {
+            hipLaunchKernelGGL(k_dense_persist, dim3(persist_bpc * env->num_cu), dim3(kStepThreads), 0, stream, dp,
+                               n);
+        } else {
+            hipLaunchKernelGGL(k_dense, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dp);
+        }
         RT_LAUNCH_CHECK("k_dense");
     } else {
         DenseVisParams dv{dp, obs};
@@ -2172,7 +2200,7 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
             }();
             hipEvent_t wait = (two && serial && (t > 0 || g == 1)) ? env->pev[1 + (1 - g)] : nullptr;
             int rc = launch_dense_finish(env, obs_d, rew, terminated_d, info, S[g], ev, e0, e1, wait,
-                                         two ? env->pev[1 + g] : nullptr);
+                                         two ? env->pev[1 + g] : nullptr, two ? env->pipe_dense_bpc : 0);
             if (rc) return rc;
         }
     }
