@@ -143,8 +143,8 @@ class PPOTrainer:
                                and getattr(env, "visionless", False))
         self._step_structs = None
         # ... and whole rollout runs in one call (rt_env_rollout_policy): one
-        # persistent launch in incremental step mode, the stepwise launches from
-        # C in dense mode; same bits as step_policy
+        # persistent launch in incremental step mode, two pipelined env groups
+        # in dense mode; same bits as step_policy
         self.fused_rollout = self.fused_env_step and bool(getattr(cfg, "fused_rollout", True))
         self._policy_counter = 0
         self._policy_seed = int(getattr(cfg, "seed", 0)) * 1_000_003 + 7919 * rank + 1

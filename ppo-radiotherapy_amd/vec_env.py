@@ -148,9 +148,9 @@ class RadiotherapyVecEnv:
 
     def rollout_policy(self, rollout) -> int:
         """`rollout.n_steps` fused rollout steps (rt_env_rollout_policy): one
-        persistent launch in incremental step mode; in dense mode the stepwise
-        launches (optionally two env groups pipelined over two streams,
-        set_rollout_groups).  `rollout` is
+        persistent launch in incremental step mode; in dense mode two env
+        groups pipelined over two streams around a persistent k_dense
+        (set_rollout_groups(1): the stepwise launches on one stream).  `rollout` is
         an _lib.RtPolicyRollout naming the storage rows of its first step.
         Returns the library's status (RT_ELIMIT: the tumour library is too
         large for the kernel's LDS budget -- step with step_policy instead)."""
@@ -161,7 +161,7 @@ class RadiotherapyVecEnv:
         return rc
 
     def set_rollout_groups(self, groups: int):
-        """Env groups of the dense-mode rollout_policy: 2 (pipelined streams) or 1."""
+        """Env groups of the dense-mode rollout_policy: 2 (default, pipelined streams) or 1."""
         _lib.check(self._L.rt_env_set_rollout_groups(self._h, int(groups)), "rt_env_set_rollout_groups")
 
     def set_next_tumours(self, ids):
