@@ -174,10 +174,11 @@ def copy_ceiling(dev, gib: float = 2.0, reps: int = 10) -> float:
     return bw
 
 
-def load_pmc(grid, envs):
-    """Per-launch HBM traffic of k_dense from the committed rocprofv3 PMC run
-    (tools/parse_pmc.py; gfx950 FETCH_SIZE x2 correction applied there)."""
-    p = os.path.join(REPO, "profiles", "k_dense_pmc.json")
+def load_pmc(grid, envs, kernel="k_dense"):
+    """Per-launch HBM traffic of k_dense / k_dense_persist (`envs` per launch)
+    from the committed rocprofv3 PMC runs (tools/parse_pmc.py; gfx950
+    FETCH_SIZE x2 correction applied there)."""
+    p = os.path.join(REPO, "profiles", f"{kernel}_pmc.json")
     try:
         with open(p) as f:
             d = json.load(f)
@@ -336,9 +337,10 @@ def main():
     dense_ms = kms["k_dense"]  # per step: the launches of all env groups
     launches = max(kcalls, 1) / K  # k_dense launches per step (2: pipelined env groups)
     achieved = bytes_launch / (dense_ms * 1e-3)  # = per-launch bytes / per-launch duration
-    traffic = load_pmc(grid, a.envs)  # measured on whole-handle launches (bench.py --env-only)
-    if traffic is not None:
-        traffic /= launches  # per launch of this run's env group
+    if launches > 1.5:  # pipelined: k_dense_persist over half the envs (tools/gpu_dense_persist_pmc.sh)
+        traffic = load_pmc(grid, a.envs // 2, "k_dense_persist")
+    else:  # whole-handle grid launches (tools/gpu_dense_pmc.sh, bench.py --env-only)
+        traffic = load_pmc(grid, a.envs)
     roof = {"bound": "hbm", "kernel": "k_dense", "achieved": achieved / 1e9,
             "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
             "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch / launches,
