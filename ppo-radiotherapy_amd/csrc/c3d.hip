@@ -75,7 +75,12 @@ struct Geom {
     int32_t YS, ZS, CS;  // LDS strides
 };
 
-template <int PZB, int PYB>
+// LDS stride residues (mod 32 dwords): (4, 8, 16) make the forward's reads
+// (16 positions x 4 channels per ds_read_b32) conflict-free; the weight
+// gradient's B gather (16 (channel, tap) columns x 4 x positions) needs
+// (4, 12, 8) -- with (4, 8, 16) it took 2.4-2.6x the conflict-free LDS cycles
+// (bank model over every stage geometry; PMC SQ_LDS_BANK_CONFLICT agreed)
+template <int PZB, int PYB, int RY = 4, int RZ = 8, int RC = 16>
 Geom make_geom(const rt_conv_layer* L) {
     Geom g{};
     g.D = L->in_dims[0];
@@ -94,9 +99,9 @@ Geom make_geom(const rt_conv_layer* L) {
     g.ZL = 2 * PZB + 2;
     g.YL = 2 * PYB + 2;
     g.XL = 4 * g.XT + 2;
-    g.YS = round_mod(g.XL, 4);
-    g.ZS = round_mod(g.YL * g.YS, 8);
-    g.CS = round_mod(g.ZL * g.ZS, 16);
+    g.YS = round_mod(g.XL, RY);
+    g.ZS = round_mod(g.YL * g.YS, RZ);
+    g.CS = round_mod(g.ZL * g.ZS, RC);
     return g;
 }
 
@@ -662,7 +667,7 @@ template <int CIN, int PZB, int PYB>
 int launch_wgrad(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                  const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
     WgradParams P{};
-    P.g = make_geom<PZB, PYB>(L);
+    P.g = make_geom<PZB, PYB, 4, 12, 8>(L);
     P.x = x;
     P.rows = rows;
     P.dP = dP;
