@@ -1817,6 +1817,10 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     wave_bytes = (wave_bytes + 15) / 16 * 16;
     env->finish_wave_lds = (int)wave_bytes;
     env->finish_wpb = 4;
+    if (const char* fw = std::getenv("RT_FINISH_WPB")) {  // experiments: k_finish waves per block (1, 2, 4)
+        const int v = std::atoi(fw);
+        if (v == 1 || v == 2 || v == 4) env->finish_wpb = v;
+    }
     while (env->finish_wpb > 1 && (size_t)env->finish_wpb * wave_bytes > 160 * 1024) env->finish_wpb /= 2;
     env->finish_smem = (size_t)env->finish_wpb * wave_bytes;
     if (env->finish_smem > 160 * 1024) { free_env(env); return fail(RT_ELIMIT, "LDS budget exceeded"); }
