@@ -199,6 +199,33 @@ def reference_style_library(n_tumours: int = 1000, seed: int = 0, shape=None, da
                          offsets=np.asarray(offsets, np.int64))
 
 
+def resampled_reference_library(shape=(64, 64, 64), data_dir: str = DATA_DIR) -> TumourLibrary:
+    """The reference's own lungs and 1000 tumours on another grid: every
+    volume nearest-resampled with the lung mask's cell-centre mapping
+    (`resample_nearest`), so an agent trained on the reference grid
+    (saves/*.model, whose observations are grid-normalised, environment.py:
+    259-268) sees the same normalised geometry.  Tumours that vanish under
+    the resampling keep their nearest voxel."""
+    ref = reference_library(data_dir)
+    lungs = resample_nearest(ref.lungs, shape).astype(np.uint8)
+    idx = [np.minimum(((np.arange(n) + 0.5) * s / n).astype(np.int64), s - 1) for n, s in zip(shape, ref.shape)]
+    parts, offsets = [], [0]
+    for k in range(ref.n_tumours):
+        src = ref.tumour_dense(k) > 0
+        vol = src[np.ix_(*idx)]
+        flat = np.flatnonzero(vol.ravel())
+        if flat.size == 0:  # thinner than a target cell: the cell nearest its centroid
+            c = ref.centroid(k)
+            cell = [int(np.argmin(np.abs((np.arange(n) + 0.5) * s / n - (ci + 0.5))))
+                    for n, s, ci in zip(shape, ref.shape, c)]
+            flat = np.array([np.ravel_multi_index(tuple(cell), shape)])
+        flat = np.sort(flat).astype(np.int32)
+        parts.append(flat)
+        offsets.append(offsets[-1] + flat.size)
+    return TumourLibrary(shape=tuple(shape), lungs=lungs, names=list(ref.names),
+                         voxels=np.concatenate(parts), offsets=np.asarray(offsets, np.int64))
+
+
 def library_for(grid) -> TumourLibrary:
     """The reference grid uses the reference assets; any other grid the
     synthetic generator (cached per process)."""

@@ -1,0 +1,208 @@
+"""The headline path (bench.py `value`) checked directly against the oracle.
+
+bench.py times `rt_env_rollout_policy` at BASELINE configs[1] (4096 envs,
+64^3): in dense step mode two env groups pipelined over two library streams
+around the persistent `k_dense_persist`, in incremental mode the persistent
+`k_rollout_policy`.  Here that exact call runs 2 x 64 = 128 rollout steps
+(crossing the t = 100 truncation of every env's first episode, irradiation
+terminations and the NEXT_STEP autoresets with their Philox tumour redraws)
+with the reference's trained agent (saves/20M.model, so many episodes end by
+irradiation), and >= 32 sampled envs are replayed on the C oracle
+(environment.py:77-105 reset, :193-243 step; gymnasium 1.0 NEXT_STEP
+autoreset + RecordEpisodeStatistics) on the actions the kernel sampled:
+
+* observations bit-exact (f32), rewards and reward components within 1e-5,
+  doses.tumour bit-exact, doses.lung within 1e-5 relative;
+* terminated / autoreset / episode r and l identical;
+* the tumour of every autoreset = the restated Philox draw (tests/rt_rng.py);
+* the final dose volumes bit-exact.
+"""
+import os
+import sys
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import rt_rng  # noqa: E402
+
+SEED = 20261016
+T_CALL = 64
+CALLS = 2
+
+
+def _agent(golden, dev, still=False):
+    """The reference's trained agent (saves/20M.model).  still=True: its
+    action mean zeroed and std 0.0025 -- the beam stays near its reset pose
+    (S/2, [0,1,0]), so tumours on that beam line are irradiated in ~10 steps
+    (no trained agent reaches ratio 0.9 on ordinary tumours)."""
+    from ppo_radiotherapy_amd.networks import PPO
+
+    z = golden("policy_ref.npz")
+    agent = PPO((9,), (6,), 64).to(dev)
+    agent.load_state_dict({k[4:]: torch.tensor(v) for k, v in z.items() if k.startswith("sd::")})
+    if still:
+        with torch.no_grad():
+            agent.actor_mean[4].weight.zero_()
+            agent.actor_mean[4].bias.zero_()
+            agent.actor_logstd.fill_(-6.0)
+    return agent
+
+
+def beam_line_library(lib, n_rods=1000):
+    """`lib` plus n_rods short rods of voxels on the reset beam's line
+    (x = D/2, z = W/2, along y; draw_line.py puts weight 1 on them): envs
+    that draw one terminate by irradiation (environment.py:184-191)."""
+    from ppo_radiotherapy_amd.assets import TumourLibrary
+
+    D, H, W = lib.shape
+    rng = np.random.default_rng(1)
+    parts, off = [lib.voxels], list(lib.offsets)
+    for _ in range(n_rods):
+        L = int(rng.integers(1, 8))
+        y0 = H // 2 - int(rng.integers(0, L))
+        ys = np.arange(y0, y0 + L)
+        v = np.sort(((D // 2) * H + ys) * W + W // 2).astype(np.int32)
+        parts.append(v)
+        off.append(off[-1] + len(v))
+    return TumourLibrary(lib.shape, lib.lungs, list(lib.names) + [f"rod{i}" for i in range(n_rods)],
+                         np.concatenate(parts).astype(np.int32), np.asarray(off, np.int64))
+
+
+def run_headline_rollout(golden, step_mode, lib, n_envs=4096, calls=CALLS, t_call=T_CALL, still=False):
+    """The bench's rollout call on n_envs envs; returns host copies of the
+    rollout storage of every call, the final obs, and the env (still open)."""
+    from ppo_radiotherapy_amd.ppo import PPOTrainer
+    from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
+
+    dev = torch.device("cuda")
+    env = RadiotherapyVecEnv(n_envs, visionless=True, library=lib, device=dev, seed=SEED, step_mode=step_mode)
+    if step_mode == "dense":
+        env.set_rollout_groups(2)
+    cfg = SimpleNamespace(num_steps=t_call, num_minibatches=4, update_epochs=1, learning_rate=3e-4, anneal_lr=False,
+                          gamma=0.99, gae_lambda=0.95, norm_adv=True, clip_coef=0.1, clip_vloss=True, ent_coef=0.0,
+                          vf_coef=0.5, max_grad_norm=0.5, seed=7, fused_env_step=True, fused_rollout=True)
+    tr = PPOTrainer(cfg, env, _agent(golden, dev, still), dev, 0, 1)
+    assert tr.fused_rollout
+    tr.reset()
+    rec = {k: [] for k in ("obs", "dones", "actions", "rewards", "infos")}
+    for _ in range(calls):
+        tr.rollout_steps(0, t_call)
+        assert tr.fused_rollout  # the rollout call ran (no stepwise fallback)
+        torch.cuda.synchronize()
+        for k in rec:
+            rec[k].append(getattr(tr, k).cpu().numpy().copy())
+    out = {k: np.concatenate(v, axis=0) for k, v in rec.items()}
+    out["final_obs"] = env.obs.cpu().numpy().copy()
+    return out, env, lib
+
+
+def pick_sample(rec, n_irr=12, n_trunc=12, n_rand=8, seed=0):
+    """Envs whose episodes end by irradiation (length < 100), envs that hit
+    the t = 100 truncation, and random envs; each ended an episode inside the
+    window, so each replay crosses an autoreset + Philox redraw."""
+    I = rec["infos"]
+    ep_done = I[..., 17] > 0.5
+    ep_len = np.where(ep_done, I[..., 19], 0)
+    irr = np.flatnonzero(((ep_len > 0) & (ep_len < 100)).any(axis=0))
+    trunc = np.flatnonzero((ep_len == 100).any(axis=0))
+    rng = np.random.default_rng(seed)
+    assert len(irr) >= n_irr and len(trunc) >= n_trunc, (len(irr), len(trunc))
+    # prefer envs that ran >= 2 episodes to the end (two redraws in the window)
+    multi = ep_done.sum(axis=0) >= 2
+    irr_m = irr[multi[irr]]
+    a = rng.choice(irr_m, min(n_irr // 2, len(irr_m)), replace=False) if len(irr_m) else np.array([], int)
+    rest = np.setdiff1d(irr, a)
+    a = np.concatenate([a, rng.choice(rest, n_irr - len(a), replace=False)])
+    b = rng.choice(np.setdiff1d(trunc, a), n_trunc, replace=False)
+    c = rng.choice(np.setdiff1d(np.arange(I.shape[1]), np.concatenate([a, b])), n_rand, replace=False)
+    return sorted(set(a.tolist()) | set(b.tolist()) | set(c.tolist()))
+
+
+def replay_env(rec, lib, e, seed=SEED, env_id_base=0, tol=1e-5):
+    """Replay env e's slice of the rollout on the oracle; returns (oracle,
+    episodes finished, irradiation ends, truncation ends)."""
+    T = rec["rewards"].shape[0]
+    K = lib.n_tumours
+    lungs = lib.lungs.astype(np.float32)
+    gid = env_id_base + e
+    draws = 0
+    tid = rt_rng.tumour_draw(seed, gid, draws, K)
+    draws += 1
+    oe = O.OracleEnv(lungs, lib.tumour_dense(tid))
+    obs = oe.reset()
+    obs_seq = rec["obs"]
+    np.testing.assert_array_equal(obs_seq[0, e], obs.astype(np.float32), err_msg=f"env {e} reset obs")
+    pending = False
+    ret, length = 0.0, 0
+    n_ep = n_irr = n_trunc = 0
+    for t in range(T):
+        info = rec["infos"][t, e]
+        assert bool(rec["dones"][t, e] > 0.5) == pending, f"env {e} t {t}: done flag"
+        if pending:  # NEXT_STEP autoreset: action ignored, reward 0, reset obs
+            tid = rt_rng.tumour_draw(seed, gid, draws, K)
+            draws += 1
+            obs = oe.reset(lib.tumour_dense(tid))
+            assert rec["rewards"][t, e] == 0.0 and info[16] == 0.0 and info[17] == 0.0, f"env {e} t {t}"
+            pending = False
+            ret, length = 0.0, 0
+        else:
+            obs, oi, done = oe.step(rec["actions"][t, e])
+            assert info[16] == 1.0, f"env {e} t {t}: stepped"
+            r = rec["rewards"][t, e]
+            assert abs(r - oi[0]) <= tol, (e, t, r, oi[0])
+            for k in (0, 1, 2, 3):
+                assert abs(info[k] - oi[k]) <= tol, (e, t, k, info[k], oi[k])
+            assert info[4] == np.float32(oi[4]), (e, t, "doses.tumour")
+            assert abs(info[5] - oi[5]) <= tol * max(1.0, abs(oi[5])), (e, t, "doses.lung")
+            np.testing.assert_allclose(info[6:10], oi[6:10], atol=1e-5, err_msg=f"env {e} t {t} overshoot")
+            np.testing.assert_allclose(info[10:16], oi[10:16], atol=1e-5, err_msg=f"env {e} t {t} pose")
+            ret += float(np.float32(oi[0]))
+            length += 1
+            assert bool(info[17] > 0.5) == done, f"env {e} t {t}: episode end"
+            if done:
+                assert abs(info[18] - ret) <= 1e-4 * max(1.0, abs(ret)) and info[19] == length, (e, t, info[18], ret, info[19], length)
+                n_ep += 1
+                n_irr += length < 100
+                n_trunc += length == 100
+                pending = True
+        nxt = obs_seq[t + 1, e] if t + 1 < T else rec["final_obs"][e]
+        np.testing.assert_array_equal(nxt, obs.astype(np.float32), err_msg=f"env {e} t {t} obs")
+    return oe, n_ep, n_irr, n_trunc
+
+
+@pytest.mark.parametrize("policy", ["trained", "still"])
+@pytest.mark.parametrize("step_mode", ["dense", "incremental"])
+def test_headline_rollout_vs_oracle(golden, step_mode, policy):
+    """4096 envs x 64^3 (the synthetic configs[1] library plus 1000 tumours on
+    the reset beam's line), 128 steps of the bench's rollout call; 32 sampled
+    envs replayed on the oracle across irradiation ends, truncations and
+    Philox autoresets.  "trained": the reference agent's own actions (38 envs
+    end an episode by irradiation, the rest at t = 100); "still": near-zero
+    actions, thousands of short irradiation episodes (several autoresets per
+    env)."""
+    from ppo_radiotherapy_amd import assets
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    lib = beam_line_library(assets.synthetic_library((64, 64, 64), 1000, 0))
+    rec, env, _ = run_headline_rollout(golden, step_mode, lib, still=policy == "still")
+    sample = pick_sample(rec)
+    assert len(sample) >= 32
+    dose = env.dose()
+    tot = {"ep": 0, "irr": 0, "trunc": 0}
+    for e in sample:
+        oe, n_ep, n_irr, n_trunc = replay_env(rec, lib, e)
+        tot["ep"] += n_ep
+        tot["irr"] += n_irr
+        tot["trunc"] += n_trunc
+        got = dose[e].cpu().numpy().reshape(lib.shape)
+        np.testing.assert_array_equal(got.view(np.uint32), oe.dose.view(np.uint32), err_msg=f"env {e} dose")
+    assert tot["irr"] >= 12 and tot["trunc"] >= 12, tot
+    env.close()

@@ -106,3 +106,17 @@ def test_reference_style_generator_against_reference_library():
     assert again.names == lib.names and np.array_equal(again.voxels, lib.voxels)
     lib64 = assets.reference_style_library(20, seed=1, shape=(64, 64, 64))
     assert lib64.shape == (64, 64, 64) and lib64.n_tumours == 20
+
+
+def test_tumour_draw_rng_known_answers():
+    """tests/rt_rng.py's Philox4x32-10 (the restated tumour-draw contract the
+    headline replay predicts autoresets with) against the Random123 KATs."""
+    import rt_rng
+
+    assert rt_rng.philox4x32_10((0, 0, 0, 0), (0, 0)) == (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)
+    assert rt_rng.philox4x32_10((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2) == (0x408F276D, 0x41C83B0E, 0xA20BC7C6,
+                                                                          0x6D5451FD)
+    assert rt_rng.philox4x32_10((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0)) == (
+        0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)
+    draws = [rt_rng.tumour_draw(5, g, i, 1000) for g in range(50) for i in range(4)]
+    assert min(draws) >= 0 and max(draws) < 1000 and len(set(draws)) > 150
