@@ -70,7 +70,12 @@ def test_conv_relu_pool_forward(cin, groups, dims, pad, B):
     cx = 2 * px - pad[2] + (k & 1)
     flat = (cz * ch + cy) * cw + cx
     active = (a >> 3) & 1
-    assert torch.equal(active.bool(), ref > 0)
+    # activity = (max > 0): where the f64 window max is within f32 rounding of
+    # zero, the f32 conv may land on the other side of the ReLU
+    bad = active.bool() != (ref > 0)
+    if bad.any():
+        worst = float(ref[bad].abs().max())
+        assert worst <= 2e-5, (int(bad.sum()), worst)
     # where the window max is unambiguous (top-2 gap), the index equals torch's
     yfull = F.relu(F.conv3d(x[rows].double(), w.double(), b.double(), groups=groups))
     ypad = F.pad(yfull, (pad[2], pad[2], pad[1], pad[1], pad[0], pad[0]), value=-1.0)
