@@ -28,9 +28,19 @@ Also reported:
   roofline               k_dense (the dominant kernel) vs HBM: HIP events the
                          library records around it on the env stream over
                          the timed region; traffic from profiles/k_dense_pmc.json
+  steady_state           >= 101 steps (2 x num_steps) with the envs' episode
+                         clocks staggered uniformly, so the window carries the
+                         t = 100 truncation autoresets a long run pays
+  other_step_mode.roofline
+                         the incremental step's transaction model (random
+                         128-B line RMWs per env-step) vs a measured random-line
+                         RMW ceiling (rt_probe_random_rmw)
+  update_allreduce_ms    (n_gpus > 1) the flat-gradient all-reduce alone
   cpu_baseline           op-for-op NumPy port of the reference step on one
-                         host core, same 64^3 workload (bounded sample); beside
-                         it the same on all host cores and the scalar C port
+                         pinned host core, BASELINE.md §3 config C1 (reference
+                         grid and tumours, seed 1, default_rng(0) actions;
+                         bounded sample); beside it the same on the box's core
+                         share and the scalar C port
   roofline.measured_copy_ceiling_GBps
                          device copy bandwidth measured in the same run
 
@@ -84,6 +94,7 @@ def parse():
                     help="CPU-baseline sample budget per leg (4 legs: numpy/C x 1/all cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-update", action="store_true")
+    ap.add_argument("--no-steady", action="store_true", help="skip the >= 101-step steady-state window")
     ap.add_argument("--env-only", action="store_true", help="time rt_env_step alone (profiling)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--vision", action="store_true",
@@ -114,14 +125,15 @@ def trainer_cfg(a):
                            micro_batch=a.micro_batch)
 
 
-def cpu_baseline(grid: int, seconds: float):
+def cpu_baseline(seconds: float):
     """The reference's single-env step on the host cores (oracle/cpu_bench.py,
-    run as a child process): the op-for-op NumPy port on one core is `value`;
-    the same on every available core (one pinned process each, capped at 16)
-    and the scalar C restatement are reported beside it."""
+    run as a child process) on BASELINE.md §3's config C1 (reference grid and
+    tumours, np.random.seed(1), default_rng(0) actions): the op-for-op NumPy
+    port on one pinned core is `value`; the same on the box's core share (one
+    pinned process each) and the scalar C restatement are reported beside it."""
     import subprocess
 
-    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_bench.py"), "--grid", str(grid),
+    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_bench.py"), "--grid", "0",
            "--seconds", str(seconds), "--kinds", "numpy,c"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=20 * seconds + 300)
     if r.returncode != 0:
@@ -129,9 +141,9 @@ def cpu_baseline(grid: int, seconds: float):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     one = d["numpy"]["one_core"]
     out = {"value": one["value"], "unit": "env steps/s", "cores": 1, "kind": "port",
-           "sample": f"{one['steps']} visionless steps of one env at {grid}^3 (oracle/numpy_env.py, "
-                     f"U(-1,1) actions, autoreset), {one['seconds']:.1f} s on 1 host core ({d['cpu_model']})",
-           "cpu_model": d["cpu_model"], "cores_available": d["cores_available"]}
+           "sample": f"{one['steps']} visionless steps of one env, {d['config']} (oracle/numpy_env.py), "
+                     f"{one['seconds']:.1f} s on 1 pinned host core ({d['cpu_model']})",
+           "cpu_model": d["cpu_model"], "cores_available": d["cores_available"], "cores_cap": d["cores_cap"]}
     if "all_cores" in d["numpy"]:
         out["all_cores"] = {k: d["numpy"]["all_cores"][k] for k in ("value", "cores", "steps")}
     out["c_port"] = {"one_core": d["c"]["one_core"]["value"],
@@ -151,6 +163,80 @@ def run_steps(tr, k: int):
         c = min(tr.T - s, k - i)
         tr.rollout_steps(s, c)
         i += c
+
+
+def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int = 2):
+    """Env steps/s over a window of calls x T (>= 101) rollout steps with the
+    envs' episode clocks spread uniformly: a 100-step pre-roll resets the envs
+    with e % 100 == k at pre-roll step k (masked rt_env_reset), so every step
+    of the window carries ~1 % of the envs through the t = 100 truncation
+    autoreset (a RESET zeroes the env's whole dose row) -- the steady state of
+    a long run, which a window started right after reset() never reaches."""
+    import torch
+
+    N, T = env.num_envs, tr.T
+    e_idx = torch.arange(N, device=dev)
+    for k in range(100):
+        env.reset(options={"mask": (e_idx % 100) == k})
+        tr.rollout_steps(k % T, 1)
+    resets = torch.zeros((), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        tr.rollout_steps(0, T)
+        resets += (tr.infos[..., 16] == 0).sum()  # autoresets in these T steps (one tiny reduction per call)
+    torch.cuda.synchronize()
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    K = calls * T
+    return {"steps": K, "ms_per_step": 1000 * dt / K, "env_steps_per_s": total_envs * K / dt,
+            "autoresets_in_window": int(resets.item()),
+            "episode_phase": "staggered uniformly over the 100-step episode (masked resets in a 100-step pre-roll)"}
+
+
+def incremental_transactions(env, lib):
+    """Transaction model of one incremental env-step: the
+    march read-modify-writes the distinct 128-B dose lines its splats touch,
+    the finish reads the lines of the tumour's voxels.  Counted on the beams
+    the envs applied last (rt_env_beam_list) and their current tumours."""
+    import torch
+
+    idx, _, cnt = env.beam_list()
+    cap = idx.shape[1]
+    valid = torch.arange(cap, device=idx.device)[None, :] < cnt.clamp_min(0)[:, None]
+    lines = torch.where(valid, idx // 32, torch.full_like(idx, -1))
+    lines, _ = lines.sort(dim=1)
+    distinct = ((lines[:, 1:] != lines[:, :-1]) & (lines[:, 1:] >= 0)).sum(1) + (lines[:, 0] >= 0).long()
+    beam_lines = float(distinct.double().mean())
+    _, _, tum = env.get_state()
+    per_tumour = np.array([len(np.unique(lib.tumour_voxels(k) // 32)) for k in range(lib.n_tumours)], np.float64)
+    tumour_lines = float(per_tumour[tum.cpu().numpy()].mean())
+    return beam_lines, tumour_lines
+
+
+def random_rmw_ceiling(dev, lib_obj, floats: int, lanes: int = 1 << 18, lines_per_lane: int = 64):
+    """Random 128-B line read-modify-writes per second (rt_probe_random_rmw:
+    one float per lane and line, 4 lines in flight per lane) over a buffer of
+    the dose array's size."""
+    import torch
+
+    from ppo_radiotherapy_amd import _lib
+
+    buf = torch.zeros(floats, dtype=torch.float32, device=dev)
+    st = _lib.stream_handle()
+    _lib.check(lib_obj.rt_probe_random_rmw(buf.data_ptr(), floats, lanes, lines_per_lane, 1, st), "probe")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record()
+    for r in range(reps):
+        _lib.check(lib_obj.rt_probe_random_rmw(buf.data_ptr(), floats, lanes, lines_per_lane, 2 + r, st), "probe")
+    e1.record()
+    torch.cuda.synchronize()
+    sec = e0.elapsed_time(e1) * 1e-3
+    del buf
+    torch.cuda.empty_cache()
+    return reps * lanes * lines_per_lane / sec
 
 
 def copy_ceiling(dev, gib: float = 2.0, reps: int = 10) -> float:
@@ -294,6 +380,12 @@ def main():
         env.set_rollout_groups(a.rollout_groups)
         iso = {k: max_over_ranks(v) for k, v in ki.items()}  # per launch (one per step)
 
+    # ---------------- steady state: >= 101 steps, staggered episode phases
+    steady = None
+    if not a.env_only and not a.vision and not a.no_steady:
+        steady = steady_state(tr, env, dev, barrier, max_over_ranks, total_envs)
+        steady["vs_value"] = steady["env_steps_per_s"] / steps_per_s
+
     # ---------------- PPO update phase + one full iteration
     upd = {}
     if not a.no_update and not a.env_only:
@@ -313,9 +405,20 @@ def main():
         torch.cuda.synchronize()
         barrier()
         di = max_over_ranks(time.perf_counter() - t0)
+        if world > 1:  # the per-minibatch flat-gradient all-reduce alone (included in the update above)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n_upd):
+                dist.all_reduce(tr.flat_grad)
+            torch.cuda.synchronize()
+            dar = max_over_ranks(time.perf_counter() - t0)
         upd = {"ppo_updates_per_s": n_upd / du, "ppo_update_ms": 1000 * du / n_upd,
                "minibatch_size_per_gpu": tr.minibatch_size, "update_minibatches_timed": n_upd,
                "train_env_steps_per_s": total_envs * T / di, "train_iteration_s": di}
+        if world > 1:
+            upd["update_allreduce_ms"] = 1000 * dar / n_upd
+            upd["update_allreduce_bytes"] = 4 * tr.flat_grad.numel()
         if tr.fused_update:
             # MLP forward + backward of both heads: 28,224 MACs per sample
             # (DESIGN.md §3); whole minibatch step (grad + reduce + clip/Adam + epoch overheads)
@@ -385,6 +488,25 @@ def main():
         env_ms2 = sum(max_over_ranks(v) for v in k2.values())
         other = {"step_mode": other_mode, "env_steps_per_s": total_envs * K / d2, "ms_per_step": 1000 * d2 / K,
                  "env_kernels_ms": k2, "env_only_kernel_steps_per_s": total_envs / (env_ms2 * 1e-3)}
+        if other_mode == "incremental" and rank == 0:
+            from ppo_radiotherapy_amd import _lib
+
+            bl, tl = incremental_transactions(env2, lib)
+            ceil = random_rmw_ceiling(dev, _lib.load(), a.envs * V)
+            sps = a.envs * K / d2  # this rank's env steps/s
+            ach_lines = sps * bl
+            ach_bytes = sps * 128 * (2 * bl + tl)
+            other["roofline"] = {
+                "bound": "random-line RMW (latency/transactions)", "kernel": "k_rollout_policy",
+                "model": "per env-step: the march read-modify-writes the distinct 128-B dose lines its splats "
+                         "touch (2 x 128 B each), the finish reads the tumour's lines (128 B each)",
+                "beam_lines_per_step": bl, "tumour_lines_per_step": tl,
+                "bytes_per_env_step": 128 * (2 * bl + tl), "achieved_GBps": ach_bytes / 1e9,
+                "frac_of_hbm_peak": ach_bytes / HBM_PEAK,
+                "line_rmw_per_s": ach_lines, "probe_line_rmw_per_s": ceil,
+                "probe": "rt_probe_random_rmw: 2^18 lanes x 64 random lines (one float per lane and line, 4 in "
+                         "flight) over a buffer the size of the dose array",
+                "frac": ach_lines / ceil}
         if not a.no_update:
             barrier()
             t0 = time.perf_counter()
@@ -425,13 +547,15 @@ def main():
                       "parallelism": f"dp{world}"},
            "env_only_kernel_steps_per_s": total_envs / (env_ms * 1e-3)}
     out.update(upd)
+    if steady is not None:
+        out["steady_state"] = steady
     out["step_mode"] = a.step_mode
     out["rollout_groups"] = a.rollout_groups if a.step_mode == "dense" and not a.vision else 1
     if other is not None:
         out["other_step_mode"] = other
     out["roofline"] = roof
     if rank == 0 and world == 1 and not a.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(a.grid, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     env.close()

@@ -174,6 +174,21 @@ int rt_debug_beam(const int32_t grid[3], int32_t m, const double* pos_d, const d
 int rt_debug_pose(const int32_t grid[3], int32_t m, const double* pos_d, const double* dir_d,
                   const float* action_d, double* out_d, void* stream);
 
+/* The beam each env applied on its last step (draw_line.py:4-102 called
+ * from environment.py:107-110 on the post-update pose): raw splats in march
+ * order as rt_debug_beam -- idx_d i32[N,cap] C-order flat voxel indices,
+ * w_d f32[N,cap] weights (a voxel can appear twice; the env adds both),
+ * count_d i32[N] (0: the env's last call was its reset, no beam applied;
+ * > cap: truncated).  Replaces reading `beam_voxels(...)` back in a debugger. */
+int rt_env_beam_list(rt_env* env, int32_t cap, int32_t* idx_d, float* w_d, int32_t* count_d, void* stream);
+
+/* Measurement hook (bench.py): `lanes` threads each read-modify-write
+ * `lines_per_lane` pseudo-random 128-B lines of buf_d (one float per line,
+ * 4 in flight) -- the access shape of the incremental step's march -- so the
+ * caller can time the random-line RMW ceiling of the device. */
+int rt_probe_random_rmw(float* buf_d, int64_t n_floats, int32_t lanes, int32_t lines_per_lane, uint64_t seed,
+                        void* stream);
+
 /* Host-side evaluation of the correctly rounded sin/cos the pose kernel uses
  * for scipy's from_rotvec half angle (no device needed; parity hook). */
 int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h);
@@ -324,6 +339,15 @@ int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_
 int rt_ppo_shuffle(int64_t n, uint64_t key, int64_t* perm_d, void* stream);
 int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
                      float* stats_d, float* workspace_d, int64_t workspace_floats, void* stream);
+/* Data-parallel form of rt_ppo_adv_stats (train.py:215-218 over the union
+ * of the ranks' minibatches): rt_ppo_adv_sums writes this rank's per-minibatch
+ * (sum, sum of squares) of adv, f64 sums_d[n_mb][2] (same workspace rule);
+ * the caller all-reduces sums_d (SUM) across ranks, then rt_ppo_adv_finalize
+ * turns it into stats_d[n_mb][2] = (mean, unbiased std) over `count` rows per
+ * minibatch (mb_size x world size). */
+int rt_ppo_adv_sums(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
+                    double* sums_d, float* workspace_d, int64_t workspace_floats, void* stream);
+int rt_ppo_adv_finalize(const double* sums_d, int64_t count, int32_t n_minibatches, float* stats_d, void* stream);
 
 /* ---- C3D feature extractor of the vision agent (networks.py:8-45) ----------
  * One stage = Conv3d(cin, 16, 3, groups) + ReLU + MaxPool3d(2, 2, pool_pad):

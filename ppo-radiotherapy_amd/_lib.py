@@ -33,10 +33,10 @@ EXPORTS = [
     "rt_env_set_next_tumours", "rt_env_dose", "rt_env_dose_index", "rt_env_get_state", "rt_env_set_pose", "rt_env_set_tumours",
     "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
-    "rt_debug_beam", "rt_debug_pose", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
+    "rt_debug_beam", "rt_debug_pose", "rt_env_beam_list", "rt_probe_random_rmw", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
     "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
-    "rt_ppo_shuffle", "rt_ppo_adv_stats",
+    "rt_ppo_shuffle", "rt_ppo_adv_stats", "rt_ppo_adv_sums", "rt_ppo_adv_finalize",
     "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
     "rt_conv_relu_pool_dgrad",
     "rt_last_error", "rt_abi_version",
@@ -147,6 +147,8 @@ def load(build_if_missing: bool = True):
         "rt_env_kernel_timing_read": ([vp, ctypes.POINTER(f64), ctypes.POINTER(i32)], ctypes.c_int),
         "rt_debug_beam": ([ctypes.POINTER(i32), i32, vp, vp, i32, vp, vp, vp, vp], ctypes.c_int),
         "rt_debug_pose": ([ctypes.POINTER(i32), i32, vp, vp, vp, vp, vp], ctypes.c_int),
+        "rt_env_beam_list": ([vp, i32, vp, vp, vp, vp], ctypes.c_int),
+        "rt_probe_random_rmw": ([vp, i64, i32, i32, ctypes.c_uint64, vp], ctypes.c_int),
         "rt_host_sincos": ([i32, vp, vp, vp], ctypes.c_int),
         "rt_host_tumour_sum": ([i64, i32, vp, vp, vp], ctypes.c_int),
         "rt_gae": ([i32, i32, vp, vp, vp, vp, vp, f64, f64, vp, vp, vp], ctypes.c_int),
@@ -165,6 +167,8 @@ def load(build_if_missing: bool = True):
                           ctypes.c_int),
         "rt_ppo_shuffle": ([i64, ctypes.c_uint64, vp, vp], ctypes.c_int),
         "rt_ppo_adv_stats": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
+        "rt_ppo_adv_sums": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
+        "rt_ppo_adv_finalize": ([vp, i64, i32, vp, vp], ctypes.c_int),
         "rt_conv_out_dims": ([ctypes.POINTER(RtConvLayer), ctypes.POINTER(i32)], ctypes.c_int),
         "rt_conv_relu_pool_fwd": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_conv_wgrad_workspace_floats": ([ctypes.POINTER(RtConvLayer), i32], i64),

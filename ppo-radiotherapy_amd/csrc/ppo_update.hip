@@ -1062,6 +1062,31 @@ __global__ __launch_bounds__(256) void k_adv_stats(const double* part, int mb, i
     stats[2 * i + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
 }
 
+// Data-parallel split of k_adv_stats: the ranks' (sum, sum of squares) per
+// minibatch (fixed-order sums of the parts) are all-reduced by the caller,
+// then turned into (mean, unbiased std) over the global minibatch size.
+__global__ __launch_bounds__(256) void k_adv_sums(const double* part, int n_mb, double* sums) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_mb) return;
+    double S = 0.0, Q = 0.0;
+    for (int k = 0; k < kAdvParts; ++k) {
+        S += part[((size_t)i * kAdvParts + k) * 2];
+        Q += part[((size_t)i * kAdvParts + k) * 2 + 1];
+    }
+    sums[2 * i] = S;
+    sums[2 * i + 1] = Q;
+}
+
+__global__ __launch_bounds__(256) void k_adv_finalize(const double* sums, int64_t count, int n_mb, float* stats) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_mb) return;
+    const double S = sums[2 * i], Q = sums[2 * i + 1];
+    const double mean = S / (double)count;
+    const double var = count > 1 ? (Q - S * mean) / (double)(count - 1) : 0.0;
+    stats[2 * i] = (float)mean;
+    stats[2 * i + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
+}
+
 // RT_PPO_GRAD_KERNEL=valu selects the VALU kernel (A/B comparisons); default MFMA
 bool rt_ppo_use_mfma() {
     static const int v = [] {
@@ -1235,6 +1260,33 @@ extern "C" int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32
     hipLaunchKernelGGL(k_adv_partial, dim3(kAdvParts, n_minibatches), dim3(kAdvThreads), 0, st, adv_d, perm_d,
                        mb_size, part);
     hipLaunchKernelGGL(k_adv_stats, dim3((n_minibatches + 255) / 256), dim3(256), 0, st, part, mb_size,
+                       n_minibatches, stats_d);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_ppo_adv_sums(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
+                               double* sums_d, float* workspace_d, int64_t workspace_floats, void* stream) {
+    if (!adv_d || !perm_d || !sums_d || !workspace_d || mb_size < 1 || n_minibatches < 1 ||
+        workspace_floats < (int64_t)n_minibatches * kAdvParts * 4)
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_adv_sums: bad argument");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    double* part = reinterpret_cast<double*>(workspace_d);
+    hipLaunchKernelGGL(k_adv_partial, dim3(kAdvParts, n_minibatches), dim3(kAdvThreads), 0, st, adv_d, perm_d,
+                       mb_size, part);
+    hipLaunchKernelGGL(k_adv_sums, dim3((n_minibatches + 255) / 256), dim3(256), 0, st, part, n_minibatches, sums_d);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_ppo_adv_finalize(const double* sums_d, int64_t count, int32_t n_minibatches, float* stats_d,
+                                   void* stream) {
+    if (!sums_d || !stats_d || count < 1 || n_minibatches < 1)
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_adv_finalize: bad argument");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_adv_finalize, dim3((n_minibatches + 255) / 256), dim3(256), 0, st, sums_d, count,
                        n_minibatches, stats_d);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));

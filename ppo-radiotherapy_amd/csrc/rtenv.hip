@@ -1327,17 +1327,44 @@ __global__ __launch_bounds__(1024) void k_rollout_policy(RolloutArgs A) {
 // ---------------------------------------------------------------------------
 // Parity hooks
 // ---------------------------------------------------------------------------
-__global__ void k_debug_beam(Geom G, int m, const double* pos, const double* dir, int cap,
-                             int32_t* idx_out, float* w_out, int32_t* count) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= m) return;
-    BeamSetup s{};
-    double p[3] = {pos[c * 3], pos[c * 3 + 1], pos[c * 3 + 2]};
-    double d[3] = {dir[c * 3], dir[c * 3 + 1], dir[c * 3 + 2]};
-    if (beam_setup(G.g, p, d, s) < 0) {
-        count[c] = -1;
-        return;
+// Random-line read-modify-write probe: the access shape of the incremental
+// step's march (each lane read-modify-writes dose floats of its own 128-B
+// line, lines scattered over a multi-GiB dose array).  Every lane RMWs
+// `lines_per_lane` random lines of buf (one float each, 4 in flight); bench.py
+// divides lines by time for the random-line ceiling the incremental step's
+// transaction model is priced against.
+__device__ __forceinline__ uint64_t probe_hash(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+__global__ __launch_bounds__(256) void k_probe_rmw(float* buf, int64_t n_lines, int lines_per_lane, uint64_t seed) {
+    const uint64_t lane = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    for (int i = 0; i < lines_per_lane; i += 4) {
+        float* p[4];
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t h = probe_hash(seed ^ (lane * 0x9E3779B97F4A7C15ull + (uint64_t)(i + u)));
+            p[u] = buf + (h % (uint64_t)n_lines) * 32 + (h >> 59);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *p[u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) *p[u] = v[u] + 1.0f;
     }
+}
+
+// beam_voxels (draw_line.py:4-102) as raw splats in march order; -1 for the
+// reference's ValueError (direction norm < eps).
+__device__ int emit_beam_list(const Geom& G, const double p[3], const double d[3], int cap, int32_t* idx_row,
+                              float* w_row) {
+    BeamSetup s{};
+    if (beam_setup(G.g, p, d, s) < 0) return -1;
     int n = 0;
     float y = s.intery0, z = s.interz0;
     for (int k = 0; k < s.niter; ++k) {
@@ -1347,15 +1374,41 @@ __global__ void k_debug_beam(Geom G, int m, const double* pos, const double* dir
         for (int i = 0; i < 4; ++i) {
             if (ii[i] < 0) continue;
             if (n < cap) {
-                idx_out[(size_t)c * cap + n] = ii[i];
-                w_out[(size_t)c * cap + n] = ww[i];
+                idx_row[n] = ii[i];
+                w_row[n] = ww[i];
             }
             ++n;
         }
         y = y + s.sgy;
         z = z + s.sgz;
     }
-    count[c] = n;
+    return n;
+}
+
+__global__ void k_debug_beam(Geom G, int m, const double* pos, const double* dir, int cap,
+                             int32_t* idx_out, float* w_out, int32_t* count) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= m) return;
+    double p[3] = {pos[c * 3], pos[c * 3 + 1], pos[c * 3 + 2]};
+    double d[3] = {dir[c * 3], dir[c * 3 + 1], dir[c * 3 + 2]};
+    count[c] = emit_beam_list(G, p, d, cap, idx_out + (size_t)c * cap, w_out + (size_t)c * cap);
+}
+
+// The beam each env applied on its last step (environment.py:107-110 adds
+// beam_voxels(pos, dir) of the post-update pose, which is the pose the env
+// holds now); an env whose last call was a reset (t = 0) applied none.
+__global__ void k_env_beam_list(Geom G, int n_env, const double* pose, const int32_t* t, int cap,
+                                int32_t* idx_out, float* w_out, int32_t* count) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_env) return;
+    if (t[e] == 0) {
+        count[e] = 0;
+        return;
+    }
+    const double* q = pose + (size_t)e * 6;
+    double p[3] = {q[0], q[1], q[2]};
+    double d[3] = {q[3], q[4], q[5]};
+    count[e] = emit_beam_list(G, p, d, cap, idx_out + (size_t)e * cap, w_out + (size_t)e * cap);
 }
 
 __global__ void k_debug_pose(Geom G, Consts C, int m, const double* pos, const double* dir,
@@ -2353,6 +2406,24 @@ int rt_debug_beam(const int32_t grid[3], int32_t m, const double* pos_d, const d
     hipLaunchKernelGGL(k_debug_beam, dim3((m + 63) / 64), dim3(64), 0, as_stream(stream), G, m, pos_d, dir_d,
                        cap, idx_d, w_d, count_d);
     RT_LAUNCH_CHECK("k_debug_beam");
+    return RT_OK;
+}
+
+int rt_probe_random_rmw(float* buf_d, int64_t n_floats, int32_t lanes, int32_t lines_per_lane, uint64_t seed,
+                        void* stream) {
+    if (!buf_d || n_floats < 32 || lanes < 256 || lanes % 256 || lines_per_lane < 4 || lines_per_lane % 4)
+        return fail(RT_EINVAL, "bad argument");
+    hipLaunchKernelGGL(k_probe_rmw, dim3(lanes / 256), dim3(256), 0, as_stream(stream), buf_d, n_floats / 32,
+                       lines_per_lane, seed);
+    RT_LAUNCH_CHECK("k_probe_rmw");
+    return RT_OK;
+}
+
+int rt_env_beam_list(rt_env* env, int32_t cap, int32_t* idx_d, float* w_d, int32_t* count_d, void* stream) {
+    if (!env || cap < 0 || !count_d || (cap > 0 && (!idx_d || !w_d))) return fail(RT_EINVAL, "bad argument");
+    hipLaunchKernelGGL(k_env_beam_list, dim3((env->N + 63) / 64), dim3(64), 0, as_stream(stream), env->G, env->N,
+                       env->st.pose, env->st.t, cap, idx_d, w_d, count_d);
+    RT_LAUNCH_CHECK("k_env_beam_list");
     return RT_OK;
 }
 

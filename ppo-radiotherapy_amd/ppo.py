@@ -133,6 +133,7 @@ class PPOTrainer:
         self.optimizer = torch.optim.Adam(self.params, lr=lr, eps=1e-5,
                                           foreach=self.device.type == "cuda", capturable=self.use_graphs)
         self.max_minibatches = 0  # >0: stop the update after this many minibatch steps (benchmarks)
+        self.record_perms = None  # a list: the fused update appends each epoch's permutation (tests)
         # fused rollout policy step (rt_policy_sample): the visionless 64-wide
         # MLP agent on the HIP env; otherwise the torch path below
         self.fused_policy = (bool(getattr(cfg, "fused_policy", True)) and self.device.type == "cuda"
@@ -167,6 +168,7 @@ class PPOTrainer:
             self._norm_ws = torch.empty(256, **kw)
             self._perm_buf = torch.empty(self.batch_size, dtype=torch.int64, **kw)
             self._adv_stats_buf = torch.empty((self.batch_size // self.minibatch_size, 2), **kw)
+            self._adv_sums = torch.empty((self.batch_size // self.minibatch_size, 2), dtype=torch.float64, **kw)
             # epoch shuffle keys: a host generator seeded from the trainer's seed and rank
             self._host_gen = torch.Generator().manual_seed(int(getattr(cfg, "seed", 0)) * 7919 + 104729 * rank + 17)
         self.next_obs = None
@@ -456,10 +458,20 @@ class PPOTrainer:
         key = int(torch.randint(0, 2 ** 62, (1,), generator=self._host_gen).item())
         perm = self._perm_buf
         _lib.check(L.rt_ppo_shuffle(self.batch_size, key, perm.data_ptr(), stream), "rt_ppo_shuffle")
+        if self.record_perms is not None:  # test hook: the epochs' minibatch rows
+            self.record_perms.append(perm.clone())
         if not self.cfg.norm_adv:
             return perm, None
         if self.world > 1:
-            return perm, self._epoch_adv_stats(self._b_adv, perm).contiguous()
+            # this rank's (sum, sum of squares) per minibatch -> ONE all-reduce
+            # of [n_mb, 2] f64 -> global (mean, std) over mbs x world rows
+            _lib.check(L.rt_ppo_adv_sums(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, n_mb,
+                                         self._adv_sums.data_ptr(), self._ws.data_ptr(), self._ws.numel(), stream),
+                       "rt_ppo_adv_sums")
+            dist.all_reduce(self._adv_sums)
+            _lib.check(L.rt_ppo_adv_finalize(self._adv_sums.data_ptr(), self.minibatch_size * self.world, n_mb,
+                                             self._adv_stats_buf.data_ptr(), stream), "rt_ppo_adv_finalize")
+            return perm, self._adv_stats_buf
         _lib.check(L.rt_ppo_adv_stats(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, n_mb,
                                       self._adv_stats_buf.data_ptr(), self._ws.data_ptr(), self._ws.numel(),
                                       stream), "rt_ppo_adv_stats")

@@ -33,6 +33,13 @@ ACTION_SIZE = 6
 MAX_TIME_STEPS = 100
 
 
+def _device_array(x, dtype, device) -> torch.Tensor:
+    """A contiguous device tensor of `x` (array-like or tensor, any device)."""
+    if torch.is_tensor(x):
+        return x.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.asarray(x), dtype=dtype, device=device)
+
+
 class RadiotherapyVecEnv:
     metadata = {"render_modes": ["human"], "render_fps": 30, "autoreset_mode": "NextStep"}
 
@@ -101,8 +108,8 @@ class RadiotherapyVecEnv:
         options = options or {}
         ids = options.get("tumour_ids")
         mask = options.get("mask")
-        ids_t = None if ids is None else torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
-        mask_t = None if mask is None else torch.as_tensor(np.asarray(mask), dtype=torch.uint8, device=self.device)
+        ids_t = None if ids is None else _device_array(ids, torch.int32, self.device)
+        mask_t = None if mask is None else _device_array(mask, torch.uint8, self.device)
         _lib.check(self._L.rt_env_reset(self._h, _lib.ptr(mask_t), _lib.ptr(ids_t), _lib.ptr(self.obs),
                                         _lib.stream_handle()), "rt_env_reset")
         self._episode_start.fill_(time.perf_counter())
@@ -177,6 +184,21 @@ class RadiotherapyVecEnv:
         _lib.check(self._L.rt_env_get_state(self._h, _lib.ptr(pose), _lib.ptr(t), _lib.ptr(tum),
                                             _lib.stream_handle()), "rt_env_get_state")
         return pose, t, tum
+
+    def beam_list(self, cap: int | None = None):
+        """The beam each env applied on its last step (rt_env_beam_list;
+        draw_line.py:4-102 from environment.py:107-110): raw splats in march
+        order, (idx i32 [N, cap] C-order flat voxel indices, w f32 [N, cap],
+        count i32 [N]); count 0 = the env's last call was its reset."""
+        if cap is None:
+            cap = 4 * (int(max(self.grid)) + 2)  # <= 4 splats per march iteration
+        N = self.num_envs
+        idx = torch.zeros((N, cap), dtype=torch.int32, device=self.device)
+        w = torch.zeros((N, cap), dtype=torch.float32, device=self.device)
+        cnt = torch.zeros(N, dtype=torch.int32, device=self.device)
+        _lib.check(self._L.rt_env_beam_list(self._h, int(cap), _lib.ptr(idx), _lib.ptr(w), _lib.ptr(cnt),
+                                            _lib.stream_handle()), "rt_env_beam_list")
+        return idx, w, cnt
 
     def set_pose(self, pose: torch.Tensor):
         p = pose.to(device=self.device, dtype=torch.float64).contiguous()

@@ -292,3 +292,39 @@ def test_incremental_equals_dense_over_resets(dev):
     assert torch.equal(d.dose(), i.dose())
     d.close()
     i.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_env_beam_list_is_the_applied_beam(dev, mode):
+    """rt_env_beam_list returns the beam each env applied on its last step:
+    dose_after == clip(dose_before + fl32(beam * 0.1f), 0, 1) on its voxels
+    and unchanged elsewhere (environment.py:107-110), count 0 after resets."""
+    lib = assets.synthetic_library((64, 64, 64), 64, 0)
+    N = 48
+    env = _vec_env(N, lib, seed=3, step_mode=mode)
+    env.reset()
+    g = torch.Generator(device=dev).manual_seed(4)
+    _, _, cnt = env.beam_list()
+    assert int(cnt.abs().sum()) == 0  # nothing applied yet
+    V = lib.V
+    for t in range(104):  # crosses the t = 100 truncation and its autoreset
+        before = env.dose().reshape(N, V).cpu().numpy()
+        a = torch.rand((N, 6), device=dev, generator=g) * 2.4 - 1.2
+        _, _, _, _, infos = env.step(a)
+        idx, w, cnt = env.beam_list()
+        after = env.dose().reshape(N, V).cpu().numpy()
+        stepped = infos["_reward_components"].cpu().numpy()
+        idx, w, cnt = idx.cpu().numpy(), w.cpu().numpy(), cnt.cpu().numpy()
+        if t % 13 != 0 and t < 99:
+            continue
+        for e in range(N):
+            if not stepped[e]:
+                assert cnt[e] == 0 and not after[e].any()
+                continue
+            assert 0 < cnt[e] <= idx.shape[1] or cnt[e] == 0
+            beam = np.zeros(V, np.float32)
+            for i in range(cnt[e]):
+                beam[idx[e, i]] = np.float32(beam[idx[e, i]] + w[e, i])
+            want = np.clip(before[e] + beam * np.float32(0.1), np.float32(0), np.float32(1))
+            np.testing.assert_array_equal(after[e].view(np.uint32), want.view(np.uint32), err_msg=f"t {t} env {e}")
+    env.close()
