@@ -180,6 +180,8 @@ def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int =
         env.reset(options={"mask": (e_idx % 100) == k})
         tr.rollout_steps(k % T, 1)
     resets = torch.zeros((), dtype=torch.int64, device=dev)
+    K = calls * T
+    env.kernel_timing(2 * K)
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
@@ -189,8 +191,10 @@ def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int =
     torch.cuda.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
-    K = calls * T
+    kms, kcalls = env.kernel_timing_read()
+    env.kernel_timing(0)
     return {"steps": K, "ms_per_step": 1000 * dt / K, "env_steps_per_s": total_envs * K / dt,
+            "kernel_ms_per_step": {k: v * kcalls / K for k, v in kms.items()},
             "autoresets_in_window": int(resets.item()),
             "episode_phase": "staggered uniformly over the 100-step episode (masked resets in a 100-step pre-roll)"}
 

@@ -135,6 +135,7 @@ struct EnvState {
     int32_t* ep_len;
     int32_t* next_tumour;
     BeamSetup* setup;
+    uint8_t* mode_b;      // [N] setup[e].mode as a byte (k_dense_persist scans a group's modes)
     int32_t* lung_cnt;    // incremental mode: # lung voxels with dose > threshold
     double* lung_sum;     // incremental mode: sum of dose over lung voxels
 };
@@ -514,15 +515,18 @@ __device__ void beam_env(const BeamParams& P, int e, int lane, const float* act)
         RT_STAMP(e, 2);
         s = pose_step(P, e, act);
         P.st.setup[e] = s;
+        P.st.mode_b[e] = (uint8_t)s.mode;
         RT_STAMP(e, 3);
     }
     if (lane == 0) RT_STAMP(e, 12);
     const int mode = rfl_i(s.mode);
     if (P.incremental && mode == MODE_RESET) {
         // reset_dose (environment.py:104) for the incremental step: k_dense is not run
-        float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
+        typedef float nf4 __attribute__((ext_vector_type(4)));
+        nf4* d4 = reinterpret_cast<nf4*>(P.st.dose + (size_t)e * P.G.Vpad);
+        const nf4 z = {0.f, 0.f, 0.f, 0.f};
         const int nvec = P.G.Vpad >> 2;
-        for (int q = lane; q < nvec; q += 64) d4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = lane; q < nvec; q += 64) __builtin_nontemporal_store(z, d4 + q);
         if (lane == 0) {
             P.st.lung_cnt[e] = 0;
             P.st.lung_sum[e] = 0.0;
@@ -645,7 +649,6 @@ struct DenseParams {
     int32_t slices;
     int32_t vec_per_slice; // float4 per slice (of the streamed segment), multiple of 256
     int32_t lung_n;        // lung-first rows: # lung voxels (the segment k_dense streams)
-    int32_t zero_per;      // RESET: float4 of the whole row zeroed per slice
     int32_t e_begin;       // env of blockIdx.y == 0 (env group of the pipelined rollout)
 };
 
@@ -674,16 +677,12 @@ __device__ __forceinline__ float4 load_nt(const float4* p) {
     return make_float4(t.x, t.y, t.z, t.w);
 }
 
+// RESET envs' rows are zeroed by zero_reset_share, not by their slices.
 __device__ __forceinline__ void dense_item(const DenseParams& P, int sl, int e) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int mode = P.st.setup[e].mode;
-    if (mode == MODE_NOOP) return;
-    float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
-    if (mode == MODE_RESET) {
-        const int z0 = sl * P.zero_per, z1 = min(z0 + P.zero_per, P.G.Vpad >> 2);
-        for (int q = z0 + tid; q < z1; q += kStepThreads) d4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        return;
-    }
+    if (mode != MODE_STEP) return;
+    const float4* d4 = reinterpret_cast<const float4*>(P.st.dose + (size_t)e * P.G.Vpad);
     const int n = P.lung_n;
     const int q0 = sl * P.vec_per_slice;
     const int q1 = min(q0 + P.vec_per_slice, (n + 3) >> 2);
@@ -735,8 +734,85 @@ __device__ __forceinline__ void dense_item(const DenseParams& P, int sl, int e) 
     __syncthreads();  // s_cnt / s_sum are reused by the next item of a persistent block
 }
 
-__global__ __launch_bounds__(256) void k_dense(DenseParams P) {
-    dense_item(P, blockIdx.x, P.e_begin + blockIdx.y);
+// reset_dose (environment.py:104) of the RESET envs is not done by their own
+// slice blocks/items: a row is 2.7x the bytes of the lung segment a slice
+// streams, so a block that drew a reset env's slice ran long and, near the
+// end of a launch, set its length.  The zeroing is spread instead: blocks
+// count the group's resets (one mode byte per env, block prefix sum), take an
+// equal share of the concatenated reset rows [0, R x row) and locate the
+// reset envs of that share by rank.
+__device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int w = 0; w < kStepThreads / 64; ++w) {
+        base += w < wid ? s_w[w] : 0;
+        tot += s_w[w];
+    }
+    *total = tot;
+    __syncthreads();  // s_w reused by the caller's next scan
+    return base + x - v;
+}
+
+constexpr int kZeroBlocks = 256;  // grid k_dense: blocks that zero RESET rows (one per CU)
+
+// zero_reset_share: part `part` of n_parts of the zeroing of the RESET rows
+// among envs [e_begin, e_begin + n_env) (reset_dose, environment.py:104).
+__device__ void zero_reset_share(const DenseParams& P, int n_env, int part, int n_parts) {
+    __shared__ int s_w[kStepThreads / 64];
+    __shared__ int s_env;
+    const int tid = threadIdx.x;
+    const int per = (n_env + kStepThreads - 1) / kStepThreads;
+    const int a0 = min(tid * per, n_env), a1 = min(a0 + per, n_env);
+    const uint8_t* mb = P.st.mode_b + P.e_begin;
+    int c = 0;
+    for (int e = a0; e < a1; ++e) c += mb[e] == MODE_RESET;
+    int R;
+    const int pre = block_excl_scan(c, s_w, &R);
+    if (R == 0) return;  // block-uniform
+    const int64_t rowv = P.G.Vpad >> 2;  // float4 per row
+    const int64_t tot = (int64_t)R * rowv;
+    const int64_t share = ((tot + n_parts - 1) / n_parts + 63) / 64 * 64;
+    const int64_t z0 = (int64_t)part * share, z1 = min(z0 + share, tot);
+    if (z0 >= z1) return;
+    for (int64_t r = z0 / rowv; r <= (z1 - 1) / rowv; ++r) {
+        if (r >= pre && r < pre + c) {  // this thread's env range holds reset rank r
+            int k = (int)(r - pre);
+            for (int e = a0; e < a1; ++e) {
+                if (mb[e] == MODE_RESET && k-- == 0) {
+                    s_env = P.e_begin + e;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        const int e = s_env;
+        __syncthreads();
+        const int64_t q0 = max(z0, r * rowv) - r * rowv, q1 = min(z1, (r + 1) * rowv) - r * rowv;
+        typedef float nf4 __attribute__((ext_vector_type(4)));
+        nf4* d4 = reinterpret_cast<nf4*>(P.st.dose + (size_t)e * P.G.Vpad);
+        const nf4 z = {0.f, 0.f, 0.f, 0.f};
+        for (int64_t q = q0 + tid; q < q1; q += kStepThreads) __builtin_nontemporal_store(z, d4 + q);
+    }
+}
+
+// Grid k_dense: the first zero_rows rows of blocks (dispatched first) zero
+// the RESET envs' rows in equal shares; the env blocks skip RESET envs.  (A
+// RESET env's own slices used to zero its row: 2.7x a slice's bytes, and such
+// a block dispatched near the end of the grid set the launch's tail.)
+__global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env, int zero_rows) {
+    if ((int)blockIdx.y < zero_rows) {
+        zero_reset_share(P, n_env, blockIdx.y * gridDim.x + blockIdx.x, zero_rows * gridDim.x);
+        return;
+    }
+    dense_item(P, blockIdx.x, P.e_begin + blockIdx.y - zero_rows);
 }
 
 // k_dense with a fixed grid (a few blocks per CU) looping over the (env,
@@ -746,7 +822,9 @@ __global__ __launch_bounds__(256) void k_dense(DenseParams P) {
 // tail), and 6 blocks x 4 waves per CU keep ~16 MB of loads in flight.
 __global__ __launch_bounds__(256) void k_dense_persist(DenseParams P, int n_env) {
     const int n_items = n_env * P.slices;
-    for (int it = blockIdx.x; it < n_items; it += gridDim.x) dense_item(P, it % P.slices, P.e_begin + it / P.slices);
+    for (int it = blockIdx.x; it < n_items; it += gridDim.x)
+        dense_item(P, it % P.slices, P.e_begin + it / P.slices);
+    zero_reset_share(P, n_env, blockIdx.x, gridDim.x);
 }
 
 // Store 4 consecutive voxels [v0, v0+4) of one obs channel row.
@@ -1560,7 +1638,6 @@ struct rt_env {
     int vec_per_slice = 0;   // float4 per slice
     int lung_first = 0;      // dose rows lung-first (dense visionless), else C order
     int lung_n = 0;          // lung voxels (the lung-first segment)
-    int zero_per = 0;        // k_dense RESET: float4 zeroed per slice
     int32_t* dose_pos_d = nullptr;  // voxel -> row position (lung_first)
     size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
     int finish_wave_lds = 0; // bytes per wave
@@ -1859,7 +1936,6 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     const int svec = env->lung_first ? std::max(1, (env->lung_n + 3) / 4) : nvec;
     env->vec_per_slice = std::min(svec, kSliceVec);
     env->slices = (svec + env->vec_per_slice - 1) / env->vec_per_slice;
-    env->zero_per = (nvec + env->slices - 1) / env->slices;
     const int maxdim = std::max(G.g[0], std::max(G.g[1], G.g[2]));
     env->view_hash_mask = env->visionless ? 0u : next_pow2((uint32_t)(8 * (maxdim + 2))) - 1;
     // per wave: plan slots (2 n floats), then either the plan's operands and
@@ -1935,6 +2011,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         (rc = dev_alloc(env, &st.flags, N)) || (rc = dev_alloc(env, &st.episode, N)) ||
         (rc = dev_alloc(env, &st.ep_return, N)) || (rc = dev_alloc(env, &st.ep_len, N)) ||
         (rc = dev_alloc(env, &st.next_tumour, N)) || (rc = dev_alloc(env, &st.setup, N)) ||
+        (rc = dev_alloc(env, &st.mode_b, N)) ||
         (rc = dev_alloc(env, &env->part_cnt, (size_t)N * env->slices)) ||
         (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices)) ||
         (rc = dev_alloc(env, &st.lung_cnt, N)) || (rc = dev_alloc(env, &st.lung_sum, N)) ||
@@ -1960,7 +2037,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         h2d(st.flags, ones.data(), N * 4) || h2d(st.next_tumour, neg.data(), N * 4) ||
         h2d(st.pose, pose0.data(), pose0.size() * 8) ||
         hipMemset(st.dose, 0, (size_t)N * G.Vpad * 4) || hipMemset(st.t, 0, N * 4) ||
-        hipMemset(st.tumour, 0, N * 4) || hipMemset(st.episode, 0, N * 4) ||
+        hipMemset(st.tumour, 0, N * 4) || hipMemset(st.episode, 0, N * 4) || hipMemset(st.mode_b, 0, N) ||
         hipMemset(st.ep_return, 0, N * 8) || hipMemset(st.ep_len, 0, N * 4) ||
         hipMemset(st.lung_cnt, 0, N * 4) || hipMemset(st.lung_sum, 0, N * 8) ||
         hipMemset(st.setup, 0, (size_t)N * sizeof(BeamSetup)) || hipDeviceSynchronize()) {
@@ -2069,7 +2146,6 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
     dp.slices = env->slices;
     dp.vec_per_slice = env->vec_per_slice;
     dp.lung_n = env->lung_n;
-    dp.zero_per = env->zero_per;
     dp.e_begin = e0;
     if (wait_ev) RT_HIP(hipStreamWaitEvent(stream, wait_ev, 0));
     if (ev) (void)hipEventRecord(ev[1], stream);
@@ -2080,7 +2156,8 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
             hipLaunchKernelGGL(k_dense_persist, dim3(persist_bpc * env->num_cu), dim3(kStepThreads), 0, stream, dp,
                                n);
         } else {
-            hipLaunchKernelGGL(k_dense, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dp);
+            const int zrows = (kZeroBlocks + env->slices - 1) / env->slices;
+            hipLaunchKernelGGL(k_dense, dim3(env->slices, n + zrows), dim3(kStepThreads), 0, stream, dp, n, zrows);
         }
         RT_LAUNCH_CHECK("k_dense");
     } else {
