@@ -39,16 +39,29 @@ def make_writer(logdir: str):
         return JsonlWriter(logdir)
 
 
+EPISODE_TAGS = ("charts/episodic_return", "charts/episodic_length", "charts/episodic_tumour_reward",
+                "charts/episodic_lung_reward", "charts/episodic_distance_reward", "charts/episodic_total_reward")
+
+
+def log_episode_steps(writer, rows):
+    """log_episode_statistics (train.py:42-66) at every rollout step where
+    episodes finished (train.py:159-161), at that step's own global_step:
+    rows = IterStats.episode_steps (global_step, n, mean r, mean l, mean
+    tumour / lung / distance / total reward of the finishing step)."""
+    for gs, _, r, l, tum, lung, dist, tot in rows:
+        for tag, v in zip(EPISODE_TAGS, (r, l, tum, lung, dist, tot)):
+            writer.add_scalar(tag, v, gs)
+
+
 def log_iteration(writer, global_step: int, st):
-    """The reference's tag set; episode means cover the episodes that finished
-    during the iteration (the reference writes them per rollout step)."""
-    if st.episodes:
-        writer.add_scalar("charts/episodic_return", st.episodic_return, global_step)
-        writer.add_scalar("charts/episodic_length", st.episodic_length, global_step)
-        writer.add_scalar("charts/episodic_tumour_reward", st.tumour_reward, global_step)
-        writer.add_scalar("charts/episodic_lung_reward", st.lung_reward, global_step)
-        writer.add_scalar("charts/episodic_distance_reward", st.distance_reward, global_step)
-        writer.add_scalar("charts/episodic_total_reward", st.total_reward, global_step)
+    """The reference's tag set: episode statistics per rollout step (as
+    train.py logs them), losses once per iteration (train.py:252-268)."""
+    if st.episode_steps is not None:
+        log_episode_steps(writer, st.episode_steps)
+    elif st.episodes:  # iteration aggregate (a trainer without per-step rows)
+        for tag, v in zip(EPISODE_TAGS, (st.episodic_return, st.episodic_length, st.tumour_reward,
+                                         st.lung_reward, st.distance_reward, st.total_reward)):
+            writer.add_scalar(tag, v, global_step)
     writer.add_scalar("charts/learning_rate", st.learning_rate, global_step)
     writer.add_scalar("losses/value_loss", st.value_loss, global_step)
     writer.add_scalar("losses/policy_loss", st.policy_loss, global_step)

@@ -50,6 +50,20 @@ class IterStats:
     learning_rate: float = float("nan")
     rollout_s: float = 0.0
     update_s: float = 0.0
+    # per rollout step with finished episodes (train.py:159-161 logs at each):
+    # rows (global_step, n, mean r, mean l, mean tumour, lung, distance, total)
+    episode_steps: list = None
+
+
+def episode_step_sums(infos: torch.Tensor) -> torch.Tensor:
+    """[T, 7] per rollout step over the envs whose episode ended there
+    (RecordEpisodeStatistics `_r`, info[RT_INFO_EP_DONE]): count, sums of
+    episode r and l, and of that final step's reward components tumour, lung,
+    distance, total -- what log_episode_statistics averages (train.py:42-66)."""
+    I = infos
+    done = (I[..., 17] > 0.5).double()
+    cols = [I[..., 18], I[..., 19], I[..., 1], I[..., 2], I[..., 3], I[..., 0]]
+    return torch.stack([done.sum(1)] + [(c.double() * done).sum(1) for c in cols], 1)
 
 
 class PPOTrainer:
@@ -645,13 +659,9 @@ class PPOTrainer:
         """One host sync per iteration: episode statistics of the episodes that
         finished during the rollout (train.py:42-66 logs them per step) and the
         last minibatch's losses (train.py:69-88)."""
-        I = self.infos
-        done = I[..., 17] > 0.5
-        vals = torch.stack([done.sum().double(), (I[..., 18] * done).sum().double(),
-                            (I[..., 19] * done).sum().double(), (I[..., 1] * done).sum().double(),
-                            (I[..., 2] * done).sum().double(), (I[..., 3] * done).sum().double(),
-                            (I[..., 0] * done).sum().double()])
-        self._allreduce_(vals, average=False)
+        per_step = episode_step_sums(self.infos)       # [T, 7]
+        self._allreduce_(per_step, average=False)     # global over ranks, per step
+        vals = per_step.sum(0)
         y_pred, y_true = self.values.reshape(-1), self.returns.reshape(-1)
         var_y = y_true.var(unbiased=False)
         ev = torch.where(var_y == 0, torch.tensor(float("nan"), device=y_true.device),
@@ -659,8 +669,16 @@ class PPOTrainer:
         parts = [vals, ev.double().reshape(1)]
         if getattr(self, "_last_stats", None) is not None:
             parts.append(self._last_stats.double())
+        parts.append(per_step.reshape(-1))
         host = torch.cat(parts).cpu().numpy()
+        steps = host[-per_step.numel():].reshape(per_step.shape)
+        host = host[:-per_step.numel()]
         st = IterStats()
+        # the rollout's steps end at global_step; step t of it at gs0 + (t + 1) N_global
+        n_global = self.N * self.world
+        gs0 = self.global_step - self.T * n_global
+        st.episode_steps = [(gs0 + (t + 1) * n_global, int(r[0]), *(r[1:] / r[0]).tolist())
+                            for t, r in enumerate(steps) if r[0] > 0]
         n = int(host[0])
         st.episodes = n
         if n:

@@ -137,3 +137,56 @@ def test_micro_batched_gradient_equals_full_minibatch():
     part = tr._minibatch_loss_backward(mb)
     torch.testing.assert_close(tr.flat_grad, g_full, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(part[[0, 1, 2]], full[[0, 1, 2]], rtol=1e-5, atol=1e-6)
+
+
+class _RecWriter:
+    def __init__(self):
+        self.rows = []
+
+    def add_scalar(self, tag, value, step):
+        self.rows.append((tag, float(value), int(step)))
+
+
+def _reference_log_episode_statistics(writer, global_step, infos):
+    """train.py:42-66, restated (numpy semantics of the reference)."""
+    ep = infos["episode"]
+    done = ep["_r"]
+    writer.add_scalar("charts/episodic_return", np.mean(ep["r"][done]), global_step)
+    writer.add_scalar("charts/episodic_length", np.mean(ep["l"][done]), global_step)
+    rc = infos["reward_components"]
+    for k, tag in (("tumour", "tumour"), ("lung", "lung"), ("distance_to_tumour", "distance"), ("total", "total")):
+        writer.add_scalar(f"charts/episodic_{tag}_reward", np.mean(rc[k][done]), global_step)
+
+
+def test_episode_statistics_logged_per_rollout_step():
+    """logger.log_iteration writes charts/episodic_* at every rollout step
+    where episodes finished, at that step's global_step, with the values
+    train.py:159-161 + log_episode_statistics compute from that step's infos."""
+    from ppo_radiotherapy_amd import logger
+
+    tr = _trainer(16, 3)
+    tr.env.t[:5] = 3  # desynchronise: episodes end at different steps
+    g = torch.Generator().manual_seed(1)
+    for it in (1, 2):
+        tr.rollout()
+        I = tr.infos
+        I[..., 1:4] = torch.rand(I[..., 1:4].shape, generator=g) - 0.5  # distinct reward components
+        tr.compute_gae()
+        st = tr.iteration_stats()
+        mine = _RecWriter()
+        logger.log_episode_steps(mine, st.episode_steps)
+        ref = _RecWriter()
+        gs0 = tr.global_step - tr.T * tr.N
+        for t in range(tr.T):
+            gs = gs0 + (t + 1) * tr.N  # CleanRL: global_step += num_envs before each step
+            row = I[t].double().numpy()
+            done = row[:, 17] > 0.5
+            if not done.any():  # "episode" in infos
+                continue
+            infos = {"episode": {"r": row[:, 18], "l": row[:, 19], "_r": done},
+                     "reward_components": {"total": row[:, 0], "tumour": row[:, 1], "lung": row[:, 2],
+                                           "distance_to_tumour": row[:, 3]}}
+            _reference_log_episode_statistics(ref, gs, infos)
+        assert len(ref.rows) >= 12 and [r[0] for r in mine.rows] == [r[0] for r in ref.rows]
+        assert [r[2] for r in mine.rows] == [r[2] for r in ref.rows]
+        np.testing.assert_allclose([r[1] for r in mine.rows], [r[1] for r in ref.rows], rtol=1e-12, atol=1e-12)
