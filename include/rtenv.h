@@ -133,6 +133,13 @@ int rt_env_step(rt_env* env, const float* actions_d, float* obs_d, float* reward
  * Parity mode: replays the reference's np.random.choice draws. */
 int rt_env_set_next_tumours(rt_env* env, const int32_t* tumour_ids_d, void* stream);
 
+/* Re-key the tumour-sampling stream (gymnasium reset(seed=...); replaces
+ * SyncVectorEnv.reset(seed) -> RadiotherapyEnv.reset(seed), train.py:136,
+ * environment.py:77): later Philox draws use key `seed` and every env's
+ * episode counter restarts at 0 (ordered on `stream`), so the tumour sequence
+ * depends only on (seed, global env id) -- not on the handle's history. */
+int rt_env_reseed(rt_env* env, uint64_t seed, void* stream);
+
 /* State access (device pointers into library-owned memory; valid until
  * rt_env_destroy).  dose is f32[N][dose_stride]; the first D*H*W floats of a
  * row hold the env's dose volume, in C order or -- dense-mode visionless

@@ -25,6 +25,10 @@ DEFAULTS = {
     "grid": None,              # None: the reference grid and assets (67x43x70); else [D,H,W] synthetic
     "tumour_library": "auto",  # auto | reference | synthetic | reference_style
     "n_synthetic_tumours": 1000,
+    # env step formulation: dense = the reference's full-volume
+    # lung reductions every step; incremental = maintained on the touched
+    # voxels (visionless only; same rewards and termination bit for bit)
+    "step_mode": "dense",
     # checkpoint / resume: with every saved .model, a full trainer
     # checkpoint {output_dir}/checkpoints/{run_name}/{exp_name}_{iteration}.ckpt;
     # resume_from: such a file -> the run continues at its iteration + 1

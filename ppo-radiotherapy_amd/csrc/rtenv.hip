@@ -2123,9 +2123,15 @@ FinishParams finish_params(const rt_env* env, float* obs, float* reward, uint8_t
     return fp;
 }
 
-void allow_lds(const void* kernel, size_t bytes) {
-    if (bytes > 64 * 1024)
-        (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+// Raise a kernel's dynamic-LDS limit to the full 160 KiB on its first launch
+// in the process, whatever that launch needs: the limit is per kernel, not per
+// handle, and a later handle (bigger tumour library, vision hash) may need more
+// than 64 KiB.  The limit does not reserve LDS; occupancy follows each launch's
+// actual request.
+void allow_lds(const void* kernel, bool& raised) {
+    if (raised) return;
+    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    raised = true;
 }
 
 // k_dense / k_dense_vis (skipped in incremental mode) then k_finish
@@ -2171,10 +2177,7 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
     fp.e_begin = e0;
     fp.N = e1;
     static bool big_lds = false;
-    if (!big_lds) {
-        allow_lds(reinterpret_cast<const void*>(&k_finish), env->finish_smem);
-        big_lds = true;
-    }
+    allow_lds(reinterpret_cast<const void*>(&k_finish), big_lds);
     hipLaunchKernelGGL(k_finish, dim3((n + fp.wpb - 1) / fp.wpb), dim3(64 * fp.wpb), env->finish_smem, stream, fp);
     RT_LAUNCH_CHECK("k_finish");
     if (ev) (void)hipEventRecord(ev[3], stream);
@@ -2242,10 +2245,7 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* ps, float* obs_d, floa
     const dim3 grid((env->N + Q.wpb - 1) / Q.wpb), block(64 * Q.wpb);
     if (env->incremental) {
         static bool big = false;
-        if (!big) {
-            allow_lds(reinterpret_cast<const void*>(&k_step_policy<true>), env->fused_smem);
-            big = true;
-        }
+        allow_lds(reinterpret_cast<const void*>(&k_step_policy<true>), big);
         hipLaunchKernelGGL(k_step_policy<true>, grid, block, env->fused_smem, s, bp, fp, Q);
         RT_LAUNCH_CHECK("k_step_policy");
         if (ev)
@@ -2253,10 +2253,7 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* ps, float* obs_d, floa
         return RT_OK;
     }
     static bool big = false;
-    if (!big) {
-        allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), env->fused_smem);
-        big = true;
-    }
+    allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), big);
     hipLaunchKernelGGL(k_step_policy<false>, grid, block, env->fused_smem, s, bp, fp, Q);
     RT_LAUNCH_CHECK("k_step_policy");
     return launch_dense_finish(env, obs_d, reward_d, terminated_d, info_d, s, ev);
@@ -2292,10 +2289,7 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
         }
     }
     static bool big = false;
-    if (!big) {
-        allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), env->fused_smem);
-        big = true;
-    }
+    allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), big);
     PolicyStepParams Q{};
     for (int i = 0; i < rtpol::kTensors; ++i) {
         if (!ps->params[i]) return fail(RT_EINVAL, "rt_env_rollout_policy: NULL parameter");
@@ -2397,10 +2391,7 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d,
     fp.gscratch = env->gscratch;
     fp.gscratch_stride = 2 * (int64_t)env->max_tvox;
     static bool big = false;
-    if (!big) {
-        allow_lds(reinterpret_cast<const void*>(&k_rollout_policy), env->rollout_smem);
-        big = true;
-    }
+    allow_lds(reinterpret_cast<const void*>(&k_rollout_policy), big);
     const dim3 grid((env->N + Q.wpb - 1) / Q.wpb), block(64 * Q.wpb);
     RolloutArgs A{bp, fp, R};
     hipLaunchKernelGGL(k_rollout_policy, grid, block, env->rollout_smem, s, A);
@@ -2446,6 +2437,15 @@ int rt_env_set_next_tumours(rt_env* env, const int32_t* ids_d, void* stream) {
     hipLaunchKernelGGL(k_set_next, dim3((env->N + 255) / 256), dim3(256), 0, as_stream(stream), env->st,
                        env->N, ids_d);
     RT_LAUNCH_CHECK("k_set_next");
+    return RT_OK;
+}
+
+int rt_env_reseed(rt_env* env, uint64_t seed, void* stream) {
+    if (!env) return fail(RT_EINVAL, "NULL argument");
+    // launches already queued captured the old key in their parameters; the
+    // counters restart on the caller's stream, in order with them
+    RT_HIP(hipMemsetAsync(env->st.episode, 0, (size_t)env->N * sizeof(uint32_t), as_stream(stream)));
+    env->seed = seed;
     return RT_OK;
 }
 

@@ -110,7 +110,7 @@ class PPOTrainer:
         # fused HIP update (rt_ppo_update: loss + backward + clip + Adam in 3
         # kernels per minibatch) for the visionless 64-wide agent
         self.fused_update = (bool(getattr(cfg, "fused_update", True)) and self.device.type == "cuda"
-                             and not bool(getattr(cfg, "cuda_graphs", False)) and self._agent_fusable(agent)
+                             and self._agent_fusable(agent)
                              and self.batch_size % self.minibatch_size == 0)
         if self.fused_update:
             # parameters become views of one flat buffer (Adam runs over it)
@@ -133,19 +133,9 @@ class PPOTrainer:
         for p in self.params:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
             off += p.numel()
-        # hipGraph capture of the minibatch step.  OFF by default: on the torch
-        # 2.10/ROCm 7.0 runtime the graph captured from autograd's backward
-        # replays with a missing ordering edge (results depend on timing; exact
-        # under AMD_SERIALIZE_KERNEL=3) -- see DESIGN.md §9, tests/test_gpu_trainer.py
-        self.use_graphs = (bool(getattr(cfg, "cuda_graphs", False)) and self.device.type == "cuda"
-                           and self.batch_size % self.minibatch_size == 0)
-        self._graph_fb = None
-        self._graph_opt = None
         self._last_stats = None
-        # a device-tensor lr lets anneal_lr update a captured optimizer step in place
-        lr = torch.tensor(float(cfg.learning_rate), device=self.device) if self.use_graphs else float(cfg.learning_rate)
-        self.optimizer = torch.optim.Adam(self.params, lr=lr, eps=1e-5,
-                                          foreach=self.device.type == "cuda", capturable=self.use_graphs)
+        self.optimizer = torch.optim.Adam(self.params, lr=float(cfg.learning_rate), eps=1e-5,
+                                          foreach=self.device.type == "cuda")
         self.max_minibatches = 0  # >0: stop the update after this many minibatch steps (benchmarks)
         self.record_perms = None  # a list: the fused update appends each epoch's permutation (tests)
         # fused rollout policy step (rt_policy_sample): the visionless 64-wide
@@ -364,22 +354,6 @@ class PPOTrainer:
         var = (s[1] - s[2] * mean * mean) / (s[2] - 1.0)
         return (adv - mean.float()) / (var.clamp_min(0).sqrt().float() + 1e-8)
 
-    def _epoch_adv_stats(self, b_adv: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
-        """[n_mb, 2] (mean, std) of every minibatch of this epoch: the
-        reference's per-minibatch normalisation (train.py:215-218), global over
-        ranks with ONE all-reduce per epoch."""
-        n_mb = self.batch_size // self.minibatch_size
-        a = b_adv[perm[:n_mb * self.minibatch_size]].view(n_mb, self.minibatch_size)
-        if self.world == 1:
-            return torch.stack([a.mean(1), a.std(1)], 1)
-        d = a.double()
-        s = torch.stack([d.sum(1), (d * d).sum(1), torch.full((n_mb,), float(self.minibatch_size),
-                                                              dtype=torch.float64, device=d.device)], 1)
-        self._allreduce_(s, average=False)
-        mean = s[:, 0] / s[:, 2]
-        var = (s[:, 1] - s[:, 2] * mean * mean) / (s[:, 2] - 1.0)
-        return torch.stack([mean, var.clamp_min(0).sqrt()], 1).float()
-
     def _minibatch_loss_backward(self, mb, adv_mean=None, adv_std=None):
         """train.py:200-246 for one minibatch: losses, then backward into the
         flat gradient bucket.  Returns the logged statistics.  With
@@ -544,8 +518,6 @@ class PPOTrainer:
         """train.py:183-248: update_epochs x num_minibatches optimizer steps."""
         if self.fused_update:
             return self._update_fused()
-        if self.use_graphs:
-            return self._update_graphed()
         self._bind_batch()
         dev = self.device
         stats_sum = torch.zeros(6, device=dev)
@@ -565,93 +537,6 @@ class PPOTrainer:
                 break
         self._last_stats = torch.cat([st[:5], (stats_sum[5] / max(n_mb, 1)).reshape(1)])
         return n_mb
-
-    # ---- hipGraph-captured update -------------------------------------------------
-    def _capture(self):
-        """Capture one minibatch step into HIP graph(s).  world == 1: one graph
-        (loss, backward, clip, Adam); world > 1: two graphs with the RCCL
-        bucket all-reduce between them.  The minibatch indices and advantage
-        statistics are static input buffers refreshed before each replay."""
-        dev = self.device
-        mbs = self.minibatch_size
-        self._bind_batch()
-        self._g_idx = torch.zeros(mbs, dtype=torch.long, device=dev)
-        self._g_adv = torch.zeros(2, device=dev)
-        self._g_adv[1] = 1.0
-        # warm up on a side stream, then restore parameters and optimizer state
-        saved_p = [p.detach().clone() for p in self.params]
-        saved_o = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in
-                   ((i, t) for i, t in enumerate(self._opt_state_tensors()))}
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                self._minibatch_loss_backward(self._g_idx, self._g_adv[0], self._g_adv[1])
-                self._optimizer_step()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        torch.cuda.synchronize(dev)
-        with torch.no_grad():
-            for p, q in zip(self.params, saved_p):
-                p.copy_(q)
-            for i, t in enumerate(self._opt_state_tensors()):
-                t.copy_(saved_o[i])
-        self._graph_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._graph_fb):
-            self._g_stats = self._minibatch_loss_backward(self._g_idx, self._g_adv[0], self._g_adv[1])
-            if self.world == 1:
-                self._optimizer_step()
-        self._graph_opt = None
-        if self.world > 1:
-            self._graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._graph_opt):
-                self._optimizer_step()
-        torch.cuda.synchronize(dev)
-
-    def _opt_state_tensors(self):
-        out = []
-        for p in self.params:
-            st = self.optimizer.state.get(p, {})
-            for k in sorted(st):
-                if torch.is_tensor(st[k]):
-                    out.append(st[k])
-        return out
-
-    def _update_graphed(self):
-        if self._graph_fb is None:
-            # the optimizer state must exist (with device step counters) before capture
-            self._init_capturable_state()
-            self._capture()
-        dev = self.device
-        clip_sum = torch.zeros((), device=dev)
-        n_mb = 0
-        mbs = self.minibatch_size
-        for _ in range(int(self.cfg.update_epochs)):
-            perm = torch.randperm(self.batch_size, device=dev, generator=self.gen)
-            adv_stats = self._epoch_adv_stats(self._b_adv, perm) if self.cfg.norm_adv else None
-            for i, start in enumerate(range(0, self.batch_size - mbs + 1, mbs)):
-                self._g_idx.copy_(perm[start:start + mbs])
-                if adv_stats is not None:
-                    self._g_adv.copy_(adv_stats[i])
-                self._graph_fb.replay()
-                if self._graph_opt is not None:
-                    self._allreduce_(self.flat_grad)
-                    self._graph_opt.replay()
-                clip_sum += self._g_stats[5]
-                n_mb += 1
-        self._last_stats = torch.cat([self._g_stats[:5], (clip_sum / max(n_mb, 1)).reshape(1)])
-        return n_mb
-
-    def _init_capturable_state(self):
-        """Adam(capturable=True) keeps its step counters on the device; run a
-        zero-gradient step once so every state tensor exists (params restored)."""
-        saved = [p.detach().clone() for p in self.params]
-        self.flat_grad.zero_()
-        self.optimizer.step()
-        with torch.no_grad():
-            for p, q in zip(self.params, saved):
-                p.copy_(q)
-            for t in self._opt_state_tensors():
-                t.zero_()
 
     # ------------------------------------------------------------------ stats
     @torch.no_grad()
@@ -695,42 +580,62 @@ class PPOTrainer:
     def anneal(self, iteration: int, num_iterations: int):
         if self.cfg.anneal_lr:
             frac = 1.0 - (iteration - 1.0) / num_iterations
-            lr = self.optimizer.param_groups[0]["lr"]
-            if torch.is_tensor(lr):
-                lr.fill_(frac * float(self.cfg.learning_rate))
-            else:
-                self.optimizer.param_groups[0]["lr"] = frac * float(self.cfg.learning_rate)
+            self.optimizer.param_groups[0]["lr"] = frac * float(self.cfg.learning_rate)
 
     # ------------------------------------------------------------------ checkpoint / resume
+    def _rng_states(self) -> dict:
+        d = {}
+        if self.gen is not None:
+            d["gen"] = self.gen.get_state()
+        if self.fused_update:
+            d["host_gen"] = self._host_gen.get_state()
+        return d
+
+    def _reseed_rngs(self, iteration: int):
+        """Per-rank sampling/shuffle streams derived from (seed, rank,
+        iteration): a resume whose checkpoint has no state for this rank."""
+        base = (int(getattr(self.cfg, "seed", 0)) * 1_000_003 + 7919 * self.rank + 104_729 * iteration) & (2 ** 63 - 1)
+        if self.gen is not None:
+            self.gen.manual_seed(base)
+        if self.fused_update:
+            self._host_gen.manual_seed(base ^ 0x5DEECE66D)
+
     def state_dict(self) -> dict:
         """What a resumed run continues from (the reference saves
         the agent's state_dict only, train.py:270-279): agent, optimizer
         (torch Adam state and, for the fused update, the flat Adam moments and
         step count), iteration, global step, the rollout policy's Philox
-        counter and the sampling/shuffle generator states.  The envs are not
-        part of it: a resumed run starts fresh episodes."""
+        counter and EVERY rank's sampling/shuffle generator states (`rng`,
+        indexed by rank).  With world > 1 this is a collective (all ranks call
+        it; rank 0 writes the file).  The envs are not part of it: a resumed
+        run starts fresh episodes on a re-keyed tumour stream (train.py)."""
         d = {"agent": self.agent.state_dict(), "optimizer": self.optimizer.state_dict(),
              "iteration": self.iteration, "global_step": self.global_step, "policy_counter": self._policy_counter,
              "world": self.world}
-        if self.gen is not None:
-            d["gen"] = self.gen.get_state()
+        mine = self._rng_states()
+        if self.world > 1 and dist.is_available() and dist.is_initialized():
+            ranks = [None] * self.world
+            dist.all_gather_object(ranks, mine)
+        else:
+            ranks = [mine]
+        d["rng"] = ranks
         if self.fused_update:
             d["adam"] = {"exp_avg": self._exp_avg.detach().clone(), "exp_avg_sq": self._exp_avg_sq.detach().clone(),
                          "step": self._adam_step}
-            d["host_gen"] = self._host_gen.get_state()
         return d
 
     def load_state_dict(self, d: dict):
         """Inverse of state_dict (parameters are copied in place, so the flat
-        parameter / gradient buffers of the fused update keep their views)."""
+        parameter / gradient buffers of the fused update keep their views).
+        Each rank takes its own generator states; when the checkpoint holds
+        none for this rank (another world size) they are re-derived from
+        (seed, rank, iteration) so replicas keep distinct streams."""
         with torch.no_grad():
             self.agent.load_state_dict(d["agent"])
         self.optimizer.load_state_dict(d["optimizer"])
         self.iteration = int(d["iteration"])
         self.global_step = int(d["global_step"])
         self._policy_counter = int(d["policy_counter"])
-        if self.gen is not None and "gen" in d and int(d.get("world", 1)) == self.world:
-            self.gen.set_state(d["gen"].cpu())
         if self.fused_update:
             a = d.get("adam")
             if a is None:
@@ -738,8 +643,15 @@ class PPOTrainer:
             self._exp_avg.copy_(a["exp_avg"])
             self._exp_avg_sq.copy_(a["exp_avg_sq"])
             self._adam_step = int(a["step"])
-            if "host_gen" in d and int(d.get("world", 1)) == self.world:
-                self._host_gen.set_state(d["host_gen"].cpu())
+        rng = d.get("rng")
+        if rng is not None and len(rng) == self.world:
+            mine = rng[self.rank]
+            if self.gen is not None and "gen" in mine:
+                self.gen.set_state(mine["gen"].cpu())
+            if self.fused_update and "host_gen" in mine:
+                self._host_gen.set_state(mine["host_gen"].cpu())
+        else:
+            self._reseed_rngs(self.iteration)
 
     def train_iteration(self, iteration: int, num_iterations: int) -> IterStats:
         self.anneal(iteration, num_iterations)

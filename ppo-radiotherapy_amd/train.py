@@ -50,12 +50,23 @@ def _library(cfg):
     return assets.synthetic_library(grid or (64, 64, 64), n, int(cfg.seed))
 
 
+def env_seed(seed: int, rank: int, start_iteration: int) -> int:
+    """Key of a rank's tumour-sampling stream (RadiotherapyVecEnv.reset(seed)).
+    A fresh run keys it seed + rank; a run resumed at iteration k > 1 folds k
+    in, so it does not replay the tumours of iteration 1."""
+    s = seed + rank
+    if start_iteration > 1:
+        s ^= (start_iteration * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    return s & 0xFFFFFFFFFFFFFFFF
+
+
 def train(cfg, writer, device, output_dir=None, run_name=None, rank=0, world=1):
     """train.py:91-282 on the device-resident env."""
     lib = _library(cfg)
     n_local = int(cfg.num_envs) // world
     envs = RadiotherapyVecEnv(n_local, visionless=bool(cfg.visionless), library=lib, device=device,
-                              seed=int(cfg.seed) + rank, env_id_base=rank * n_local)
+                              seed=int(cfg.seed) + rank, env_id_base=rank * n_local,
+                              step_mode=str(cfg.get("step_mode", "dense")))
     obs_shape = envs.single_observation_space.shape
     act_shape = envs.single_action_space.shape
     Model = PPO if cfg.visionless else PPO_3DCNN
@@ -66,7 +77,6 @@ def train(cfg, writer, device, output_dir=None, run_name=None, rank=0, world=1):
     gen = torch.Generator(device=device)
     gen.manual_seed(int(cfg.seed) * 7919 + rank)
     tr = PPOTrainer(cfg, envs, agent, device, rank, world, gen)
-    tr.reset(seed=int(cfg.seed))
     start = 1
     if cfg.get("resume_from"):
         ck = torch.load(cfg.resume_from, map_location=device, weights_only=True)
@@ -74,6 +84,7 @@ def train(cfg, writer, device, output_dir=None, run_name=None, rank=0, world=1):
         start = tr.iteration + 1
         if rank == 0:
             print(f"resumed from {cfg.resume_from} at iteration {start}")
+    tr.reset(seed=env_seed(int(cfg.seed), rank, start))
     iterator = range(start, int(cfg.num_iterations) + 1)
     if cfg.use_tqdm and rank == 0:
         try:
@@ -92,16 +103,19 @@ def train(cfg, writer, device, output_dir=None, run_name=None, rank=0, world=1):
             writer.add_scalar("perf/updates_per_s",
                               int(cfg.update_epochs) * int(cfg.num_minibatches) / max(st.update_s, 1e-9),
                               tr.global_step)
-        if (rank == 0 and cfg.save_model and output_dir is not None and
+        if (cfg.save_model and output_dir is not None and
                 ((cfg.save_frequency_iterations and iteration % cfg.save_frequency_iterations == 0)
                  or iteration == cfg.num_iterations)):
-            os.makedirs(f"{output_dir}/models/{run_name}", exist_ok=True)
-            model_path = f"{output_dir}/models/{run_name}/{cfg.exp_name}_{iteration}.model"
-            torch.save(agent.state_dict(), model_path)
-            print(f"model saved to {model_path}")
-            if cfg.get("save_checkpoint", True):
-                os.makedirs(f"{output_dir}/checkpoints/{run_name}", exist_ok=True)
-                torch.save(tr.state_dict(), f"{output_dir}/checkpoints/{run_name}/{cfg.exp_name}_{iteration}.ckpt")
+            # every rank takes part (the checkpoint gathers all ranks' generator states)
+            ckpt = tr.state_dict() if cfg.get("save_checkpoint", True) else None
+            if rank == 0:
+                os.makedirs(f"{output_dir}/models/{run_name}", exist_ok=True)
+                model_path = f"{output_dir}/models/{run_name}/{cfg.exp_name}_{iteration}.model"
+                torch.save(agent.state_dict(), model_path)
+                print(f"model saved to {model_path}")
+                if ckpt is not None:
+                    os.makedirs(f"{output_dir}/checkpoints/{run_name}", exist_ok=True)
+                    torch.save(ckpt, f"{output_dir}/checkpoints/{run_name}/{cfg.exp_name}_{iteration}.ckpt")
     envs.close()
     return agent
 

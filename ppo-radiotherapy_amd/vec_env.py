@@ -104,8 +104,14 @@ class RadiotherapyVecEnv:
     # ------------------------------------------------------------------ API
     def reset(self, seed: int | None = None, options: dict | None = None):
         """Reset every env (gymnasium VectorEnv.reset).  `options` may hold
-        `tumour_ids` (int[N], -1 = sample) and `mask` (bool[N])."""
+        `tumour_ids` (int[N], -1 = sample) and `mask` (bool[N]).  `seed`
+        re-keys the tumour-sampling stream (rt_env_reseed): the tumours drawn
+        from here on depend only on (seed, global env id)."""
         options = options or {}
+        if seed is not None:
+            _lib.check(self._L.rt_env_reseed(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.stream_handle()),
+                       "rt_env_reseed")
+            self._seed = int(seed)
         ids = options.get("tumour_ids")
         mask = options.get("mask")
         ids_t = None if ids is None else _device_array(ids, torch.int32, self.device)

@@ -328,3 +328,67 @@ def test_env_beam_list_is_the_applied_beam(dev, mode):
             want = np.clip(before[e] + beam * np.float32(0.1), np.float32(0), np.float32(1))
             np.testing.assert_array_equal(after[e].view(np.uint32), want.view(np.uint32), err_msg=f"t {t} env {e}")
     env.close()
+
+
+def test_reset_seed_rekeys_tumour_stream(dev):
+    """reset(seed=s) (rt_env_reseed): the tumours drawn afterwards are the
+    Philox draws of key s from draw index 0 (tests/rt_rng.py), whatever the
+    handle drew before -- a resumed run does not replay iteration 1's tumours
+    and a given seed reproduces its sequence."""
+    import rt_rng
+
+    lib = assets.synthetic_library((64, 64, 64), 1000, 0)
+    N = 64
+    env = _vec_env(N, lib, seed=5)
+    env.reset()
+    env.reset()  # two draws on key 5
+    first = env.get_state()[2].cpu().numpy()
+    np.testing.assert_array_equal(first, [rt_rng.tumour_draw(5, e, 1, 1000) for e in range(N)])
+    env.reset(seed=77)
+    a = env.get_state()[2].cpu().numpy()
+    np.testing.assert_array_equal(a, [rt_rng.tumour_draw(77, e, 0, 1000) for e in range(N)])
+    env.reset()
+    env.reset(seed=77)
+    np.testing.assert_array_equal(env.get_state()[2].cpu().numpy(), a)
+    env.close()
+
+
+_LDS_ORDER = r"""
+import sys
+sys.path.insert(0, {repo!r})
+import _rtpkg
+import numpy as np, torch
+from ppo_radiotherapy_amd import assets
+from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
+small = assets.synthetic_library((32, 32, 32), 8, 0)
+ref = assets.synthetic_library((64, 64, 64), 8, 0)
+# one 2400-voxel tumour: k_finish needs > 64 KiB of dynamic LDS on this handle
+big = np.sort(np.random.default_rng(0).choice(64 ** 3, 2400, replace=False)).astype(np.int32)
+vox = np.concatenate([ref.voxels, big])
+off = np.concatenate([ref.offsets, [ref.offsets[-1] + big.size]])
+lib = assets.TumourLibrary(shape=ref.shape, lungs=ref.lungs, names=ref.names + ["big"], voxels=vox, offsets=off)
+for mode in ("dense", "incremental"):
+    for L, ids in ((small, None), (lib, [8] * 16)):
+        env = RadiotherapyVecEnv(16, visionless=True, library=L, seed=1, step_mode=mode)
+        env.reset(options=None if ids is None else {{"tumour_ids": ids}})
+        for t in range(3):
+            env.step(torch.zeros((16, 6), device="cuda"))
+        torch.cuda.synchronize()
+        env.close()
+print("lds-order ok")
+"""
+
+
+def test_small_then_large_lds_handle_in_one_process(dev):
+    """a handle whose k_finish needs <= 64 KiB of LDS created first
+    must not stop a later handle that needs more from launching (the dynamic-LDS
+    limit is raised per kernel on first use).  Fresh process: the first launch
+    of each kernel in it is the small handle's."""
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _LDS_ORDER.format(repo=repo)], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "lds-order ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -190,3 +190,55 @@ def test_episode_statistics_logged_per_rollout_step():
         assert len(ref.rows) >= 12 and [r[0] for r in mine.rows] == [r[0] for r in ref.rows]
         assert [r[2] for r in mine.rows] == [r[2] for r in ref.rows]
         np.testing.assert_allclose([r[1] for r in mine.rows], [r[1] for r in ref.rows], rtol=1e-12, atol=1e-12)
+
+
+def _ckpt_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = _trainer(8, seed=10 + rank, rank=rank, world=world)
+    broadcast_parameters(tr.agent)
+    tr.rollout()
+    tr.compute_gae()
+    tr.update()
+    ck = tr.state_dict()  # collective: gathers every rank's generator state
+    expect_next = torch.randint(0, 2 ** 62, (4,), generator=tr.gen)
+    # a fresh replica resumed from the (rank-0-written) checkpoint
+    fresh = _trainer(8, seed=999, rank=rank, world=world)
+    fresh.load_state_dict(ck)
+    got_next = torch.randint(0, 2 ** 62, (4,), generator=fresh.gen)
+    same_params = all(bool((p == r).all()) for p, r in zip(fresh.params, tr.params))
+    # another world size: no state for this rank -> re-derived, still distinct per rank
+    other = dict(ck, rng=ck["rng"][:1] * (world + 1))
+    moved = _trainer(8, seed=999, rank=rank, world=world)
+    moved.load_state_dict(other)
+    derived = torch.randint(0, 2 ** 62, (4,), generator=moved.gen)
+    q.put((rank, len(ck["rng"]), expect_next.numpy(), got_next.numpy(), same_params, derived.numpy()))
+    dist.destroy_process_group()
+
+
+def test_checkpoint_keeps_per_rank_generator_states():
+    """every rank resumes its own sampling stream (not rank 0's)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, n, expect, got, same, _ in res:
+        assert n == world and same
+        np.testing.assert_array_equal(got, expect)  # resumed stream continues this rank's own
+    assert not np.array_equal(res[0][2], res[1][2])   # ranks' streams differ
+    assert not np.array_equal(res[0][5], res[1][5])   # also when re-derived
+
+
+def test_env_seed_folds_resume_iteration():
+    from ppo_radiotherapy_amd.train import env_seed
+
+    assert env_seed(1, 0, 1) == 1 and env_seed(1, 3, 1) == 4
+    assert env_seed(1, 0, 2) != env_seed(1, 0, 1) and env_seed(1, 0, 2) != env_seed(1, 0, 3)
+    assert 0 <= env_seed(2 ** 64 - 1, 7, 5) < 2 ** 64
