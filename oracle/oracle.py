@@ -54,6 +54,7 @@ def lib():
         L.or_np_sum_f32.argtypes = [f_p, ctypes.c_int64]
         L.or_np_sum_f32.restype = ctypes.c_float
         L.or_apply_rotation.argtypes = [d_p, f_p, ctypes.c_double, d_p, d_p]
+        L.or_apply_rotation_sc.argtypes = [d_p, f_p, ctypes.c_double, d_p, d_p, d_p]
         L.or_apply_translation.argtypes = [d_p, d_p, P(ctypes.c_int64), d_p, d_p]
         L.or_map_translation.argtypes = [f_p, P(ctypes.c_int64), d_p]
         L.or_map_rotation.argtypes = [f_p, f_p]
@@ -120,13 +121,17 @@ def np_sum_f32(a: np.ndarray) -> np.float32:
     return np.float32(lib().or_np_sum_f32(_ptr(a, ctypes.c_float), a.size))
 
 
-def apply_rotation(direction, rotvec, min_angle=MIN_ANGLE_Z):
+def apply_rotation(direction, rotvec, min_angle=MIN_ANGLE_Z, half_sincos=None):
+    """transforms.py:7-59.  half_sincos: None = libm sin/cos of theta/2 (as
+    scipy's from_rotvec); else (sin, cos) of theta/2 to use instead."""
     d = np.ascontiguousarray(direction, dtype=np.float64)
     r = np.ascontiguousarray(rotvec, dtype=np.float32)
     out = np.zeros(3, np.float64)
     os_ = np.zeros(1, np.float64)
-    lib().or_apply_rotation(_ptr(d, ctypes.c_double), _ptr(r, ctypes.c_float), float(min_angle),
-                            _ptr(out, ctypes.c_double), _ptr(os_, ctypes.c_double))
+    sc = None if half_sincos is None else np.ascontiguousarray(half_sincos, dtype=np.float64)
+    lib().or_apply_rotation_sc(_ptr(d, ctypes.c_double), _ptr(r, ctypes.c_float), float(min_angle),
+                               None if sc is None else _ptr(sc, ctypes.c_double),
+                               _ptr(out, ctypes.c_double), _ptr(os_, ctypes.c_double))
     return out, float(os_[0])
 
 

@@ -76,16 +76,19 @@ def test_pose_cases(golden, dev):
     act = np.zeros((m, 6), np.float32)
     act[:, 3:] = z["rot_action"]
     out = _run_pose(L, dev, (67, 43, 70), pos, z["rot_dir_in"], act)
-    # scipy's from_rotvec uses libm sin/cos; the kernel evaluates them correctly
-    # rounded (double-double), which glibc is in all but ~0.15 % of arguments.
-    # Flagged tolerance: bit-exact for >= 99 % of rotations, the
-    # rest within a few ulp.
+    # scipy's from_rotvec takes sin/cos of theta/2 from libm; the kernel
+    # evaluates them correctly rounded (rtdd::sincos_cr).  Gate: the kernel is
+    # bit-exact against the oracle fed the correctly rounded half-angle sin/cos
+    # on EVERY rotation, and differs from the reference only on the rotations
+    # whose glibc sin or cos is itself 1 ulp off (5 of 3000; traced in
+    # tests/test_oracle.py::test_pose_ulp_differences_trace_to_libm_sincos).
+    from pose_trace import pose_ulp_trace
+
     got, want = out[:, 3:6], z["rot_dir_out"]
-    exact = np.all(got == want, axis=1)
-    assert exact.mean() >= 0.99, exact.mean()
-    ulp = np.abs(got.view(np.int64) - want.view(np.int64))
-    big = np.abs(want) > 1e-3
-    assert ulp[big].max() <= 8, ulp[big].max()
+    cr, libm_off = pose_ulp_trace(z)
+    assert np.array_equal(got.view(np.int64), cr.view(np.int64))
+    differs = ~np.all(got == want, axis=1)
+    assert not np.any(differs & ~libm_off)
     assert np.abs(got - want).max() <= 1e-15
     assert np.max(np.abs(out[:, 9] - z["rot_overshoot"])) <= 1e-12
     # translation cases

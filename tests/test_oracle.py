@@ -1,6 +1,8 @@
 """Pins the C restatement (oracle/rt_oracle.c) against golden vectors that
 tools/gen_golden.py produced by running the reference itself
 (draw_line.py, transforms.py, environment.py)."""
+import math
+
 import numpy as np
 import pytest
 
@@ -111,3 +113,24 @@ def test_env_terminates_by_irradiation(golden):
             _, info, done = env.step(z["actions"][e][t])
             assert info[0] == z["reward"][e][t] and info[1] == z["tumour"][e][t]
             assert done == bool(z["done"][e][t])
+
+
+def test_pose_ulp_differences_trace_to_libm_sincos(golden):
+    """every golden rotation where the correctly rounded
+    half-angle sin/cos (the device's) gives other bits than the reference is
+    one where glibc's sin or cos of theta/2 is itself 1 ulp from the correctly
+    rounded value; everywhere else the outputs are bit-identical.  The
+    amplification (1 ulp in sin/cos -> up to a few ulp of a small direction
+    component) is the quaternion -> matrix -> apply -> renormalise chain."""
+    z = golden("transform_cases.npz")
+    from pose_trace import pose_ulp_trace
+
+    cr, libm_off = pose_ulp_trace(z)
+    want = z["rot_dir_out"]
+    differs = ~np.all(cr == want, axis=1)
+    assert not np.any(differs & ~libm_off)           # no other source of difference
+    assert libm_off.mean() < 0.01                      # glibc: ~0.15 % of arguments
+    ulp = np.abs(cr.view(np.int64) - want.view(np.int64))[differs]
+    assert np.abs(cr - want).max() <= 2e-16 * 4
+    print(f"{libm_off.sum()} of {len(want)} rotations have a non-correctly-rounded libm sin/cos; "
+          f"{differs.sum()} differ; max {ulp.max() if ulp.size else 0} ulp")
