@@ -38,6 +38,13 @@ extern "C" int rt_internal_fail(int code, const char* msg);
 
 namespace {
 
+// experiment knob (kernel-variant A/B builds only, tools/build_variant.py):
+// 1 = forward epilogue reduced to one store per tile, 2 = forward without the
+// input-tile load
+#ifndef RT_C3D_EXP
+#define RT_C3D_EXP 0
+#endif
+
 constexpr int CO = 16;
 constexpr int kThreads = 512;      // weight-gradient kernel: 8 waves = position groups x column groups
 // forward / data-gradient kernels: conv1 (4 input channels, 95 VGPRs) runs
@@ -299,7 +306,7 @@ __global__ __launch_bounds__(conv_threads<CIN>()) void k_conv_relu_pool(FwdParam
     const int64_t srow = P.rows ? P.rows[b] : b;
     const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
     const int z0 = 2 * pz0 - g.pd, y0 = 2 * py0 - g.ph, x0 = -g.pw;
-    load_tile<CIN, conv_threads<CIN>()>(xs, xb, g, z0, y0, x0);
+    if (RT_C3D_EXP != 2) load_tile<CIN, conv_threads<CIN>()>(xs, xb, g, z0, y0, x0);
     float af[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) af[s] = a_frag<CIN, G>(P.w, s, c, gq);
@@ -318,6 +325,10 @@ __global__ __launch_bounds__(conv_threads<CIN>()) void k_conv_relu_pool(FwdParam
     float* ybase = P.y + ((int64_t)b * CO + 4 * gq + myr) * chan;
     uint8_t* abase = TRAIN ? P.amax + ((int64_t)b * CO + 4 * gq + myr) * chan : nullptr;
     conv_core<CIN, PYB>(xs, af, g, PZB * PYB, [&](const f4 (&acc)[2], int row, int xp) {
+        if constexpr (RT_C3D_EXP == 1) {
+            ybase[(row * 64 + xp * 2) & 1023] = acc[0][0] + acc[1][1] + acc[0][2] + acc[1][3];
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int tx = 2 * xp + u;
@@ -345,6 +356,318 @@ __global__ __launch_bounds__(conv_threads<CIN>()) void k_conv_relu_pool(FwdParam
             }
         }
     });
+}
+
+// ---------------------------------------------------------------------------
+// Forward, z-ring version (the launched forward).  A block owns a y band of
+// PYB pooled rows (full x) of one sample and sweeps a chunk of ZC pooled z
+// rows.  Its LDS holds a ring of kRing input z-planes (all CIN channels,
+// [ci][yl][xl]); pooled row k needs planes 2k..2k+3 (relative to the pool
+// padding), and while the waves compute it the next two planes stream into
+// the two free slots by LDS DMA (global_load_lds, VEC floats per lane), so
+// the input is read once per chunk (plus 2 halo planes) and its transfer
+// overlaps the MFMAs; one barrier per pooled row.  Each item (2 tiles of
+// 2x2x4 positions) runs the MFMA chain of 27 k-steps per input-channel quad;
+// the epilogue of the PREVIOUS item (bias, ReLU, window max / first argmax,
+// stores through a buffer descriptor whose range check drops masked lanes --
+// no branches) is issued between this item's MFMAs.
+//
+// LDS strides (dwords mod 32): row YS = 4, channel CS = 8, slot = 16 (the
+// ring wrap too: 6 slots), so the 32 lanes of a ds_read (16 positions x 2
+// channels) hit 32 banks.
+constexpr int kRing = 6;
+constexpr int kRingMaxPieces = 12;  // DMA pieces per wave and slot (registers)
+
+struct RingGeom {
+    Geom g;            // dims, pool padding, XT; YL, XL, YS; CS = channel stride
+    int32_t SLOT;      // floats per plane slot (CIN channels)
+    int32_t npiece;    // 64*VEC-float DMA pieces per slot
+    int32_t nyb;       // y bands
+    int32_t ZC;        // pooled z rows per block (z chunk)
+};
+
+template <int CIN, int PYB, int VEC>
+RingGeom make_ring_geom(const rt_conv_layer* L, int B, int nthreads) {
+    RingGeom r{};
+    Geom& g = r.g;
+    g.D = L->in_dims[0];
+    g.H = L->in_dims[1];
+    g.W = L->in_dims[2];
+    g.cd = g.D - 2;
+    g.ch = g.H - 2;
+    g.cw = g.W - 2;
+    g.pd = L->pool_pad[0];
+    g.ph = L->pool_pad[1];
+    g.pw = L->pool_pad[2];
+    g.PD = (g.cd + 2 * g.pd - 2) / 2 + 1;
+    g.PH = (g.ch + 2 * g.ph - 2) / 2 + 1;
+    g.PW = (g.cw + 2 * g.pw - 2) / 2 + 1;
+    g.XT = (g.PW + 1) / 2;
+    g.ZL = 4;
+    g.YL = 2 * PYB + 2;
+    g.XL = 4 * g.XT + 2;
+    g.YS = round_mod((g.XL + VEC - 1) / VEC * VEC, 4);
+    g.ZS = 0;
+    g.CS = round_mod(g.YL * g.YS, 8);
+    r.SLOT = round_mod(CIN * g.CS, 16);
+    r.npiece = (r.SLOT + 64 * VEC - 1) / (64 * VEC);
+    r.nyb = (g.PH + PYB - 1) / PYB;
+    // z chunks: enough blocks to fill the chip a few times over (each chunk
+    // re-reads 2 halo planes)
+    const int64_t per_chunk = (int64_t)r.nyb * B;
+    int nzc = (int)std::min<int64_t>(g.PD, std::max<int64_t>(1, (4096 + per_chunk - 1) / per_chunk));
+    r.ZC = (g.PD + nzc - 1) / nzc;
+    (void)nthreads;
+    return r;
+}
+
+struct RingParams {
+    const float* x;
+    const int64_t* rows;  // sample b reads x row rows[b] (null: b)
+    const float* w;
+    const float* bias;
+    float* y;
+    uint8_t* amax;  // null: inference
+    RingGeom rg;
+};
+
+template <int CIN, int G, int PYB, int VEC, int NTH, bool TRAIN>
+__global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
+    extern __shared__ float xs[];
+    constexpr int NS = nsteps<CIN>();
+    constexpr int NB = NS / 9;           // 9-step batches: one (channel quad, dz) each
+    constexpr int NW = NTH / 64;
+    const Geom& g = P.rg.g;
+    const int SLOT = P.rg.SLOT;
+    const int b = blockIdx.z, py0 = blockIdx.x * PYB;
+    const int k0 = blockIdx.y * P.rg.ZC, k1 = min(g.PD, k0 + P.rg.ZC);
+    if (k0 >= k1) return;
+    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t srow = P.rows ? P.rows[b] : b;
+    const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
+    const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
+    const int plane = g.H * g.W;
+
+    // ---- this lane's DMA sources: piece i of a slot -> offset within a plane
+    // of channel 0 (clamped: out-of-volume values feed masked positions only)
+    int goff[kRingMaxPieces];
+    const int npw = (P.rg.npiece - wave + NW - 1) / NW;  // pieces of this wave
+#pragma unroll
+    for (int i = 0; i < kRingMaxPieces; ++i) {
+        int f = ((wave + NW * i) * 64 + lane) * VEC;
+        f = min(f, SLOT - VEC);
+        int ci = f / g.CS;
+        const int rem = f - ci * g.CS;
+        int yl = rem / g.YS;
+        const int xl = rem - yl * g.YS;
+        ci = min(ci, CIN - 1);
+        yl = min(yl, g.YL - 1);
+        const int gy = min(max(y0 + yl, 0), g.H - 1);
+        const int gx = min(max(x0 + xl, 0), g.W - VEC);
+        goff[i] = ci * g.D * plane + gy * g.W + gx;
+    }
+    auto load_plane = [&](int t, int slot) {  // relative plane t (input z = t - pd) -> ring slot
+        const int iz = min(max(t - g.pd, 0), g.D - 1);
+        const float* src = xb + (size_t)iz * plane;
+        float* dst = xs + slot * SLOT;
+#pragma unroll
+        for (int i = 0; i < kRingMaxPieces; ++i) {
+            if (i >= npw) break;
+            const int f0 = (wave + NW * i) * 64 * VEC;
+            if (f0 + lane * VEC < SLOT) {
+                if constexpr (VEC == 4)
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(src + goff[i]), (lds_ptr_t)(dst + f0), 16, 0, 0);
+                else
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(src + goff[i]), (lds_ptr_t)(dst + f0), 4, 0, 0);
+            }
+        }
+    };
+
+    // ---- weights (A fragments), bias, epilogue constants
+    float af[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) af[s] = a_frag<CIN, G>(P.w, s, c, gq);
+    float bias[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[r] = P.bias[4 * gq + r];
+    const int zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
+    const int widx = zc * 4 + yc * 2 + (xc & 1);  // rank of the lane in its pooling window
+    const int myr = widx & 3;                      // after the window reduction: lane stores channel 4g + myr
+    const bool storer = widx < 4;
+    const int chan = g.PD * g.PH * g.PW;
+    const int cbase = (4 * gq + myr) * chan;       // element offset of this lane's channel in the sample
+    const __amdgpu_buffer_rsrc_t ysrd = __builtin_amdgcn_make_buffer_rsrc(
+        P.y + (int64_t)b * CO * chan, 0, CO * chan * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t asrd = __builtin_amdgcn_make_buffer_rsrc(
+        TRAIN ? (void*)(P.amax + (int64_t)b * CO * chan) : (void*)P.y, 0, TRAIN ? CO * chan : 0, 0x00020000);
+    const int lane_xy = gq * g.CS + yc * g.YS + xc;
+    const int nxp = (g.XT + 1) / 2;
+    const int nitem = PYB * nxp;
+    const int NI = (nitem + NW - 1) / NW;  // item rounds per pooled row (all waves run NI)
+
+    // epilogue of one item (tiles tx = 2xp, 2xp+1 of row r at pooled z pz)
+    auto epi = [&](const f4 (&acc)[2], int r, int xp, int pz, bool ok) {
+        const int py = py0 + r;
+        const int cz = 2 * pz - g.pd + zc, cy = 2 * py - g.ph + yc;
+        const bool vzy = ok && cz >= 0 && cz < g.cd && cy >= 0 && cy < g.ch;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int tx = 2 * xp + u;
+            const int cx = 4 * tx - g.pw + xc;
+            const bool valid = vzy && cx >= 0 && cx < g.cw;
+            const int px = 2 * tx + (xc >> 1);
+            float mine = 0.0f;
+            int kmine = 0;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const float v = valid ? fmaxf(acc[u][rr] + bias[rr], 0.0f) : -INFINITY;
+                const float m = win_max(v);
+                mine = rr == myr ? m : mine;
+                if constexpr (TRAIN) {
+                    const int k = win_min(v == m ? widx : 8);  // torch: first maximum in (z, y, x) window order
+                    kmine = rr == myr ? k : kmine;
+                }
+            }
+            const bool st = ok && storer && tx < g.XT && py < g.PH && px < g.PW;
+            const int o = cbase + (pz * g.PH + py) * g.PW + px;
+            if constexpr (RT_C3D_EXP == 5) {
+                if (st) {
+                    P.y[(int64_t)b * CO * chan + o] = mine;
+                    if constexpr (TRAIN) P.amax[(int64_t)b * CO * chan + o] = (uint8_t)(kmine | (mine > 0.0f ? 8 : 0));
+                }
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mine), ysrd, st ? 4 * o : INT32_MIN, 0, 0);
+                if constexpr (TRAIN)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kmine | (mine > 0.0f ? 8 : 0)), asrd,
+                                                         st ? o : INT32_MIN, 0, 0);
+            }
+        }
+    };
+
+    // ---- prologue: planes 0..3 of the chunk
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load_plane(2 * k0 + i, i);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+
+    f4 pacc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+    int pr = 0, pxp = 0, ppz = k0;
+    bool pok = false;
+    int sb = 0;  // ring slot of plane 2k
+    for (int k = k0; k < k1; ++k) {
+        if (k + 1 < k1) {  // planes of the next pooled row -> the two free slots
+            load_plane(2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4);
+            load_plane(2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5);
+        }
+        int zoff[3];
+#pragma unroll
+        for (int dz = 0; dz < 3; ++dz) {
+            int sl = sb + zc + dz;
+            sl = sl >= kRing ? sl - kRing : sl;
+            zoff[dz] = sl * SLOT + lane_xy;
+        }
+        int r = 0, xp = wave;
+        while (xp >= nxp) {
+            xp -= nxp;
+            ++r;
+        }
+        for (int it = 0; it < NI; ++it) {
+            const bool ok = r < PYB;
+            const int rr = ok ? r : PYB - 1;
+            const int tb = 2 * rr * g.YS + 8 * xp;
+            float bv[2][2][9];
+            auto fetch = [&](float (&dst)[2][9], int bj) {
+                const int dz = bj % 3, j = bj / 3;
+                const int base = zoff[dz] + tb + j * 4 * g.CS;
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        dst[0][dy * 3 + dx] = xs[base + dy * g.YS + dx];
+                        dst[1][dy * 3 + dx] = xs[base + dy * g.YS + dx + 4];
+                    }
+            };
+            fetch(bv[0], 0);
+            epi(pacc, pr, pxp, ppz, pok);  // the previous item's epilogue, between this item's MFMAs
+            f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+            for (int bj = 0; bj < NB; ++bj) {
+                if (bj + 1 < NB) fetch(bv[(bj + 1) & 1], bj + 1);
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    acc[0] = mfma4(af[bj * 9 + q], bv[bj & 1][0][q], acc[0]);
+                    acc[1] = mfma4(af[bj * 9 + q], bv[bj & 1][1][q], acc[1]);
+                }
+            }
+            pacc[0] = acc[0];
+            pacc[1] = acc[1];
+            pr = r;
+            pxp = xp;
+            ppz = k;
+            pok = ok;
+            xp += NW;
+            while (xp >= nxp) {
+                xp -= nxp;
+                ++r;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next row has landed
+        __syncthreads();                     // ... every wave's; and nobody still reads the slots reloaded next
+        sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+    }
+    epi(pacc, pr, pxp, ppz, pok);
+}
+
+template <int CIN, int G, int PYB, int VEC, int NTH>
+int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
+                const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+    RingParams P{x, rows, w, bias, y, amax, rg};
+    const size_t lds = (size_t)kRing * rg.SLOT * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, true>);
+        allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, false>);
+        attr = true;
+    }
+    dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, B);
+    if (amax)
+        hipLaunchKernelGGL((k_conv_ring<CIN, G, PYB, VEC, NTH, true>), grid, dim3(NTH), lds, st, P);
+    else
+        hipLaunchKernelGGL((k_conv_ring<CIN, G, PYB, VEC, NTH, false>), grid, dim3(NTH), lds, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+// the forward: the widest y band whose ring fits the LDS budget (80 KiB: two
+// 8-wave blocks per CU for conv1; the 16-channel stages hold 2 waves per SIMD
+// by registers, one 8-wave block per CU, 160 KiB)
+template <int CIN, int G>
+int launch_fwd_ring(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
+                    const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+    constexpr int NTH = 512;
+    const size_t budget = (CIN == 4 ? 80 : 160) * 1024;
+    const bool vec4 = RT_C3D_EXP != 4 && CIN == 4 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
+                      (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    auto fits = [&](const RingGeom& rg, int vec) {
+        return (size_t)kRing * rg.SLOT * sizeof(float) <= budget &&
+               (rg.npiece + NTH / 64 - 1) / (NTH / 64) <= kRingMaxPieces && rg.g.W >= vec;
+    };
+    constexpr int PY_BIG = CIN == 4 ? 4 : 2;
+    if constexpr (CIN == 4) {
+        if (!vec4) goto scalar;
+        RingGeom rg = make_ring_geom<CIN, PY_BIG, 4>(L, B, NTH);
+        if (fits(rg, 4)) return launch_ring<CIN, G, PY_BIG, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+        rg = make_ring_geom<CIN, PY_BIG / 2, 4>(L, B, NTH);
+        if (fits(rg, 4)) return launch_ring<CIN, G, PY_BIG / 2, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+    }
+scalar:
+    RingGeom rg = make_ring_geom<CIN, PY_BIG, 1>(L, B, NTH);
+    if (fits(rg, 1)) return launch_ring<CIN, G, PY_BIG, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+    rg = make_ring_geom<CIN, PY_BIG / 2, 1>(L, B, NTH);
+    if (fits(rg, 1)) return launch_ring<CIN, G, PY_BIG / 2, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+    return rt_internal_fail(RT_ELIMIT, "rt_conv: input plane ring exceeds LDS (grid too wide)");
 }
 
 // ---------------------------------------------------------------------------
@@ -722,10 +1045,16 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     if (bad_layer(L) || batch < 1 || batch > 65535 || !x_d || !w_d || !b_d || !y_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_fwd: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (L->cin == 4) return launch_fwd<4, 1, 2, 4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-    if (L->groups == 1) return launch_fwd<16, 1, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-    if (L->groups == 2) return launch_fwd<16, 2, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-    return launch_fwd<16, 4, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    if (RT_C3D_EXP == 3) {  // the previous one-region-per-block forward (A/B builds)
+        if (L->cin == 4) return launch_fwd<4, 1, 2, 4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+        if (L->groups == 1) return launch_fwd<16, 1, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+        if (L->groups == 2) return launch_fwd<16, 2, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+        return launch_fwd<16, 4, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    }
+    if (L->cin == 4) return launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    if (L->groups == 1) return launch_fwd_ring<16, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    if (L->groups == 2) return launch_fwd_ring<16, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    return launch_fwd_ring<16, 4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
 }
 
 extern "C" int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* L, int32_t batch) {
