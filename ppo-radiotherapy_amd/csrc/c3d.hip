@@ -31,6 +31,7 @@
 #include <cstdint>
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 #include "rtenv.h"
 
@@ -80,6 +81,7 @@ struct Geom {
     int32_t XT;          // x tiles (4 conv positions = 2 windows each)
     int32_t ZL, YL, XL;  // LDS tile extents
     int32_t YS, ZS, CS;  // LDS strides
+    int32_t PYB_tiles;   // ring weight gradient: position tiles per pooled row
 };
 
 // LDS stride residues (mod 32 dwords): (4, 8, 16) make the forward's reads
@@ -421,6 +423,61 @@ RingGeom make_ring_geom(const rt_conv_layer* L, int B, int nthreads) {
     return r;
 }
 
+// LDS-DMA loader of ring slots: slot = one input z-plane of all CIN channels
+// of the block's y band, [ci][yl][xl]; lane l of wave w fills VEC floats of
+// piece w + NW*i.  Sources are clamped into the volume (out-of-volume values
+// feed masked positions only, and stay finite for the backward).
+template <int CIN, int VEC, int NW>
+struct RingLoader {
+    int goff[kRingMaxPieces];  // per piece: offset within a plane of channel 0
+    int npw;                   // pieces of this wave
+
+    __device__ __forceinline__ void init(const RingGeom& rg, int y0, int x0, int wave, int lane) {
+        const Geom& g = rg.g;
+        const int plane = g.H * g.W;
+        npw = (rg.npiece - wave + NW - 1) / NW;
+#pragma unroll
+        for (int i = 0; i < kRingMaxPieces; ++i) {
+            int f = ((wave + NW * i) * 64 + lane) * VEC;
+            f = min(f, rg.SLOT - VEC);
+            int ci = f / g.CS;
+            const int rem = f - ci * g.CS;
+            int yl = rem / g.YS;
+            const int xl = rem - yl * g.YS;
+            ci = min(ci, CIN - 1);
+            yl = min(yl, g.YL - 1);
+            const int gy = min(max(y0 + yl, 0), g.H - 1);
+            const int gx = min(max(x0 + xl, 0), g.W - VEC);
+            goff[i] = ci * g.D * plane + gy * g.W + gx;
+        }
+    }
+    // relative plane t (input z = t - pd, clamped) -> ring slot.  The pieces
+    // are expanded by a fold over a compile-time index sequence (goff stays in
+    // registers; a loop the compiler keeps rolled would index it dynamically)
+    template <int I>
+    __device__ __forceinline__ void piece(const float* src, float* dst, int wave, int lane, int slot_floats) const {
+        const int f0 = (wave + NW * I) * 64 * VEC;
+        if (I < npw && f0 + lane * VEC < slot_floats) {
+            if constexpr (VEC == 4)
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(src + goff[I]), (lds_ptr_t)(dst + f0), 16, 0, 0);
+            else
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(src + goff[I]), (lds_ptr_t)(dst + f0), 4, 0, 0);
+        }
+    }
+    template <int... I>
+    __device__ __forceinline__ void pieces(const float* src, float* dst, int wave, int lane, int slot_floats,
+                                           std::integer_sequence<int, I...>) const {
+        (piece<I>(src, dst, wave, lane, slot_floats), ...);
+    }
+    __device__ __forceinline__ void load(const float* xb, const RingGeom& rg, float* xs, int t, int slot, int wave,
+                                         int lane) const {
+        const Geom& g = rg.g;
+        const int iz = min(max(t - g.pd, 0), g.D - 1);
+        pieces(xb + (size_t)iz * g.H * g.W, xs + slot * rg.SLOT, wave, lane, rg.SLOT,
+               std::make_integer_sequence<int, kRingMaxPieces>{});
+    }
+};
+
 struct RingParams {
     const float* x;
     const int64_t* rows;  // sample b reads x row rows[b] (null: b)
@@ -447,42 +504,10 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
     const int64_t srow = P.rows ? P.rows[b] : b;
     const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
     const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
-    const int plane = g.H * g.W;
 
-    // ---- this lane's DMA sources: piece i of a slot -> offset within a plane
-    // of channel 0 (clamped: out-of-volume values feed masked positions only)
-    int goff[kRingMaxPieces];
-    const int npw = (P.rg.npiece - wave + NW - 1) / NW;  // pieces of this wave
-#pragma unroll
-    for (int i = 0; i < kRingMaxPieces; ++i) {
-        int f = ((wave + NW * i) * 64 + lane) * VEC;
-        f = min(f, SLOT - VEC);
-        int ci = f / g.CS;
-        const int rem = f - ci * g.CS;
-        int yl = rem / g.YS;
-        const int xl = rem - yl * g.YS;
-        ci = min(ci, CIN - 1);
-        yl = min(yl, g.YL - 1);
-        const int gy = min(max(y0 + yl, 0), g.H - 1);
-        const int gx = min(max(x0 + xl, 0), g.W - VEC);
-        goff[i] = ci * g.D * plane + gy * g.W + gx;
-    }
-    auto load_plane = [&](int t, int slot) {  // relative plane t (input z = t - pd) -> ring slot
-        const int iz = min(max(t - g.pd, 0), g.D - 1);
-        const float* src = xb + (size_t)iz * plane;
-        float* dst = xs + slot * SLOT;
-#pragma unroll
-        for (int i = 0; i < kRingMaxPieces; ++i) {
-            if (i >= npw) break;
-            const int f0 = (wave + NW * i) * 64 * VEC;
-            if (f0 + lane * VEC < SLOT) {
-                if constexpr (VEC == 4)
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(src + goff[i]), (lds_ptr_t)(dst + f0), 16, 0, 0);
-                else
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(src + goff[i]), (lds_ptr_t)(dst + f0), 4, 0, 0);
-            }
-        }
-    };
+    RingLoader<CIN, VEC, NW> ld;
+    ld.init(P.rg, y0, x0, wave, lane);
+    auto load_plane = [&](int t, int slot) { ld.load(xb, P.rg, xs, t, slot, wave, lane); };
 
     // ---- weights (A fragments), bias, epilogue constants
     float af[NS];
@@ -884,6 +909,160 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad(WgradParams P) {
     }
 }
 
+// Weight gradient, z-ring version (the launched one): a block owns a y band
+// of one sample at a time (samples blockIdx.z, + gridDim.z, ...) and sweeps
+// its pooled z rows with the forward's plane ring; the dY operand of the next
+// pooled row (pooled gradient + argmax byte per lane and position tile) is
+// loaded into registers together with the next planes' DMA, so one wait +
+// barrier per row covers both.  Column tiles and the MFMA mapping are those
+// of k_conv_wgrad.
+constexpr int kWgMaxTiles = 8;  // position tiles per wave and pooled row
+
+struct WgradRingParams {
+    const float* x;
+    const int64_t* rows;
+    const float* dP;
+    const uint8_t* am;
+    float* part;  // [nblk][16 * ncol * 16]
+    int32_t B;
+    RingGeom rg;
+};
+
+template <int CIN, int PYB, int VEC>
+__global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P) {
+    extern __shared__ float xs[];
+    constexpr int NW = kThreads / 64;
+    constexpr int NCT = ncol_tiles<CIN>();
+    constexpr int WC = NCT / kWgradTiles;  // column groups (1 for conv1, 4 for the 16-channel stages)
+    constexpr int WP = NW / WC;            // position groups
+    static_assert(NCT % kWgradTiles == 0, "column tiles");
+    const Geom& g = P.rg.g;
+    const int SLOT = P.rg.SLOT;
+    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wc = wave % WC, wp = wave / WC;
+    const int t0c = wc * kWgradTiles;
+    const int py0 = blockIdx.x * PYB;
+    const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
+    RingLoader<CIN, VEC, NW> ld;
+    ld.init(P.rg, y0, x0, wave, lane);
+    // column 16(t0c + T) + c = (ci, tap): in-plane LDS offset and dz, or a constant B
+    int kin[kWgradTiles], kdz[kWgradTiles];
+    float kconst[kWgradTiles];
+#pragma unroll
+    for (int T = 0; T < kWgradTiles; ++T) {
+        const int k = 16 * (t0c + T) + c;
+        if (k < CIN * 27) {
+            const int ci = k / 27, q = k % 27;
+            kin[T] = ci * g.CS + ((q / 3) % 3) * g.YS + q % 3;
+            kdz[T] = q / 9;
+            kconst[T] = -1.0f;
+        } else {
+            kin[T] = 0;
+            kdz[T] = 0;
+            kconst[T] = k == CIN * 27 ? 1.0f : 0.0f;
+        }
+    }
+    f4 acc[kWgradTiles];
+#pragma unroll
+    for (int T = 0; T < kWgradTiles; ++T) acc[T] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int ntile = PYB * g.XT;                     // position tiles per pooled row
+    const int ntw = (ntile - wp + WP - 1) / WP;       // this wave's: t = wp + WP * i
+    const int chan = g.PD * g.PH * g.PW;
+    for (int b = blockIdx.z; b < P.B; b += gridDim.z) {
+        const int64_t srow = P.rows ? P.rows[b] : b;
+        const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
+        const uint8_t* amb = P.am + ((int64_t)b * CO + c) * chan;
+        const float* dpb = P.dP + ((int64_t)b * CO + c) * chan;
+        int abyte[2][kWgMaxTiles];
+        float ad[2][kWgMaxTiles];
+        // lane (c, g) of tile t: channel c at the 4 positions 4q + g, all in pooled window px = 2tx + (g >> 1)
+        auto load_a = [&](int k, int (&byte)[kWgMaxTiles], float (&d)[kWgMaxTiles]) {
+#pragma unroll
+            for (int i = 0; i < kWgMaxTiles; ++i) {
+                const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
+                const int py = py0 + r, px = 2 * tx + (gq >> 1);
+                const bool ok = i < ntw && py < g.PH && px < g.PW;
+                const int o = (k * g.PH + py) * g.PW + px;
+                byte[i] = ok ? amb[o] : 0;
+                d[i] = ok ? dpb[o] : 0.0f;
+            }
+        };
+        __syncthreads();  // the previous sample's ring reads are done
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ld.load(xb, P.rg, xs, i, i, wave, lane);
+        load_a(0, abyte[0], ad[0]);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+        int sb = 0;
+        // one pooled row; the register buffer parity is compile-time (no dynamic indexing)
+        auto step = [&](int k, auto parity) {
+            constexpr int cur = decltype(parity)::value;
+            if (k + 1 < g.PD) {
+                load_a(k + 1, abyte[cur ^ 1], ad[cur ^ 1]);
+                ld.load(xb, P.rg, xs, 2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4, wave, lane);
+                ld.load(xb, P.rg, xs, 2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5, wave, lane);
+            }
+            int kaddr[4][kWgradTiles];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int T = 0; T < kWgradTiles; ++T) {
+                    int sl = sb + (q >> 1) + kdz[T];
+                    sl = sl >= kRing ? sl - kRing : sl;
+                    kaddr[q][T] = sl * SLOT + (q & 1) * g.YS + gq + kin[T];
+                }
+#pragma unroll
+            for (int i = 0; i < kWgMaxTiles; ++i) {
+                if (i >= ntw) break;
+                const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
+                const int toff = 2 * r * g.YS + 4 * tx;
+                const int byte = abyte[cur][i];
+                const float d = ad[cur][i];
+                float bv[4][kWgradTiles];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int T = 0; T < kWgradTiles; ++T)
+                        bv[q][T] = kconst[T] < 0.0f ? xs[kaddr[q][T] + toff] : kconst[T];
+                float a[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)  // position n = 4q + g: zc = q >> 1, yc = q & 1, xc = g
+                    a[q] = ((byte & 8) && (byte & 7) == ((q >> 1) * 4 + (q & 1) * 2 + (gq & 1))) ? d : 0.0f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int T = 0; T < kWgradTiles; ++T) acc[T] = mfma4(a[q], bv[q][T], acc[T]);
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            __syncthreads();
+            sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+        };
+        for (int k = 0; k < g.PD; k += 2) {
+            step(k, std::integral_constant<int, 0>{});
+            if (k + 1 < g.PD) step(k + 1, std::integral_constant<int, 1>{});
+        }
+    }
+    // D (lane (c, g)): rows co = 4g + r, column 16T + c; the WP position
+    // groups are summed through LDS (the ring's space) in a fixed order
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    float* out = P.part + (size_t)blk * (CO * NCT * 16);
+    constexpr int REG = CO * NCT * 16;
+    __syncthreads();
+    float* R = xs;
+#pragma unroll
+    for (int T = 0; T < kWgradTiles; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) R[wp * REG + (4 * gq + r) * (NCT * 16) + 16 * (t0c + T) + c] = acc[T][r];
+    __syncthreads();
+    for (int i = threadIdx.x; i < REG; i += kThreads) {
+        float v = R[i];
+#pragma unroll
+        for (int k = 1; k < WP; ++k) v += R[k * REG + i];
+        out[i] = v;
+    }
+}
+
 // sum of the block partials -> dW [16][cin/G][27] (in-group columns) and db [16]
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* part, int nblk, int cin, int groups, int ncol,
                                                       float* dw, float* db) {
@@ -1019,6 +1198,73 @@ int launch_wgrad(const rt_conv_layer* L, int32_t B, const float* x, const int64_
     return RT_OK;
 }
 
+// ring weight gradient: plan (y band, DMA width) and launch
+template <int CIN, int PYB, int VEC>
+int launch_wgrad_ring_k(const RingGeom& rg, int32_t B, int gz, const float* x, const int64_t* rows,
+                        const float* dP, const uint8_t* am, float* ws, hipStream_t st) {
+    WgradRingParams P{x, rows, dP, am, ws, B, rg};
+    constexpr int NCT = ncol_tiles<CIN>();
+    constexpr int WC = NCT / kWgradTiles, WP = (kThreads / 64) / WC;
+    const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * CO * NCT * 16) * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        allow_big_lds(&k_conv_wgrad_ring<CIN, PYB, VEC>);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_conv_wgrad_ring<CIN, PYB, VEC>), dim3(rg.nyb, 1, gz), dim3(kThreads), lds, st, P);
+    return RT_OK;
+}
+
+constexpr int kWgradRingBlocks = 512;
+
+template <int CIN>
+int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
+                      const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
+    constexpr int NCT = ncol_tiles<CIN>();
+    constexpr int WC = NCT / kWgradTiles, WP = (kThreads / 64) / WC;
+    const size_t budget = (CIN == 4 ? 80 : 160) * 1024;
+    const bool vec4 = RT_C3D_EXP != 4 && CIN == 4 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
+                      (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    auto fits = [&](const RingGeom& rg, int vec) {
+        const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * CO * NCT * 16) * sizeof(float);
+        return lds <= budget && (rg.npiece + kThreads / 64 - 1) / (kThreads / 64) <= kRingMaxPieces &&
+               (rg.g.PYB_tiles + WP - 1) / WP <= kWgMaxTiles && rg.g.W >= vec;
+    };
+    int rc = RT_ELIMIT, nblk = 0;
+    auto go = [&](const RingGeom& rg, auto launch) {
+        const int gz = std::max(1, std::min<int>(B, kWgradRingBlocks / std::max(1, rg.nyb)));
+        nblk = rg.nyb * gz;
+        if ((int64_t)nblk * CO * NCT * 16 > ws_floats) return rt_internal_fail(RT_EINVAL, "rt_conv_wgrad: workspace too small");
+        return launch(rg, gz);
+    };
+    constexpr int PY_BIG = CIN == 4 ? 4 : 2;
+#define RT_WG_TRY(PYB_, VEC_)                                                                          \
+    {                                                                                                 \
+        RingGeom rg = make_ring_geom<CIN, PYB_, VEC_>(L, B, kThreads);                                \
+        rg.g.PYB_tiles = PYB_ * rg.g.XT;                                                              \
+        if (rc == RT_ELIMIT && fits(rg, VEC_))                                                        \
+            rc = go(rg, [&](const RingGeom& r, int gz) {                                              \
+                return launch_wgrad_ring_k<CIN, PYB_, VEC_>(r, B, gz, x, rows, dP, am, ws, st);       \
+            });                                                                                       \
+    }
+    if constexpr (CIN == 4) {
+        if (vec4) {
+            RT_WG_TRY(PY_BIG, 4)
+            RT_WG_TRY(PY_BIG / 2, 4)
+        }
+    }
+    RT_WG_TRY(PY_BIG, 1)
+    RT_WG_TRY(PY_BIG / 2, 1)
+#undef RT_WG_TRY
+    if (rc != RT_OK) return rc == RT_ELIMIT ? rt_internal_fail(RT_ELIMIT, "rt_conv_wgrad: ring exceeds LDS") : rc;
+    const int nout = CO * (L->cin / L->groups) * 27 + CO;
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((nout + 255) / 256), dim3(256), 0, st, (const float*)ws, nblk, L->cin,
+                       L->groups, NCT * 16, dw, db);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
 bool bad_layer(const rt_conv_layer* L) {
     if (!L) return true;
     if (!((L->cin == 4 && L->groups == 1) || (L->cin == 16 && (L->groups == 1 || L->groups == 2 || L->groups == 4))))
@@ -1059,6 +1305,10 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
 
 extern "C" int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* L, int32_t batch) {
     if (bad_layer(L) || batch < 1) return 0;
+    if (RT_C3D_EXP != 3) {  // ring: at most kWgradRingBlocks partial rows (one per block)
+        if (L->cin == 4) return (int64_t)kWgradRingBlocks * CO * ncol_tiles<4>() * 16;
+        return (int64_t)kWgradRingBlocks * CO * ncol_tiles<16>() * 16;
+    }
     if (L->cin == 4) return (int64_t)wgrad_blocks<4, 2, 4>(L, batch) * CO * ncol_tiles<4>() * 16;
     return (int64_t)wgrad_blocks<16, 1, 2>(L, batch) * CO * ncol_tiles<16>() * 16;
 }
@@ -1069,6 +1319,10 @@ extern "C" int rt_conv_relu_pool_wgrad(const rt_conv_layer* L, int32_t batch, co
     if (bad_layer(L) || batch < 1 || !x_d || !dy_d || !argmax_d || !dw_d || !db_d || !ws_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_wgrad: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (RT_C3D_EXP != 3) {
+        if (L->cin == 4) return launch_wgrad_ring<4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+        return launch_wgrad_ring<16>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+    }
     if (L->cin == 4) return launch_wgrad<4, 2, 4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
     return launch_wgrad<16, 1, 2>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
 }
