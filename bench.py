@@ -43,6 +43,11 @@ Also reported:
                          share and the scalar C port
   roofline.measured_copy_ceiling_GBps
                          device copy bandwidth measured in the same run
+  c3d_mfma               configs[3]'s C3D feature extractor (the MFMA path,
+                         north_star): its stage kernels on 512 vision
+                         observations at 64^3, inference forward and the
+                         training pass, TFLOP/s and fraction of the f32 MFMA
+                         peak (HIP events on the kernels' stream)
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       (N > 1 under torch.distributed.run, one rank per GPU)
@@ -94,6 +99,7 @@ def parse():
                     help="CPU-baseline sample budget per leg (4 legs: numpy/C x 1/all cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-update", action="store_true")
+    ap.add_argument("--no-c3d", action="store_true", help="skip the C3D MFMA stage timing (c3d_mfma)")
     ap.add_argument("--no-steady", action="store_true", help="skip the >= 101-step steady-state window")
     ap.add_argument("--env-only", action="store_true", help="time rt_env_step alone (profiling)")
     ap.add_argument("--seed", type=int, default=1)
@@ -278,6 +284,101 @@ def load_pmc(grid, envs, kernel="k_dense"):
     except Exception:
         pass
     return None
+
+
+def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
+    """BASELINE configs[3]'s C3D (north_star: "MFMA utilisation on the 3D-conv
+    against gfx950 peak"): the feature extractor's three fused stage kernels
+    on `batch` observations of a vision env at `grid` (a rollout step of 512
+    envs), timed with HIP events on the stream they run on: inference forward
+    (the rollout policy) and the training pass (forward with argmax bytes,
+    weight gradients of the three stages, data gradients of stages 3 and 2).
+    FLOPs count each stage's grouped convolution once per pass (SURVEY §8
+    a-15: 0.999 GFLOP per 64^3 forward); `frac` is against the dense f32
+    MFMA peak."""
+    import ctypes
+
+    import torch
+
+    from ppo_radiotherapy_amd import _lib
+    from ppo_radiotherapy_amd.networks import FeaturesExtractor3D
+    from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
+
+    env = RadiotherapyVecEnv(batch, visionless=False, library=lib, device=dev, seed=7)
+    env.reset()
+    g = torch.Generator(device=dev).manual_seed(3)
+    for _ in range(6):
+        env.step(torch.rand((batch, 6), device=dev, generator=g) * 2 - 1)
+    obs = env.obs.clone()
+    env.close()
+    torch.manual_seed(0)
+    fe = FeaturesExtractor3D((4, *grid), 64).to(dev)
+    plan = fe._plan()
+    convs = [m for m in fe.modules() if isinstance(m, torch.nn.Conv3d)]
+    L = _lib.load()
+    st = _lib.stream_handle()
+    names = ["conv1", "conv2", "conv3"]
+    cins = [4, 16, 16]
+    flops = []
+    dims = list(grid)
+    for k, (layer, od) in enumerate(plan):
+        cpg = cins[k] // int(layer.groups)
+        flops.append(2 * batch * 16 * cpg * 27 * int(np.prod([d - 2 for d in dims])))
+        dims = list(od)
+
+    def timed(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    acts, ams, grads = [obs], [], []
+    for k, (layer, od) in enumerate(plan):
+        acts.append(torch.empty((batch, 16, *od), device=dev))
+        ams.append(torch.empty((batch, 16, *od), dtype=torch.uint8, device=dev))
+        grads.append(torch.randn((batch, 16, *od), device=dev) * 1e-3)
+    stages = {}
+    fwd_ms = train_ms = 0.0
+    for k, (layer, od) in enumerate(plan):
+        w, bb = convs[k].weight.detach().contiguous(), convs[k].bias.detach().contiguous()
+
+        def fwd(am):
+            return lambda: _lib.check(L.rt_conv_relu_pool_fwd(ctypes.byref(layer), batch, acts[k].data_ptr(), None,
+                                                              w.data_ptr(), bb.data_ptr(), acts[k + 1].data_ptr(),
+                                                              _lib.ptr(am), st), "fwd")
+        t_inf = timed(fwd(None))
+        t_trn = timed(fwd(ams[k]))
+        dw, db = torch.empty_like(w), torch.empty_like(bb)
+        ws = torch.empty(int(L.rt_conv_wgrad_workspace_floats(ctypes.byref(layer), batch)), device=dev)
+        t_wg = timed(lambda: _lib.check(L.rt_conv_relu_pool_wgrad(
+            ctypes.byref(layer), batch, acts[k].data_ptr(), None, grads[k].data_ptr(), ams[k].data_ptr(),
+            dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(), st), "wgrad"))
+        row = {"forward_ms": t_inf, "forward_tflops": flops[k] / t_inf / 1e9, "train_forward_ms": t_trn,
+               "wgrad_ms": t_wg, "wgrad_tflops": flops[k] / t_wg / 1e9}
+        t_dg = 0.0
+        if k > 0:
+            dx = torch.empty_like(acts[k])
+            t_dg = timed(lambda: _lib.check(L.rt_conv_relu_pool_dgrad(
+                ctypes.byref(layer), batch, w.data_ptr(), grads[k].data_ptr(), ams[k].data_ptr(), dx.data_ptr(), st),
+                "dgrad"))
+            row.update({"dgrad_ms": t_dg, "dgrad_tflops": flops[k] / t_dg / 1e9})
+        stages[names[k]] = row
+        fwd_ms += t_inf
+        train_ms += t_trn + t_wg + t_dg
+    f_fwd = sum(flops)
+    f_train = 2 * sum(flops) + sum(flops[1:])
+    return {"bound": "mfma", "workload": f"C3D extractor stages, {batch} observations at {grid[0]}^3 "
+                                         "(BASELINE configs[3] rollout step), f32 MFMA",
+            "peak": F32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+            "forward": {"ms": fwd_ms, "flop": f_fwd, "achieved": f_fwd / fwd_ms / 1e9,
+                        "frac": f_fwd / (fwd_ms * 1e-3) / F32_MFMA_PEAK},
+            "train_pass": {"ms": train_ms, "flop": f_train, "achieved": f_train / train_ms / 1e9,
+                           "frac": f_train / (train_ms * 1e-3) / F32_MFMA_PEAK},
+            "stages": stages, "timing": "HIP events on the kernels' stream, mean of 5 back-to-back launches"}
 
 
 def main():
@@ -558,6 +659,8 @@ def main():
     if other is not None:
         out["other_step_mode"] = other
     out["roofline"] = roof
+    if rank == 0 and not a.no_c3d and not a.env_only:
+        out["c3d_mfma"] = c3d_roofline(dev, lib, grid)
     if rank == 0 and world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     if rank == 0:
