@@ -108,8 +108,9 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=0)
     ap.add_argument("--step-mode", choices=["dense", "incremental"], default="dense",
                     help="env step formulation measured as `value` (the other is reported beside it)")
-    ap.add_argument("--rollout-groups", type=int, default=2, choices=[1, 2],
-                    help="dense mode: env groups of the rollout call (2 = two pipelined streams)")
+    ap.add_argument("--rollout-groups", type=int, default=2, choices=[0, 1, 2],
+                    help="dense mode: env groups of the rollout call (2 = two pipelined streams, "
+                         "0 = one persistent launch with a per-env dense pass)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
     ap.add_argument("--rehearse-same-device", action="store_true",
@@ -452,18 +453,33 @@ def main():
     # ---------------- timed rollout (or env-only)
     K = a.steps
     actions = torch.rand((a.envs, 6), device=dev, generator=gen) * 2 - 1
-    env.kernel_timing(2 * K)  # HIP events around k_beam / k_dense / k_finish (one slot per env group and step)
+
+    def rollout_pass():
+        if a.env_only:
+            for i in range(K):
+                env.step(actions, info_out=tr.infos[i % T])
+        else:
+            run_steps(tr, K)
+
+    # `value`: the uninstrumented pass (the library's timing events, recorded
+    # between kernels, cost ~4 % of the pipelined step)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if a.env_only:
-        for i in range(K):
-            env.step(actions, info_out=tr.infos[i % T])
-    else:
-        run_steps(tr, K)
+    rollout_pass()
     torch.cuda.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
+    # kernel times: an identical pass with HIP events around k_beam / k_dense /
+    # k_finish (one slot per env group and step; one per persistent launch)
+    env.kernel_timing(2 * K)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rollout_pass()
+    torch.cuda.synchronize()
+    barrier()
+    dt_timed = max_over_ranks(time.perf_counter() - t0)
     kms, kcalls = env.kernel_timing_read()
     kms = {k: v * kcalls / K for k, v in kms.items()}  # per step (a persistent rollout launch spans many)
     env.kernel_timing(0)
@@ -542,14 +558,24 @@ def main():
     if a.vision:  # k_dense_vis: read the C-order dose row, write the lungs and dose channels
         bytes_launch = a.envs * 12 * V
         bytes_model = "12 B x V x envs (k_dense_vis: dose read, two observation channels written)"
-    dense_ms = kms["k_dense"]  # per step: the launches of all env groups
-    launches = max(kcalls, 1) / K  # k_dense launches per step (2: pipelined env groups)
-    achieved = bytes_launch / (dense_ms * 1e-3)  # = per-launch bytes / per-launch duration
-    if launches > 1.5:  # pipelined: k_dense_persist over half the envs (tools/gpu_dense_persist_pmc.sh)
-        traffic = load_pmc(grid, a.envs // 2, "k_dense_persist")
-    else:  # whole-handle grid launches (tools/gpu_dense_pmc.sh, bench.py --env-only)
-        traffic = load_pmc(grid, a.envs)
-    roof = {"bound": "hbm", "kernel": "k_dense", "achieved": achieved / 1e9,
+    persistent_dense = (not a.vision and not a.env_only and a.step_mode == "dense" and a.rollout_groups == 0)
+    launches = max(kcalls, 1) / K  # launches per step (2: pipelined env groups; 1/K: one persistent launch)
+    if persistent_dense:
+        # one k_rollout_policy<dense> launch per rollout call: each wave streams
+        # its env's lung segment every step (dense_env); its whole duration is
+        # in the first interval, and its bytes are the dense stream's
+        dense_ms = sum(kms.values())
+        kernel_name = "k_rollout_policy<dense>"
+        traffic = load_pmc(grid, a.envs, "k_rollout_policy")
+    else:
+        dense_ms = kms["k_dense"]  # per step: the launches of all env groups
+        kernel_name = "k_dense"
+        if launches > 1.5:  # pipelined: k_dense_persist over half the envs (tools/gpu_dense_persist_pmc.sh)
+            traffic = load_pmc(grid, a.envs // 2, "k_dense_persist")
+        else:  # whole-handle grid launches (tools/gpu_dense_pmc.sh, bench.py --env-only)
+            traffic = load_pmc(grid, a.envs)
+    achieved = bytes_launch / (dense_ms * 1e-3)  # = per-launch bytes / per-launch duration (per step)
+    roof = {"bound": "hbm", "kernel": kernel_name, "achieved": achieved / 1e9,
             "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
             "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch / launches,
             "kernel_ms": dense_ms / launches, "launches_per_step": launches, "k_dense_ms_per_step": dense_ms,
@@ -564,6 +590,7 @@ def main():
                             "kernel_ms_all": iso, "note": "k_dense over all envs, one launch per step, "
                                                           "nothing co-running (one-group pass)"}
     roof["step_frac_of_hbm"] = a.envs * 4 * Vl / (dt / K) / HBM_PEAK if not a.vision else None
+    roof["timed_pass_ms_per_step"] = 1000 * dt_timed / K  # the instrumented pass (kernel times above)
     if rank == 0 and not a.env_only:
         cbw = copy_ceiling(dev)
         roof["measured_copy_ceiling_GBps"] = cbw / 1e9

@@ -270,8 +270,11 @@ typedef struct rt_policy_rollout {
 
 int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* obs_d, uint8_t* terminated_d,
                           void* stream);
-/* Env groups of the dense-mode rt_env_rollout_policy: 2 (default, two
- * pipelined library streams) or 1 (every launch on the caller's stream). */
+/* Env groups of the dense-mode rt_env_rollout_policy: 2 (two pipelined
+ * library streams), 1 (every launch on the caller's stream) or 0 (one
+ * persistent launch: each env's wave runs policy, march, the dense lung
+ * reduction of its own row and the finish, step after step; the launch
+ * returns RT_ELIMIT when the library's largest tumour does not fit). */
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:

@@ -49,7 +49,10 @@ constexpr int kStepThreads = 256;
 #ifndef RT_SLICE_VEC
 #define RT_SLICE_VEC 8192
 #endif
-constexpr int kUnroll = RT_DENSE_UNROLL;  // float4 loads in flight per thread
+constexpr int kUnroll = RT_DENSE_UNROLL;
+#ifndef RT_PDENSE_U
+#define RT_PDENSE_U 4  // persistent dense rollout: float4 loads per lane per register set (two sets)
+#endif  // float4 loads in flight per thread
 constexpr int kSliceVec = RT_SLICE_VEC;   // k_dense slice: 8192 float4 = 128 KiB of dose
 constexpr int kMaxTumourVoxels = 16384;  // tumour voxels (op slots n + n-1 < 2^16; k_finish LDS per wave)
 constexpr int kMaxGridDim = 1024;
@@ -411,6 +414,7 @@ struct BeamParams {
     int32_t e_begin;              //   (an env group of the pipelined dense rollout)
     int32_t is_reset_call;
     int32_t incremental;          // RT_STEP_INCREMENTAL (visionless only)
+    int32_t zero_reset;           // the env's own wave zeroes its row on RESET (persistent rollouts)
     uint64_t seed;
     int64_t env_id_base;
 };
@@ -509,7 +513,7 @@ __device__ __forceinline__ float rfl_f(float x) {
 // (read from P.actions).
 // act: the env's 6 action floats in registers (fused policy step) or null
 // (read from P.actions).
-__device__ void beam_env(const BeamParams& P, int e, int lane, const float* act) {
+__device__ int beam_env(const BeamParams& P, int e, int lane, const float* act) {
     BeamSetup s{};
     if (lane == 0) {
         RT_STAMP(e, 2);
@@ -520,8 +524,9 @@ __device__ void beam_env(const BeamParams& P, int e, int lane, const float* act)
     }
     if (lane == 0) RT_STAMP(e, 12);
     const int mode = rfl_i(s.mode);
-    if (P.incremental && mode == MODE_RESET) {
-        // reset_dose (environment.py:104) for the incremental step: k_dense is not run
+    if ((P.incremental || P.zero_reset) && mode == MODE_RESET) {
+        // reset_dose (environment.py:104) when no k_dense runs (incremental step,
+        // persistent rollouts): the env's own wave zeroes its row
         typedef float nf4 __attribute__((ext_vector_type(4)));
         nf4* d4 = reinterpret_cast<nf4*>(P.st.dose + (size_t)e * P.G.Vpad);
         const nf4 z = {0.f, 0.f, 0.f, 0.f};
@@ -531,9 +536,9 @@ __device__ void beam_env(const BeamParams& P, int e, int lane, const float* act)
             P.st.lung_cnt[e] = 0;
             P.st.lung_sum[e] = 0.0;
         }
-        return;
+        return mode;
     }
-    if (mode != MODE_STEP) return;
+    if (mode != MODE_STEP) return mode;
     BeamSetup b;
     b.niter = rfl_i(s.niter);
     b.start = rfl_i(s.start);
@@ -546,7 +551,7 @@ __device__ void beam_env(const BeamParams& P, int e, int lane, const float* act)
     b.sgy = rfl_f(s.sgy);
     b.sgz = rfl_f(s.sgz);
     const int niter = b.niter;
-    if (niter <= 0) return;  // (incremental counters unchanged: the beam missed the box)
+    if (niter <= 0) return mode;  // (incremental counters unchanged: the beam missed the box)
     float* dose = P.st.dose + (size_t)e * P.G.Vpad;
     const float bd = P.C.beam_dose;
     const bool pairs = b.dom != 0;
@@ -614,6 +619,7 @@ __device__ void beam_env(const BeamParams& P, int e, int lane, const float* act)
         }
     }
     if (lane == 0) RT_STAMP(e, 4);
+    return mode;
 }
 
 __global__ __launch_bounds__(256) void k_beam(BeamParams P) {
@@ -959,6 +965,7 @@ struct FinishParams {
     uint32_t hash_mask;  // vision: beam-view hash slots - 1
     int32_t wave_lds;    // bytes of LDS per wave
     int32_t wpb;         // envs (waves) per block: 4, or fewer when big tumours need the LDS
+    int32_t lung_n;      // lung-first rows: # lung voxels (persistent dense rollout: the wave's stream)
 };
 
 __device__ __forceinline__ void write_obs9(float* obs, const Geom& G, int e, const double* pose,
@@ -1295,6 +1302,62 @@ __global__ __launch_bounds__(1024) void k_step_policy(BeamParams B, FinishParams
 }
 
 // ---------------------------------------------------------------------------
+// dense_env: k_dense's reductions for ONE env by its own wave (the persistent
+// dense rollout): count(dose > 0.2) and the f64 sum over the lung segment of
+// the env's lung-first row (the first lung_n floats), written to the env's
+// lung_cnt / lung_sum, which finish_env then reads as in incremental mode.
+// 8 non-temporal 16-B loads in flight per lane; the 4096 waves of a launch
+// keep ~32 MB of loads in flight.  The count is an exact integer (rewards and
+// termination are those of k_dense bit for bit); the sum (info doses.lung)
+// rounds in another order than k_dense's slices.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void dense_env(const FinishParams& P, int e, int lane) {
+    constexpr int U = RT_PDENSE_U;
+    const float4* d4 = reinterpret_cast<const float4*>(P.st.dose + (size_t)e * P.G.Vpad);
+    const int n = P.lung_n;
+    const int nq = (n + 3) >> 2;
+    const float thr = P.C.lung_thr;
+    int cnt = 0;
+    double lsum = 0.0;
+    auto fetch = [&](float4 (&v)[U], int base) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = base + u * 64 + lane;
+            v[u] = q < nq ? load_nt(&d4[q]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto consume = [&](const float4 (&v)[U], int base) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = base + u * 64 + lane;
+            float4 x = v[u];
+            if (4 * q + 3 >= n) {  // the segment's last float4 may hold non-lung voxels
+                if (4 * q + 1 >= n) x.y = 0.0f;
+                if (4 * q + 2 >= n) x.z = 0.0f;
+                x.w = 0.0f;
+            }
+            cnt += (x.x > thr ? 1 : 0) + (x.y > thr ? 1 : 0) + (x.z > thr ? 1 : 0) + (x.w > thr ? 1 : 0);
+            lsum += (((double)x.x + (double)x.y) + (double)x.z) + (double)x.w;
+        }
+    };
+    // two register sets: the next U loads are in flight while the current U are reduced
+    float4 va[U], vb[U];
+    fetch(va, 0);
+    for (int base = 0; base < nq; base += 128 * U) {
+        fetch(vb, base + 64 * U);
+        consume(va, base);
+        fetch(va, base + 128 * U);
+        consume(vb, base + 64 * U);
+    }
+    cnt = wave_sum_i(cnt);
+    lsum = wave_sum_d(lsum);
+    if (lane == 0) {
+        P.st.lung_cnt[e] = cnt;
+        P.st.lung_sum[e] = lsum;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_rollout_policy: n_steps rollout steps of the visionless agent in ONE
 // persistent launch (incremental step mode).  Envs never interact, so a wave
 // can run its env's whole step chain -- policy sample, pose update, march,
@@ -1323,6 +1386,7 @@ struct RolloutArgs {
     RolloutParams R;
 };
 
+template <bool DENSE>
 __global__ __launch_bounds__(1024) void k_rollout_policy(RolloutArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     rtpol::Lds& L = *reinterpret_cast<rtpol::Lds*>(rsm);
@@ -1388,10 +1452,17 @@ __global__ __launch_bounds__(1024) void k_rollout_policy(RolloutArgs A) {
         float a6[rtpol::NACT];
 #pragma unroll
         for (int i = 0; i < rtpol::NACT; ++i) a6[i] = rtpol::lane_f(smp.action, i);
-        beam_env(B, e, lane, a6);
+        const int mode = beam_env(B, e, lane, a6);
         // this wave's dose stores are visible to its own lanes' loads below
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if constexpr (DENSE) {
+            if (mode == MODE_STEP) {
+                dense_env(F, e, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+        }
         FinishParams Ft = F;
+        if constexpr (DENSE) Ft.incremental = 1;  // the counts dense_env just wrote
         Ft.reward = R.reward_store + (size_t)t * N;
         Ft.info = R.info_store ? R.info_store + (size_t)t * N * RT_INFO_W : nullptr;
         finish_env(Ft, e, lane, fin);
@@ -1983,7 +2054,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         const int wpb = 16;
         const size_t per_wave = (160 * 1024 - off) / wpb / 16 * 16;
         const int cap = (int)((per_wave - kMaxPlanLevels * sizeof(int32_t)) / (3 * sizeof(float)));
-        if (env->incremental && env->visionless && per_wave >= rtpol::H * sizeof(float) && cap >= 1) {
+        if (env->visionless && per_wave >= rtpol::H * sizeof(float) && cap >= 1) {
             env->rollout_wpb = wpb;
             env->rollout_fin_off = (int)off;
             env->rollout_wave_lds = (int)per_wave;
@@ -2120,6 +2191,7 @@ FinishParams finish_params(const rt_env* env, float* obs, float* reward, uint8_t
     fp.hash_mask = env->view_hash_mask;
     fp.wave_lds = env->finish_wave_lds;
     fp.wpb = env->finish_wpb;
+    fp.lung_n = env->lung_n;
     return fp;
 }
 
@@ -2342,24 +2414,17 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
 }
 
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups) {
-    if (!env || groups < 1 || groups > 2) return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups must be 1 or 2");
+    if (!env || groups < 0 || groups > 2) return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups must be 0, 1 or 2");
     env->rollout_groups = groups;
     return RT_OK;
 }
 
-int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
-                          void* stream) {
-    if (!env || !r || !obs_d || !terminated_d || !r->reward_store) return fail(RT_EINVAL, "NULL argument");
+// One persistent launch for the whole rollout: k_rollout_policy<false>
+// (incremental step mode) or <true> (dense mode, rollout groups 0: each wave
+// streams its env's lung segment after the march, dense_env).
+static int rollout_persistent(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
+                              hipStream_t s) {
     const rt_policy_step* ps = &r->step;
-    if (!ps->params || !ps->obs_in || !ps->obs_store || !ps->done_store || !ps->act_store || !ps->logp_store ||
-        !ps->value_store)
-        return fail(RT_EINVAL, "NULL argument");
-    if (!env->visionless) return fail(RT_EINVAL, "rt_env_rollout_policy: the fused policy is the visionless MLP");
-    if (ps->n_params != rtpol::kTensors) return fail(RT_EINVAL, "rt_env_rollout_policy: expected 13 parameter tensors");
-    if (r->n_steps < 1) return fail(RT_EINVAL, "rt_env_rollout_policy: n_steps < 1");
-    if (!env->incremental) return rollout_dense(env, r, obs_d, terminated_d, as_stream(stream));
-    if (env->rollout_wpb == 0)
-        return fail(RT_ELIMIT, "rt_env_rollout_policy: policy + finish scratch exceed LDS (largest tumour too big)");
     RolloutParams R{};
     PolicyStepParams& Q = R.q;
     for (int i = 0; i < rtpol::kTensors; ++i) {
@@ -2381,24 +2446,46 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d,
     R.info_store = r->info_store;
     R.n_steps = r->n_steps;
     R.fin_off = env->rollout_fin_off;
-    hipStream_t s = as_stream(stream);
     hipEvent_t* ev = next_timing_slot(env);
     if (ev) (void)hipEventRecord(ev[0], s);
     BeamParams bp = beam_params(env, false, nullptr, nullptr, nullptr);
+    bp.zero_reset = 1;
     FinishParams fp = finish_params(env, obs_d, nullptr, terminated_d, nullptr);
     fp.max_tvox = env->rollout_cap;
     fp.wave_lds = env->rollout_wave_lds;
     fp.gscratch = env->gscratch;
     fp.gscratch_stride = 2 * (int64_t)env->max_tvox;
-    static bool big = false;
-    allow_lds(reinterpret_cast<const void*>(&k_rollout_policy), big);
     const dim3 grid((env->N + Q.wpb - 1) / Q.wpb), block(64 * Q.wpb);
     RolloutArgs A{bp, fp, R};
-    hipLaunchKernelGGL(k_rollout_policy, grid, block, env->rollout_smem, s, A);
+    if (env->incremental) {
+        static bool big = false;
+        allow_lds(reinterpret_cast<const void*>(&k_rollout_policy<false>), big);
+        hipLaunchKernelGGL(k_rollout_policy<false>, grid, block, env->rollout_smem, s, A);
+    } else {
+        static bool big = false;
+        allow_lds(reinterpret_cast<const void*>(&k_rollout_policy<true>), big);
+        hipLaunchKernelGGL(k_rollout_policy<true>, grid, block, env->rollout_smem, s, A);
+    }
     RT_LAUNCH_CHECK("k_rollout_policy");
     if (ev)
         for (int k = 1; k < 4; ++k) (void)hipEventRecord(ev[k], s);
     return RT_OK;
+}
+
+int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
+                          void* stream) {
+    if (!env || !r || !obs_d || !terminated_d || !r->reward_store) return fail(RT_EINVAL, "NULL argument");
+    const rt_policy_step* ps = &r->step;
+    if (!ps->params || !ps->obs_in || !ps->obs_store || !ps->done_store || !ps->act_store || !ps->logp_store ||
+        !ps->value_store)
+        return fail(RT_EINVAL, "NULL argument");
+    if (!env->visionless) return fail(RT_EINVAL, "rt_env_rollout_policy: the fused policy is the visionless MLP");
+    if (ps->n_params != rtpol::kTensors) return fail(RT_EINVAL, "rt_env_rollout_policy: expected 13 parameter tensors");
+    if (r->n_steps < 1) return fail(RT_EINVAL, "rt_env_rollout_policy: n_steps < 1");
+    if (!env->incremental && env->rollout_groups > 0) return rollout_dense(env, r, obs_d, terminated_d, as_stream(stream));
+    if (env->rollout_wpb == 0)
+        return fail(RT_ELIMIT, "rt_env_rollout_policy: policy + finish scratch exceed LDS (largest tumour too big)");
+    return rollout_persistent(env, r, obs_d, terminated_d, as_stream(stream));
 }
 
 int rt_env_kernel_timing(rt_env* env, int32_t capacity) {
