@@ -50,6 +50,14 @@ constexpr int kStepThreads = 256;
 #define RT_SLICE_VEC 8192
 #endif
 constexpr int kUnroll = RT_DENSE_UNROLL;
+// Library events order work between the library's own streams on one device
+// (the pipelined rollout's fork / turns / join) or time kernels; neither needs
+// the system-scope release + acquire (L2 writeback and invalidate) a default
+// event record performs.  Kernel boundaries keep their device-scope release.
+#ifndef RT_EVENT_SYSFENCE
+#define RT_EVENT_SYSFENCE 0
+#endif
+constexpr unsigned kEventNoSysFence = RT_EVENT_SYSFENCE ? 0u : hipEventDisableSystemFence;
 #ifndef RT_PDENSE_U
 #define RT_PDENSE_U 4  // persistent dense rollout: float4 loads per lane per register set (two sets)
 #endif  // float4 loads in flight per thread
@@ -2130,7 +2138,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
                 return fail(RT_EDEVICE, "hipStreamCreateWithFlags failed");
             }
         for (hipEvent_t& ev : env->pev)
-            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming | kEventNoSysFence) != hipSuccess) {
                 free_env(env);
                 return fail(RT_EDEVICE, "hipEventCreateWithFlags failed");
             }
@@ -2496,7 +2504,7 @@ int rt_env_kernel_timing(rt_env* env, int32_t capacity) {
     env->timing_n = 0;
     if (capacity == 0) return RT_OK;
     env->tev.resize((size_t)4 * capacity);
-    for (auto& e : env->tev) RT_HIP(hipEventCreate(&e));
+    for (auto& e : env->tev) RT_HIP(hipEventCreateWithFlags(&e, kEventNoSysFence));
     env->timing_cap = capacity;
     return RT_OK;
 }
