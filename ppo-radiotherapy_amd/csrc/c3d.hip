@@ -378,7 +378,13 @@ __global__ __launch_bounds__(conv_threads<CIN>()) void k_conv_relu_pool(FwdParam
 // ring wrap too: 6 slots), so the 32 lanes of a ds_read (16 positions x 2
 // channels) hit 32 banks.
 constexpr int kRing = 6;
-constexpr int kRingMaxPieces = 12;  // DMA pieces per wave and slot (registers)
+// DMA pieces per wave and slot (one source offset register each): conv1's
+// 16-B pieces need 2 per wave at 64^3 and 128^3; 4-B pieces up to 8 (conv1
+// on unaligned rows) or 12 (16-channel slots)
+template <int CIN, int VEC>
+constexpr int ring_max_pieces() {
+    return VEC == 4 ? 2 : (CIN == 4 ? 8 : 12);
+}
 
 struct RingGeom {
     Geom g;            // dims, pool padding, XT; YL, XL, YS; CS = channel stride
@@ -429,7 +435,8 @@ RingGeom make_ring_geom(const rt_conv_layer* L, int B, int nthreads) {
 // feed masked positions only, and stay finite for the backward).
 template <int CIN, int VEC, int NW>
 struct RingLoader {
-    int goff[kRingMaxPieces];  // per piece: offset within a plane of channel 0
+    static constexpr int MP = ring_max_pieces<CIN, VEC>();
+    int goff[MP];              // per piece: offset within a plane of channel 0
     int npw;                   // pieces of this wave
 
     __device__ __forceinline__ void init(const RingGeom& rg, int y0, int x0, int wave, int lane) {
@@ -437,7 +444,7 @@ struct RingLoader {
         const int plane = g.H * g.W;
         npw = (rg.npiece - wave + NW - 1) / NW;
 #pragma unroll
-        for (int i = 0; i < kRingMaxPieces; ++i) {
+        for (int i = 0; i < MP; ++i) {
             int f = ((wave + NW * i) * 64 + lane) * VEC;
             f = min(f, rg.SLOT - VEC);
             int ci = f / g.CS;
@@ -474,7 +481,7 @@ struct RingLoader {
         const Geom& g = rg.g;
         const int iz = min(max(t - g.pd, 0), g.D - 1);
         pieces(xb + (size_t)iz * g.H * g.W, xs + slot * rg.SLOT, wave, lane, rg.SLOT,
-               std::make_integer_sequence<int, kRingMaxPieces>{});
+               std::make_integer_sequence<int, MP>{});
     }
 };
 
@@ -677,7 +684,9 @@ int launch_fwd_ring(const rt_conv_layer* L, int32_t B, const float* x, const int
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     auto fits = [&](const RingGeom& rg, int vec) {
         return (size_t)kRing * rg.SLOT * sizeof(float) <= budget &&
-               (rg.npiece + NTH / 64 - 1) / (NTH / 64) <= kRingMaxPieces && rg.g.W >= vec;
+               (rg.npiece + NTH / 64 - 1) / (NTH / 64) <= (vec == 4 ? ring_max_pieces<CIN, 4>()
+                                                                   : ring_max_pieces<CIN, 1>()) &&
+               rg.g.W >= vec;
     };
     constexpr int PY_BIG = CIN == 4 ? 4 : 2;
     if constexpr (CIN == 4) {
@@ -1227,7 +1236,9 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     auto fits = [&](const RingGeom& rg, int vec) {
         const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * CO * NCT * 16) * sizeof(float);
-        return lds <= budget && (rg.npiece + kThreads / 64 - 1) / (kThreads / 64) <= kRingMaxPieces &&
+        return lds <= budget &&
+               (rg.npiece + kThreads / 64 - 1) / (kThreads / 64) <=
+                   (vec == 4 ? ring_max_pieces<CIN, 4>() : ring_max_pieces<CIN, 1>()) &&
                (rg.g.PYB_tiles + WP - 1) / WP <= kWgMaxTiles && rg.g.W >= vec;
     };
     int rc = RT_ELIMIT, nblk = 0;
