@@ -108,7 +108,7 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=0)
     ap.add_argument("--step-mode", choices=["dense", "incremental"], default="dense",
                     help="env step formulation measured as `value` (the other is reported beside it)")
-    ap.add_argument("--rollout-groups", type=int, default=2, choices=[0, 1, 2],
+    ap.add_argument("--rollout-groups", type=int, default=2, choices=[0, 1, 2, 3, 4],
                     help="dense mode: env groups of the rollout call (2 = two pipelined streams, "
                          "0 = one persistent launch with a per-env dense pass)")
     ap.add_argument("--update-minibatches", type=int, default=0,

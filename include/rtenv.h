@@ -270,8 +270,9 @@ typedef struct rt_policy_rollout {
 
 int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* obs_d, uint8_t* terminated_d,
                           void* stream);
-/* Env groups of the dense-mode rt_env_rollout_policy: 2 (two pipelined
- * library streams), 1 (every launch on the caller's stream) or 0 (one
+/* Env groups of the dense-mode rt_env_rollout_policy: 2..4 (pipelined
+ * library streams taking turns on k_dense in a ring; default 2), 1 (every
+ * launch on the caller's stream) or 0 (one
  * persistent launch: each env's wave runs policy, march, the dense lung
  * reduction of its own row and the finish, step after step; the launch
  * returns RT_ELIMIT when the library's largest tumour does not fit). */

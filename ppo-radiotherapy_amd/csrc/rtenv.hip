@@ -1701,6 +1701,8 @@ struct PlanBuilder {
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
+constexpr int kMaxRolloutGroups = 4;
+
 struct rt_env {
     int device = 0;
     int N = 0;
@@ -1745,8 +1747,8 @@ struct rt_env {
     // groups on two library streams; events fork, hand the k_dense turn from
     // one group to the other, join
     int rollout_groups = 2;  // DESIGN.md §3 "Pipelined dense rollout"
-    hipStream_t pipe[2] = {nullptr, nullptr};
-    hipEvent_t pev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // fork, dense[2], join[2]
+    hipStream_t pipe[kMaxRolloutGroups] = {};
+    hipEvent_t pev[1 + 2 * kMaxRolloutGroups] = {};  // fork, dense[G], join[G]
     std::vector<void*> allocs;
 };
 
@@ -2354,16 +2356,21 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
                          hipStream_t s) {
     const rt_policy_step* ps = &r->step;
     const int N = env->N;
-    const bool two = env->rollout_groups > 1 && env->pipe[0] && N >= 32;
-    const int wpb = two ? env->pipe_wpb : env->fused_wpb;
-    const size_t smem = two ? env->pipe_smem : env->fused_smem;
-    const int h = two ? (N / 2 + wpb - 1) / wpb * wpb : N;  // group boundary on a block boundary
-    const int bounds[3] = {0, h, N};
-    const int G = two ? 2 : 1;
-    hipStream_t S[2] = {s, s};
-    if (two) {
+    int G = env->pipe[0] ? env->rollout_groups : 1;
+    while (G > 1 && N < 16 * G) --G;
+    const bool piped = G > 1;
+    const int wpb = piped ? env->pipe_wpb : env->fused_wpb;
+    const size_t smem = piped ? env->pipe_smem : env->fused_smem;
+    // group boundaries on block boundaries
+    int bounds[kMaxRolloutGroups + 1];
+    for (int g = 0; g <= G; ++g) bounds[g] = g == G ? N : (int)((int64_t)N * g / G / wpb * wpb);
+    hipStream_t S[kMaxRolloutGroups];
+    hipEvent_t* dense_ev = env->pev + 1;
+    hipEvent_t* join_ev = env->pev + 1 + kMaxRolloutGroups;
+    for (int g = 0; g < G; ++g) S[g] = s;
+    if (piped) {
         RT_HIP(hipEventRecord(env->pev[0], s));
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < G; ++g) {
             S[g] = env->pipe[g];
             RT_HIP(hipStreamWaitEvent(S[g], env->pev[0], 0));
         }
@@ -2378,6 +2385,10 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
     Q.seed = ps->seed;
     Q.id_base = ps->env_id_base;
     Q.wpb = wpb;
+    static const bool serial = [] {
+        const char* v = std::getenv("RT_PIPE_SERIAL");  // experiments: 0 = no k_dense turns
+        return !(v && v[0] == '0');
+    }();
     const size_t Nn = (size_t)N;
     for (int t = 0; t < r->n_steps; ++t) {
         Q.obs_in = t == 0 ? ps->obs_in : obs_d;
@@ -2401,28 +2412,26 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
             hipLaunchKernelGGL(k_step_policy<false>, dim3((e1 - e0 + wpb - 1) / wpb), dim3(64 * wpb), smem,
                                S[g], bp, fp, Q);
             RT_LAUNCH_CHECK("k_step_policy");
-            // k_dense turns: group 0 of step t after group 1 of step t-1, group 1 after group 0
-            static const bool serial = [] {
-                const char* v = std::getenv("RT_PIPE_SERIAL");  // experiments: 0 = no k_dense turns
-                return !(v && v[0] == '0');
-            }();
-            hipEvent_t wait = (two && serial && (t > 0 || g == 1)) ? env->pev[1 + (1 - g)] : nullptr;
+            // k_dense turns in a ring: group g of step t after group g-1 of step t
+            // (group 0 after group G-1 of step t-1)
+            hipEvent_t wait = (piped && serial && (t > 0 || g > 0)) ? dense_ev[(g + G - 1) % G] : nullptr;
             int rc = launch_dense_finish(env, obs_d, rew, terminated_d, info, S[g], ev, e0, e1, wait,
-                                         two ? env->pev[1 + g] : nullptr, two ? env->pipe_dense_bpc : 0);
+                                         piped ? dense_ev[g] : nullptr, piped ? env->pipe_dense_bpc : 0);
             if (rc) return rc;
         }
     }
-    if (two) {
-        for (int g = 0; g < 2; ++g) {
-            RT_HIP(hipEventRecord(env->pev[3 + g], S[g]));
-            RT_HIP(hipStreamWaitEvent(s, env->pev[3 + g], 0));
+    if (piped) {
+        for (int g = 0; g < G; ++g) {
+            RT_HIP(hipEventRecord(join_ev[g], S[g]));
+            RT_HIP(hipStreamWaitEvent(s, join_ev[g], 0));
         }
     }
     return RT_OK;
 }
 
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups) {
-    if (!env || groups < 0 || groups > 2) return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups must be 0, 1 or 2");
+    if (!env || groups < 0 || groups > kMaxRolloutGroups)
+        return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups must be 0 (persistent) or 1..4");
     env->rollout_groups = groups;
     return RT_OK;
 }

@@ -174,7 +174,7 @@ class RadiotherapyVecEnv:
         return rc
 
     def set_rollout_groups(self, groups: int):
-        """Env groups of the dense-mode rollout_policy: 2 (default, pipelined streams) or 1."""
+        """Env groups of the dense-mode rollout_policy: 2..4 (pipelined streams; default 2), 1 or 0 (persistent)."""
         _lib.check(self._L.rt_env_set_rollout_groups(self._h, int(groups)), "rt_env_set_rollout_groups")
 
     def set_next_tumours(self, ids):

@@ -80,7 +80,8 @@ def _compare(a, b, it, loose_dose_lung=False):
 
 @pytest.mark.parametrize("step_mode,big,groups", [("incremental", 0, 0), ("incremental", 1000, 0),
                                                    ("incremental", 12000, 0), ("dense", 0, 2),
-                                                   ("dense", 1000, 2), ("dense", 0, 1), ("dense", 0, 0),
+                                                   ("dense", 1000, 2), ("dense", 0, 3), ("dense", 1000, 4),
+                                                   ("dense", 0, 1), ("dense", 0, 0),
                                                    ("dense", 12000, 0)])
 def test_rollout_call_is_bitwise_the_stepwise_rollout(step_mode, big, groups):
     from ppo_radiotherapy_amd import assets
@@ -130,7 +131,7 @@ def test_rollout_policy_rejects_vision_and_bad_groups():
     tr.reset()
     ro = tr._rollout_struct(0, 4)
     with pytest.raises(_lib.RtError, match="groups"):
-        env.set_rollout_groups(3)
+        env.set_rollout_groups(5)
     with pytest.raises(_lib.RtError, match="groups"):
         env.set_rollout_groups(-1)
     env.close()
