@@ -560,8 +560,9 @@ def main():
     bytes_launch = a.envs * 4 * Vl
     bytes_model = f"4 B x {Vl} lung voxels x envs (lung-first dose rows; {Vl / V:.3f} of the volume)"
     if a.vision:  # k_dense_vis: read the C-order dose row, write the lungs and dose channels
-        bytes_launch = a.envs * 12 * V
-        bytes_model = "12 B x V x envs (k_dense_vis: dose read, two observation channels written)"
+        bytes_launch = a.envs * 20 * V
+        bytes_model = ("20 B x V x envs (k_dense_vis: dose read, the four observation channels written -- "
+                       "lungs and dose, tumour and beam-view zeroed for k_finish's scatter)")
     persistent_dense = (not a.vision and not a.env_only and a.step_mode == "dense" and a.rollout_groups == 0)
     launches = max(kcalls, 1) / K  # launches per step (2: pipelined env groups; 1/K: one persistent launch)
     if persistent_dense:
