@@ -394,7 +394,11 @@ constexpr int NPAIR = MT / 128;
 constexpr int WP = 68;    // LDS row stride of W2 (b128 fragment reads 2-way, b32 reads conflict-free)
 constexpr int W1P = 12;   // augmented W1 row: 9 weights, bias, 2 zeros
 constexpr int SP = 24;    // scratch row stride (16 samples + pad: b128 reads conflict-free)
-constexpr int SCR = 152;  // scratch rows per wave: A 0..63, B 64..127, X^T 128..143, GM^T 144..151
+constexpr int SCR = 136;  // scratch rows per wave: A 0..63, B 64..127, GM^T 128..135
+// per-wave tile inputs, copied from the minibatch rows by LDS DMA one tile
+// ahead, [column][16 samples]: obs^T [9][16] at 0; actor: actions^T [6][16] at
+// 144, logp at 240, adv at 256; critic: returns at 144, values at 160
+constexpr int IN_OBS = 0, IN_ACT = 144, IN_LOGP = 240, IN_ADV = 256, IN_RET = 144, IN_VAL = 160, IN_FLOATS = 272;
 constexpr int kMaxGradBlocks = 256;
 
 struct MfmaLds {
@@ -406,6 +410,7 @@ struct MfmaLds {
     float ls[8];
     float isd[8];  // 1 / exp(logstd), [6]: 1 / (adv std + 1e-8)
     float scr[MT / 64][SCR * SP];
+    float in[MT / 64][IN_FLOATS];
 };
 static_assert(sizeof(MfmaLds) <= 160 * 1024, "LDS");
 constexpr int kW2Region = 2 * H * H;    // reduction phase 1: both W2 of one pair
@@ -450,12 +455,49 @@ __device__ __forceinline__ int rest_slot(int p) {
 }
 constexpr int kRestDump = 1875;
 
+typedef __attribute__((address_space(1))) void* glb_ptr_t;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Copy the inputs of tile t (16 minibatch rows: obs, and the actor's actions,
+// logp, adv or the critic's returns, values) into the wave's `in` buffer with
+// async global->LDS loads (no VGPRs; completion by vmcnt).  The buffer is
+// sample-minor ([column][16 samples]), so lane l always copies sample l & 15
+// and needs one row index.  Samples past the minibatch read row 0: finite,
+// and their loss terms are masked by `live`.
+template <int HEAD>
+__device__ __forceinline__ void mf_prefetch(const GradParams& P, float* in, int t, int lane) {
+    const int m = t * 16 + (lane & 15), hi = lane >> 4;
+    const int64_t r = m < P.mb ? P.idx[m] : 0;
+    const float* ob = P.obs + r * NOBS + hi;
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)ob, (lds_ptr_t)(in + IN_OBS), 4, 0, 0);             // columns 0..3
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)(ob + 4), (lds_ptr_t)(in + IN_OBS + 64), 4, 0, 0);  // 4..7
+    if (lane < 16) __builtin_amdgcn_global_load_lds((glb_ptr_t)(ob + 8), (lds_ptr_t)(in + IN_OBS + 128), 4, 0, 0);
+    if constexpr (HEAD == 0) {
+        const float* ac = P.act + r * NACT + hi;
+        __builtin_amdgcn_global_load_lds((glb_ptr_t)ac, (lds_ptr_t)(in + IN_ACT), 4, 0, 0);  // columns 0..3
+        if (lane < 32) {
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(ac + 4), (lds_ptr_t)(in + IN_ACT + 64), 4, 0, 0);  // 4, 5
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(lane < 16 ? P.logp + r : P.adv + r),
+                                             (lds_ptr_t)(in + IN_LOGP), 4, 0, 0);
+        }
+    } else {
+        if (lane < 32)
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(lane < 16 ? P.ret + r : P.val + r), (lds_ptr_t)(in + IN_RET),
+                                             4, 0, 0);
+    }
+}
+
+// X^T of the augmented first layer (row NOBS = the bias input 1, rows above 0)
+__device__ __forceinline__ float xin(const float* in, int row, int smp) {
+    return row < NOBS ? in[IN_OBS + row * 16 + smp] : (row == NOBS ? 1.0f : 0.0f);
+}
+
 // forward of this wave's trunk for its tile: h1, h2 = tanh layers, transposed tiles
-__device__ __forceinline__ void mf_fwd(const MfmaLds& S, int h, const float* Xs, int c, int g, f4 h1[4], f4 h2[4]) {
+__device__ __forceinline__ void mf_fwd(const MfmaLds& S, int h, const float* in, int c, int g, f4 h1[4], f4 h2[4]) {
 #pragma clang fp contract(fast)
     float xb[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) xb[q] = Xs[(4 * q + g) * SP + c];
+    for (int q = 0; q < 3; ++q) xb[q] = xin(in, 4 * q + g, c);
 #pragma unroll
     for (int J = 0; J < 4; ++J) {
         f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -492,20 +534,22 @@ struct Acc {
 };
 
 template <int HEAD>
-__device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, float* A, float* Bs, float* Xs,
-                                        float* GMs, int c, int g, int t, float inv_n, Acc<HEAD>& acc) {
+__device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, float* A, float* Bs, float* in,
+                                        float* GMs, int c, int g, int t, int t_next, float inv_n, Acc<HEAD>& acc) {
 // the update is not bit-exact against torch anyway (MFMA f32 sums, tanh_fast): let the VALU
 // products fuse (the file builds with -ffp-contract=off for the env-facing code)
 #pragma clang fp contract(fast)
     constexpr int NOUT = HEAD == 0 ? NACT : 1;
     const int m = t * 16 + c;
     const bool live = m < P.mb;
-    const int64_t row = live ? P.idx[m] : 0;
-    wave_sync();  // the previous tile's reads of the scratch are done
-    for (int i = g; i <= NOBS; i += 4) Xs[i * SP + c] = !live ? 0.0f : (i < NOBS ? P.obs[row * NOBS + i] : 1.0f);
-    wave_sync();
+    __builtin_amdgcn_s_waitcnt(0);  // this tile's inputs (LDS DMA issued during the previous tile) have landed
+    wave_sync();  // ... and the previous tile's reads of the scratch are done
     f4 h1[4], h2[4];
-    mf_fwd(S, HEAD, Xs, c, g, h1, h2);
+    mf_fwd(S, HEAD, in, c, g, h1, h2);
+    // [X | 1] operand of the dW1 product (samples 4g..4g+3 of input row c), read now: `in` is refilled below
+    float xd[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xd[k] = xin(in, c, 4 * g + k);
     // head outputs: partial dots over this lane's 16 units, summed over the sample's 4 g-lanes
     float out[NOUT];
 #pragma unroll
@@ -530,13 +574,13 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
             float z[NACT], logp = 0.0f, ent = 0.0f;
 #pragma unroll
             for (int k = 0; k < NACT; ++k) {
-                z[k] = (P.act[row * NACT + k] - out[k]) * S.isd[k];
+                z[k] = (in[IN_ACT + k * 16 + c] - out[k]) * S.isd[k];
                 logp += -0.5f * z[k] * z[k] - S.ls[k] - kHalfLog2Pi;
                 ent += 0.5f + kHalfLog2Pi + S.ls[k];
             }
-            const float lr = logp - P.logp[row];
+            const float lr = logp - in[IN_LOGP + c];
             const float r = __expf(lr);
-            float Av = P.adv[row];
+            float Av = in[IN_ADV + c];
             if (P.adv_stats) Av = (Av - P.adv_stats[0]) * S.isd[NACT];
             const float pg1 = -Av * r;
             const float rc = fminf(fmaxf(r, P.clip_lo), P.clip_hi);
@@ -562,7 +606,7 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
             }
         } else {
             const float value = out[0];
-            const float R = P.ret[row], V = P.val[row];
+            const float R = in[IN_RET + c], V = in[IN_VAL + c];
             float vl, dv;
             if (P.clip_vloss) {
                 const float d = value - V;
@@ -583,6 +627,13 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
                 acc.sc[1] += vl;
             }
         }
+    }
+    // every read of `in` for this tile is done (xd and the loss inputs are in
+    // registers): stream the next tile's inputs in beside the backward
+    if (t_next >= 0) {
+        asm volatile("" ::"v"(xd[0]), "v"(xd[1]), "v"(xd[2]), "v"(xd[3]));
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the LDS reads have returned
+        mf_prefetch<HEAD>(P, in, t_next, 16 * g + c);
     }
     // ---- dW3
     if constexpr (HEAD == 0) {
@@ -673,14 +724,13 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
         for (int r = 0; r < 4; ++r) A[(16 * J + 4 * g + r) * SP + c] = g1[J][r];
     wave_sync();
     // ---- [dW1 | db1] += G1^T . [X | 1]
-    const float4 xb = ld4(&Xs[c * SP + 4 * g]);
 #pragma unroll
     for (int J = 0; J < 4; ++J) {
         const float4 a = ld4(&A[(16 * J + c) * SP + 4 * g]);
-        acc.d1[J] = mfma4(a.x, xb.x, acc.d1[J]);
-        acc.d1[J] = mfma4(a.y, xb.y, acc.d1[J]);
-        acc.d1[J] = mfma4(a.z, xb.z, acc.d1[J]);
-        acc.d1[J] = mfma4(a.w, xb.w, acc.d1[J]);
+        acc.d1[J] = mfma4(a.x, xd[0], acc.d1[J]);
+        acc.d1[J] = mfma4(a.y, xd[1], acc.d1[J]);
+        acc.d1[J] = mfma4(a.z, xd[2], acc.d1[J]);
+        acc.d1[J] = mfma4(a.w, xd[3], acc.d1[J]);
     }
 }
 
@@ -689,8 +739,8 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
     const int c = lane & 15, g = lane >> 4;
     float* A = S.scr[2 * pair + HEAD];
     float* Bs = A + 64 * SP;
-    float* Xs = A + 128 * SP;
-    float* GMs = A + 144 * SP;
+    float* GMs = A + 128 * SP;
+    float* in = S.in[2 * pair + HEAD];
     Acc<HEAD> acc;
     const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -708,8 +758,9 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
     const int tw = blockIdx.x * (MT / 64) + 2 * pair + HEAD;  // trace row of this wave
     (void)tw;  // used by RT_STAMP in trace builds only
     int nt_done = 0;
-    for (int t = blockIdx.x * NPAIR + pair; t < ntiles; t += gridDim.x * NPAIR) {
-        mf_tile<HEAD>(S, P, A, Bs, Xs, GMs, c, g, t, inv_n, acc);
+    const int tstep = gridDim.x * NPAIR;
+    for (int t = blockIdx.x * NPAIR + pair; t < ntiles; t += tstep) {
+        mf_tile<HEAD>(S, P, A, Bs, in, GMs, c, g, t, t + tstep < ntiles ? t + tstep : -1, inv_n, acc);
         if (lane == 0 && nt_done++ == 0) RT_STAMP(tw, 6);
     }
     if (lane == 0) RT_STAMP(tw, 2);
@@ -802,6 +853,15 @@ __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
     __shared__ __attribute__((aligned(16))) MfmaLds S;
     const int tid = threadIdx.x;
     if ((tid & 63) == 0) RT_STAMP(blockIdx.x * (MT / 64) + (tid >> 6), 0);
+    {  // the first tile's inputs stream in while the parameters are staged
+        const int wave = tid >> 6, pair = wave & 3, t0 = blockIdx.x * NPAIR + pair;
+        if (t0 < (P.mb + 15) / 16) {
+            if (wave >= 4)
+                mf_prefetch<1>(P, S.in[2 * pair + 1], t0, tid & 63);
+            else
+                mf_prefetch<0>(P, S.in[2 * pair], t0, tid & 63);
+        }
+    }
     for (int i = tid; i < H * H; i += MT) {
         S.w2[0][(i >> 6) * WP + (i & 63)] = P.w.p[2][i];
         S.w2[1][(i >> 6) * WP + (i & 63)] = P.w.p[9][i];
@@ -826,15 +886,18 @@ __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
         S.b3[NACT] = P.w.p[12][0];
         S.isd[NACT] = P.adv_stats ? 1.0f / (P.adv_stats[1] + 1e-8f) : 1.0f;
     }
-    // X^T rows 10..15 stay zero (padding of the augmented K = 16)
-    for (int i = tid; i < (MT / 64) * 6 * SP; i += MT) S.scr[i / (6 * SP)][(138 + (i / SP) % 6) * SP + i % SP] = 0.0f;
     __syncthreads();
     const int wave = tid >> 6, lane = tid & 63;
     if (lane == 0) RT_STAMP(blockIdx.x * (MT / 64) + wave, 1);
-    if (wave & 1)
-        mf_wave<1>(S, P, wave >> 1, lane);
+    // waves w and w + 4 share SIMD w (a 512-thread workgroup places two waves
+    // per SIMD, in dispatch order): actors are waves 0..3, critics 4..7, so
+    // every SIMD pairs an actor with a critic -- and the heavier actor is the
+    // older wave, which wins VALU arbitration (MI355X_MICROARCH.md, two waves
+    // per SIMD).  (wave & 1 as the role put both actors of two pairs on one SIMD.)
+    if (wave >= 4)
+        mf_wave<1>(S, P, wave & 3, lane);
     else
-        mf_wave<0>(S, P, wave >> 1, lane);
+        mf_wave<0>(S, P, wave & 3, lane);
 }
 
 int grad_blocks(int mb) {
