@@ -928,24 +928,27 @@ struct ReduceParams {
     float ent_coef;
 };
 
-// block: 64 columns; wave w of 16 sums rows w, w+16, ... (2 chains); the 16
-// wave sums are combined in a fixed order (deterministic).  Also emits the
+// block: 64 columns; wave w of 16 sums rows w, w+16, ..., w+240 (all 16
+// loads in flight, then a fixed-order pairwise sum; rows past nblk add 0); the
+// 16 wave sums are combined in a fixed order (deterministic).  Also emits the
 // block's share of ||grad||^2 for the clip in k_adam.
+static_assert(kMaxGradBlocks <= 16 * 16, "k_ppo_reduce covers 256 partial rows");
 __global__ __launch_bounds__(1024) void k_ppo_reduce(ReduceParams P) {
     __shared__ float part[16][kReduceCols];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int p = blockIdx.x * kReduceCols + lane;
     const bool ok = p < NP + NSTAT;
-    float a0 = 0.0f, a1 = 0.0f;
-    if (ok) {
-        int b = w;
-        for (; b + 16 < P.nblk; b += 32) {
-            a0 += P.ws[(size_t)b * PSTRIDE + p];
-            a1 += P.ws[(size_t)(b + 16) * PSTRIDE + p];
-        }
-        if (b < P.nblk) a0 += P.ws[(size_t)b * PSTRIDE + p];
+    float x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int b = w + 16 * k;
+        x[k] = (ok && b < P.nblk) ? P.ws[(size_t)b * PSTRIDE + p] : 0.0f;
     }
-    part[w][lane] = a0 + a1;
+#pragma unroll
+    for (int h = 8; h > 0; h >>= 1)
+#pragma unroll
+        for (int k = 0; k < h; ++k) x[k] += x[k + h];
+    part[w][lane] = x[0];
     __syncthreads();
     if (w != 0) return;
     float a = 0.0f;
