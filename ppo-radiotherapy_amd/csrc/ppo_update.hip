@@ -533,24 +533,19 @@ struct Acc {
     float sc[HEAD == 0 ? 2 * NACT + 5 : 2];  // actor: db3[6], dlogstd[6], pg, ent, -lr, r-1-lr, clipped; critic: db3, vl
 };
 
+// ---- the phases of one 16-sample tile for one head (mf_tile runs them for
+// the wave's head).  LDS scratch rows are exchanged between the lanes of the
+// wave only at wave_sync points.
+#define RT_FP_FAST _Pragma("clang fp contract(fast)")
+
+// head outputs and the per-sample loss derivative w.r.t. them (train.py:200-236)
 template <int HEAD>
-__device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, float* A, float* Bs, float* in,
-                                        float* GMs, int c, int g, int t, int t_next, float inv_n, Acc<HEAD>& acc) {
-// the update is not bit-exact against torch anyway (MFMA f32 sums, tanh_fast): let the VALU
-// products fuse (the file builds with -ffp-contract=off for the env-facing code)
-#pragma clang fp contract(fast)
+__device__ __forceinline__ void ph_out_loss(const MfmaLds& S, const GradParams& P, const float* in, int c, int g,
+                                            bool live, float inv_n, const f4 h2[4], Acc<HEAD>& acc,
+                                            float go[HEAD == 0 ? NACT : 1]) {
+    RT_FP_FAST
     constexpr int NOUT = HEAD == 0 ? NACT : 1;
-    const int m = t * 16 + c;
-    const bool live = m < P.mb;
-    __builtin_amdgcn_s_waitcnt(0);  // this tile's inputs (LDS DMA issued during the previous tile) have landed
-    wave_sync();  // ... and the previous tile's reads of the scratch are done
-    f4 h1[4], h2[4];
-    mf_fwd(S, HEAD, in, c, g, h1, h2);
-    // [X | 1] operand of the dW1 product (samples 4g..4g+3 of input row c), read now: `in` is refilled below
-    float xd[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) xd[k] = xin(in, c, 4 * g + k);
-    // head outputs: partial dots over this lane's 16 units, summed over the sample's 4 g-lanes
+    // partial dots over this lane's 16 units, summed over the sample's 4 g-lanes
     float out[NOUT];
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) {
@@ -565,85 +560,86 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
         p += __shfl_xor(p, 32, 64);
         out[o] = p + S.b3[wr];
     }
-    // ---- per-sample loss derivative w.r.t. this head's outputs (train.py:200-236)
-    float go[NOUT];
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) go[o] = 0.0f;
-    if (live) {
-        if constexpr (HEAD == 0) {
-            float z[NACT], logp = 0.0f, ent = 0.0f;
+    if (!live) return;
+    if constexpr (HEAD == 0) {
+        float z[NACT], logp = 0.0f, ent = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NACT; ++k) {
+            z[k] = (in[IN_ACT + k * 16 + c] - out[k]) * S.isd[k];
+            logp += -0.5f * z[k] * z[k] - S.ls[k] - kHalfLog2Pi;
+            ent += 0.5f + kHalfLog2Pi + S.ls[k];
+        }
+        const float lr = logp - in[IN_LOGP + c];
+        const float r = __expf(lr);
+        float Av = in[IN_ADV + c];
+        if (P.adv_stats) Av = (Av - P.adv_stats[0]) * S.isd[NACT];
+        const float pg1 = -Av * r;
+        const float rc = fminf(fmaxf(r, P.clip_lo), P.clip_hi);
+        const float pg2 = -Av * rc;
+        // torch.maximum backward: the larger input takes the gradient, ties split it
+        const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+        const float w2 = pg2 > pg1 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+        const float pass = (r >= P.clip_lo && r <= P.clip_hi) ? 1.0f : 0.0f;  // clamp backward
+        const float g_logp = inv_n * (w1 * -Av + w2 * -Av * pass) * r;
+#pragma unroll
+        for (int k = 0; k < NACT; ++k) go[k] = g_logp * z[k] * S.isd[k];
+        if (g == 0) {  // one contribution per sample
 #pragma unroll
             for (int k = 0; k < NACT; ++k) {
-                z[k] = (in[IN_ACT + k * 16 + c] - out[k]) * S.isd[k];
-                logp += -0.5f * z[k] * z[k] - S.ls[k] - kHalfLog2Pi;
-                ent += 0.5f + kHalfLog2Pi + S.ls[k];
+                acc.sc[k] += go[k];
+                acc.sc[NACT + k] += g_logp * (z[k] * z[k] - 1.0f);
             }
-            const float lr = logp - in[IN_LOGP + c];
-            const float r = __expf(lr);
-            float Av = in[IN_ADV + c];
-            if (P.adv_stats) Av = (Av - P.adv_stats[0]) * S.isd[NACT];
-            const float pg1 = -Av * r;
-            const float rc = fminf(fmaxf(r, P.clip_lo), P.clip_hi);
-            const float pg2 = -Av * rc;
-            // torch.maximum backward: the larger input takes the gradient, ties split it
-            const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
-            const float w2 = pg2 > pg1 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
-            const float pass = (r >= P.clip_lo && r <= P.clip_hi) ? 1.0f : 0.0f;  // clamp backward
-            const float g_logp = inv_n * (w1 * -Av + w2 * -Av * pass) * r;
-#pragma unroll
-            for (int k = 0; k < NACT; ++k) go[k] = g_logp * z[k] * S.isd[k];
-            if (g == 0) {  // one contribution per sample
-#pragma unroll
-                for (int k = 0; k < NACT; ++k) {
-                    acc.sc[k] += go[k];
-                    acc.sc[NACT + k] += g_logp * (z[k] * z[k] - 1.0f);
-                }
-                acc.sc[2 * NACT + 0] += fmaxf(pg1, pg2);
-                acc.sc[2 * NACT + 1] += ent;
-                acc.sc[2 * NACT + 2] += -lr;
-                acc.sc[2 * NACT + 3] += (r - 1.0f) - lr;
-                acc.sc[2 * NACT + 4] += fabsf(r - 1.0f) > P.clip ? 1.0f : 0.0f;
-            }
+            acc.sc[2 * NACT + 0] += fmaxf(pg1, pg2);
+            acc.sc[2 * NACT + 1] += ent;
+            acc.sc[2 * NACT + 2] += -lr;
+            acc.sc[2 * NACT + 3] += (r - 1.0f) - lr;
+            acc.sc[2 * NACT + 4] += fabsf(r - 1.0f) > P.clip ? 1.0f : 0.0f;
+        }
+    } else {
+        const float value = out[0];
+        const float R = in[IN_RET + c], V = in[IN_VAL + c];
+        float vl, dv;
+        if (P.clip_vloss) {
+            const float d = value - V;
+            const float vc = V + fminf(fmaxf(d, -P.clip), P.clip);
+            const float vu = (value - R) * (value - R), vcc = (vc - R) * (vc - R);
+            vl = fmaxf(vu, vcc);
+            const float wu = vu > vcc ? 1.0f : (vu == vcc ? 0.5f : 0.0f);
+            const float wc = vcc > vu ? 1.0f : (vu == vcc ? 0.5f : 0.0f);
+            const float dpass = (d >= -P.clip && d <= P.clip) ? 1.0f : 0.0f;
+            dv = wu * 2.0f * (value - R) + wc * 2.0f * (vc - R) * dpass;
         } else {
-            const float value = out[0];
-            const float R = in[IN_RET + c], V = in[IN_VAL + c];
-            float vl, dv;
-            if (P.clip_vloss) {
-                const float d = value - V;
-                const float vc = V + fminf(fmaxf(d, -P.clip), P.clip);
-                const float vu = (value - R) * (value - R), vcc = (vc - R) * (vc - R);
-                vl = fmaxf(vu, vcc);
-                const float wu = vu > vcc ? 1.0f : (vu == vcc ? 0.5f : 0.0f);
-                const float wc = vcc > vu ? 1.0f : (vu == vcc ? 0.5f : 0.0f);
-                const float dpass = (d >= -P.clip && d <= P.clip) ? 1.0f : 0.0f;
-                dv = wu * 2.0f * (value - R) + wc * 2.0f * (vc - R) * dpass;
-            } else {
-                vl = (value - R) * (value - R);
-                dv = 2.0f * (value - R);
-            }
-            go[0] = P.vf_coef * 0.5f * inv_n * dv;
-            if (g == 0) {
-                acc.sc[0] += go[0];
-                acc.sc[1] += vl;
-            }
+            vl = (value - R) * (value - R);
+            dv = 2.0f * (value - R);
+        }
+        go[0] = P.vf_coef * 0.5f * inv_n * dv;
+        if (g == 0) {
+            acc.sc[0] += go[0];
+            acc.sc[1] += vl;
         }
     }
-    // every read of `in` for this tile is done (xd and the loss inputs are in
-    // registers): stream the next tile's inputs in beside the backward
-    if (t_next >= 0) {
-        asm volatile("" ::"v"(xd[0]), "v"(xd[1]), "v"(xd[2]), "v"(xd[3]));
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the LDS reads have returned
-        mf_prefetch<HEAD>(P, in, t_next, 16 * g + c);
-    }
-    // ---- dW3
+}
+
+// actor: GM^T -> scratch, H2^T -> A (read back after a wave_sync by ph_dw3)
+template <int HEAD>
+__device__ __forceinline__ void ph_dw3_pre(float* A, float* GMs, const f4 h2[4], const float* go, int c, int g) {
     if constexpr (HEAD == 0) {
-        // GM^T -> scratch, H2^T -> A; dW3 += GM^T . H2 over the tile's samples
         for (int o = g; o < NACT; o += 4) GMs[o * SP + c] = go[o];
 #pragma unroll
         for (int J = 0; J < 4; ++J)
 #pragma unroll
             for (int r = 0; r < 4; ++r) A[(16 * J + 4 * g + r) * SP + c] = h2[J][r];
-        wave_sync();
+    }
+}
+
+// dW3 += GM^T . H2 over the tile's samples (actor, MFMA); critic: per-lane partials
+template <int HEAD>
+__device__ __forceinline__ void ph_dw3(const float* A, const float* GMs, const f4 h2[4], const float* go, int c, int g,
+                                       Acc<HEAD>& acc) {
+    RT_FP_FAST
+    if constexpr (HEAD == 0) {
         const float4 ga = c < NACT ? ld4(&GMs[c * SP + 4 * g]) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
         for (int J = 0; J < 4; ++J) {
@@ -659,8 +655,14 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc.d3[J][r] += go[0] * h2[J][r];
     }
-    // ---- G2^T = (W3^T go) * (1 - H2^2); db2 += G2
-    f4 g2[4];
+}
+
+// G2^T = (W3^T go) * (1 - H2^2); db2 += G2
+template <int HEAD>
+__device__ __forceinline__ void ph_g2(const MfmaLds& S, const float* go, const f4 h2[4], int g, Acc<HEAD>& acc,
+                                      f4 g2[4]) {
+    RT_FP_FAST
+    constexpr int NOUT = HEAD == 0 ? NACT : 1;
 #pragma unroll
     for (int J = 0; J < 4; ++J) {
         f4 a = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -678,35 +680,40 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
             acc.db2[4 * J + r] += g2[J][r];
         }
     }
-    wave_sync();
+}
+
+// transposed tiles -> scratch rows [unit][16 samples]
+__device__ __forceinline__ void ph_put(float* A, const f4 v[4], int c, int g) {
 #pragma unroll
     for (int J = 0; J < 4; ++J)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            A[(16 * J + 4 * g + r) * SP + c] = g2[J][r];
-            Bs[(16 * J + 4 * g + r) * SP + c] = h1[J][r];
-        }
-    wave_sync();
-    // ---- dW2 += G2^T . H1 over the tile's samples
-    {
-        float4 a[4], bq[4];
+        for (int r = 0; r < 4; ++r) A[(16 * J + 4 * g + r) * SP + c] = v[J][r];
+}
+
+// dW2 += G2^T . H1 over the tile's samples (G2^T in A, H1^T in Bs)
+template <int HEAD>
+__device__ __forceinline__ void ph_dw2(const float* A, const float* Bs, int c, int g, Acc<HEAD>& acc) {
+    float4 a[4], bq[4];
 #pragma unroll
-        for (int J = 0; J < 4; ++J) {
-            a[J] = ld4(&A[(16 * J + c) * SP + 4 * g]);
-            bq[J] = ld4(&Bs[(16 * J + c) * SP + 4 * g]);
-        }
-#pragma unroll
-        for (int J = 0; J < 4; ++J)
-#pragma unroll
-            for (int T = 0; T < 4; ++T) {
-                acc.d2[J][T] = mfma4(a[J].x, bq[T].x, acc.d2[J][T]);
-                acc.d2[J][T] = mfma4(a[J].y, bq[T].y, acc.d2[J][T]);
-                acc.d2[J][T] = mfma4(a[J].z, bq[T].z, acc.d2[J][T]);
-                acc.d2[J][T] = mfma4(a[J].w, bq[T].w, acc.d2[J][T]);
-            }
+    for (int J = 0; J < 4; ++J) {
+        a[J] = ld4(&A[(16 * J + c) * SP + 4 * g]);
+        bq[J] = ld4(&Bs[(16 * J + c) * SP + 4 * g]);
     }
-    // ---- G1^T = (W2^T . G2^T) * (1 - H1^2)   (A operand W2[16J+4g+r][16I+c])
-    f4 g1[4];
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+        for (int T = 0; T < 4; ++T) {
+            acc.d2[J][T] = mfma4(a[J].x, bq[T].x, acc.d2[J][T]);
+            acc.d2[J][T] = mfma4(a[J].y, bq[T].y, acc.d2[J][T]);
+            acc.d2[J][T] = mfma4(a[J].z, bq[T].z, acc.d2[J][T]);
+            acc.d2[J][T] = mfma4(a[J].w, bq[T].w, acc.d2[J][T]);
+        }
+}
+
+// G1^T = (W2^T . G2^T) * (1 - H1^2)   (A operand W2[16J+4g+r][16I+c])
+template <int HEAD>
+__device__ __forceinline__ void ph_g1(const MfmaLds& S, const f4 g2[4], const f4 h1[4], int c, int g, f4 g1[4]) {
+    RT_FP_FAST
 #pragma unroll
     for (int I = 0; I < 4; ++I) {
         f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -717,13 +724,11 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
 #pragma unroll
         for (int r = 0; r < 4; ++r) g1[I][r] = z[r] * (1.0f - h1[I][r] * h1[I][r]);
     }
-    wave_sync();
-#pragma unroll
-    for (int J = 0; J < 4; ++J)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) A[(16 * J + 4 * g + r) * SP + c] = g1[J][r];
-    wave_sync();
-    // ---- [dW1 | db1] += G1^T . [X | 1]
+}
+
+// [dW1 | db1] += G1^T . [X | 1]   (G1^T in A)
+template <int HEAD>
+__device__ __forceinline__ void ph_dw1(const float* A, const float xd[4], int c, int g, Acc<HEAD>& acc) {
 #pragma unroll
     for (int J = 0; J < 4; ++J) {
         const float4 a = ld4(&A[(16 * J + c) * SP + 4 * g]);
@@ -732,6 +737,50 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
         acc.d1[J] = mfma4(a.z, xd[2], acc.d1[J]);
         acc.d1[J] = mfma4(a.w, xd[3], acc.d1[J]);
     }
+}
+
+// [X | 1] operand of the dW1 product (samples 4g..4g+3 of input row c)
+__device__ __forceinline__ void load_xd(const float* in, int c, int g, float xd[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xd[k] = xin(in, c, 4 * g + k);
+}
+
+template <int HEAD>
+__device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, float* A, float* Bs, float* in,
+                                        float* GMs, int c, int g, int t, int t_next, float inv_n, Acc<HEAD>& acc) {
+    constexpr int NOUT = HEAD == 0 ? NACT : 1;
+    const bool live = t * 16 + c < P.mb;
+    __builtin_amdgcn_s_waitcnt(0);  // this tile's inputs (LDS DMA issued during the previous tile) have landed
+    wave_sync();  // ... and the previous tile's reads of the scratch are done
+    f4 h1[4], h2[4];
+    mf_fwd(S, HEAD, in, c, g, h1, h2);
+    float xd[4];  // read now: `in` is refilled below
+    load_xd(in, c, g, xd);
+    float go[NOUT];
+    ph_out_loss<HEAD>(S, P, in, c, g, live, inv_n, h2, acc, go);
+    // every read of `in` for this tile is done (xd and the loss inputs are in
+    // registers): stream the next tile's inputs in beside the backward
+    if (t_next >= 0) {
+        asm volatile("" ::"v"(xd[0]), "v"(xd[1]), "v"(xd[2]), "v"(xd[3]));
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the LDS reads have returned
+        mf_prefetch<HEAD>(P, in, t_next, 16 * g + c);
+    }
+    ph_dw3_pre<HEAD>(A, GMs, h2, go, c, g);
+    if constexpr (HEAD == 0) wave_sync();
+    ph_dw3<HEAD>(A, GMs, h2, go, c, g, acc);
+    f4 g2[4];
+    ph_g2<HEAD>(S, go, h2, g, acc, g2);
+    wave_sync();
+    ph_put(A, g2, c, g);
+    ph_put(Bs, h1, c, g);
+    wave_sync();
+    ph_dw2<HEAD>(A, Bs, c, g, acc);
+    f4 g1[4];
+    ph_g1<HEAD>(S, g2, h1, c, g, g1);
+    wave_sync();
+    ph_put(A, g1, c, g);
+    wave_sync();
+    ph_dw1<HEAD>(A, xd, c, g, acc);
 }
 
 template <int HEAD>
