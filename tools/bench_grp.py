@@ -1,6 +1,6 @@
 """Grouped C3D stage forwards (conv2 groups=2 on 31^3, conv3 groups=4 on
 14^3 -- the 64^3 vision shapes; --big: the 128^3 shapes 63^3 / 30^3) at batch
-B: ms per call, inference and training (argmax) variants.  RT_C3D_GRP=0
+B: ms per call, inference and training (argmax) variants.  RT_C3D_ZS=0
 selects the dense ring kernel (A/B)."""
 import ctypes
 import json
@@ -45,7 +45,7 @@ def main():
             torch.cuda.synchronize()
             res["train" if train else "infer"] = 1e3 * (time.perf_counter() - t0) / n
         out[name] = res
-    print(json.dumps({"grp": os.environ.get("RT_C3D_GRP", "1"), "big": big, **out}))
+    print(json.dumps({"zs": os.environ.get("RT_C3D_ZS", "1"), "big": big, **out}))
 
 
 if __name__ == "__main__":
