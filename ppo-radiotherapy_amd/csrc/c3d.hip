@@ -689,9 +689,9 @@ int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* ro
 // (shuffle by 16), z pairs columns s ^ 1 (DPP quad_perm); the argmax byte
 // follows torch's first-maximum rule in (z, y, x) window order.
 // ---------------------------------------------------------------------------
-template <int PYB>
+template <int G, int PYB>
 RingGeom make_ring_geom_zs(const rt_conv_layer* L, int B) {
-    constexpr int CPG = 8;
+    constexpr int CPG = CO / G;
     RingGeom r{};
     Geom& g = r.g;
     g.D = L->in_dims[0];
@@ -716,20 +716,28 @@ RingGeom make_ring_geom_zs(const rt_conv_layer* L, int B) {
     r.SLOT = round_mod(CPG * g.CS, 16);
     r.npiece = (r.SLOT + 63) / 64;
     r.nyb = (g.PH + PYB - 1) / PYB;
-    const int64_t per_chunk = (int64_t)r.nyb * B * 2;
+    const int64_t per_chunk = (int64_t)r.nyb * B * G;
     int nzc = (int)std::min<int64_t>(g.PD, std::max<int64_t>(1, (4096 + per_chunk - 1) / per_chunk));
     r.ZC = (g.PD + nzc - 1) / nzc;
+    r.ZC = (r.ZC + G / 2 - 1) / (G / 2) * (G / 2);  // whole tiles (G / 2 pooled rows each) per chunk
     return r;
 }
 
-template <int PYB, bool TRAIN>
+// ring slots of the z-shift kernel: the G + 2 planes of a tile + the next G
+template <int G>
+constexpr int ring_zs_slots() {
+    return 2 * G + 2;
+}
+
+template <int G, int PYB, bool TRAIN>
 __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
     extern __shared__ float xs[];
-    constexpr int CPG = 8, NW = 8, KS = 72, NB = KS / 9;
+    constexpr int CPG = CO / G, NW = 8, ZX = G + 2, KS = CPG * ZX * 9 / 4, NB = KS / 9, NR = ring_zs_slots<G>();
+    constexpr int QPB = CPG / 4;  // channel quads per plane: batch bj = (tz' = bj / QPB, quad bj % QPB)
     static_assert(PYB % 2 == 0, "4-row y tiles");
     const Geom& g = P.rg.g;
     const int SLOT = P.rg.SLOT;
-    const int grp = blockIdx.z & 1, b = blockIdx.z >> 1, py0 = blockIdx.x * PYB;
+    const int grp = blockIdx.z % G, b = blockIdx.z / G, py0 = blockIdx.x * PYB;
     const int k0 = blockIdx.y * P.rg.ZC, k1 = min(g.PD, k0 + P.rg.ZC);
     if (k0 >= k1) return;
     const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
@@ -742,12 +750,12 @@ __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
     ld.init(P.rg, y0, x0, wave, lane);
     auto load_plane = [&](int t, int slot) { ld.load(xb, P.rg, xs, t, slot, wave, lane); };
 
-    // B = Wext: k-step st = 9 bj + q, batch bj = (tz', ci half), q = (ty, tx); lane group = ci in the half
-    const int co_l = c >> 1, sz = c & 1;
+    // B = Wext: k-step st = 9 bj + q, batch bj = (tz', channel quad), q = (ty, tx); lane group = ci in the quad
+    const int co_l = c / G, sz = c % G;
     float bw[KS];
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
-        const int bj = st / 9, q = st % 9, tz = bj >> 1, ci = 4 * (bj & 1) + gq, dz = tz - sz;
+        const int bj = st / 9, q = st % 9, tz = bj / QPB, ci = 4 * (bj % QPB) + gq, dz = tz - sz;
         bw[st] = (dz >= 0 && dz < 3) ? P.w[((grp * CPG + co_l) * CPG + ci) * 27 + dz * 9 + q] : 0.0f;
     }
     const int co = grp * CPG + co_l;
@@ -756,16 +764,16 @@ __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
     float* ybase = P.y + ((int64_t)b * CO + co) * chan;
     uint8_t* abase = TRAIN ? P.amax + ((int64_t)b * CO + co) * chan : nullptr;
     const int lane_xy = gq * g.CS + (c >> 2) * g.YS + (c & 3);
-    const int rank_zy = sz * 4 + (gq & 1) * 2;
-    const bool storer = sz == 0 && (gq & 1) == 0;
+    const int rank_zy = (sz & 1) * 4 + (gq & 1) * 2;
+    const bool storer = (sz & 1) == 0 && (gq & 1) == 0;
     constexpr int NYT = PYB / 2;
     const int nxp = (g.XT + 1) / 2;
     const int nitem = NYT * nxp;
     const int NI = (nitem + NW - 1) / NW;
 
-    // epilogue of one item: tiles tx = 2xp, 2xp + 1 of y tile yt at pooled row pz
-    auto epi = [&](const f4 (&acc)[2], int yt, int xp, int pz, bool ok) {
-        const int cz = 2 * pz - g.pd + sz, cy = y0 + 4 * yt + gq;
+    // epilogue of one item: tiles tx = 2xp, 2xp + 1 of y tile yt at pooled rows pz0 .. pz0 + G/2 - 1
+    auto epi = [&](const f4 (&acc)[2], int yt, int xp, int pz0, bool ok) {
+        const int cz = 2 * pz0 - g.pd + sz, cy = y0 + 4 * yt + gq, pz = pz0 + (sz >> 1);
         const bool vzy = ok && cz >= 0 && cz < g.cd && cy >= 0 && cy < g.ch;
         const int py = py0 + 2 * yt + (gq >> 1);
 #pragma unroll
@@ -792,7 +800,7 @@ __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
                     k = min(k, __builtin_amdgcn_mov_dpp(k, 0xB1, 0xF, 0xF, true));
                 }
                 const int px = 2 * tx + j;
-                if (ok && storer && tx < g.XT && px < g.PW && py < g.PH) {
+                if (ok && storer && tx < g.XT && px < g.PW && py < g.PH && pz < g.PD) {
                     const int64_t o = ((int64_t)pz * g.PH + py) * g.PW + px;
                     ybase[o] = M;
                     if constexpr (TRAIN) abase[o] = (uint8_t)(k | (M > 0.0f ? 8 : 0));
@@ -801,9 +809,9 @@ __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
         }
     };
 
-    // ---- prologue: planes 0..3 of the chunk
+    // ---- prologue: planes 0 .. G+1 of the chunk
 #pragma unroll
-    for (int i = 0; i < 4; ++i) load_plane(2 * k0 + i, i);
+    for (int i = 0; i < ZX; ++i) load_plane(2 * k0 + i, i);
     __builtin_amdgcn_s_waitcnt(0x0F70);
     __syncthreads();
 
@@ -811,16 +819,19 @@ __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
     int pyt = 0, pxp = 0, ppz = k0;
     bool pok = false;
     int sb = 0;  // ring slot of plane 2k
-    for (int k = k0; k < k1; ++k) {
-        if (k + 1 < k1) {  // planes of the next pooled row -> the two free slots
-            load_plane(2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4);
-            load_plane(2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5);
-        }
-        int zoff[4];
+    for (int k = k0; k < k1; k += G / 2) {  // one tile row = G conv planes = G/2 pooled rows
+        if (k + G / 2 < k1) {  // planes of the next tile row -> the G free slots
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+            for (int i = 0; i < G; ++i) {
+                const int sl = sb + ZX + i;
+                load_plane(2 * k + ZX + i, sl >= NR ? sl - NR : sl);
+            }
+        }
+        int zoff[ZX];
+#pragma unroll
+        for (int t = 0; t < ZX; ++t) {
             int sl = sb + t;
-            sl = sl >= kRing ? sl - kRing : sl;
+            sl = sl >= NR ? sl - NR : sl;
             zoff[t] = sl * SLOT + lane_xy;
         }
         for (int i = 0; i < NI; ++i) {
@@ -831,7 +842,7 @@ __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
             const int tb = 4 * yt * g.YS + 8 * xp;
             float bv[2][2][9];
             auto fetch = [&](float (&dst)[2][9], int bj) {
-                const int base = zoff[bj >> 1] + (bj & 1) * 4 * g.CS + tb;
+                const int base = zoff[bj / QPB] + (bj % QPB) * 4 * g.CS + tb;
 #pragma unroll
                 for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
@@ -861,45 +872,46 @@ __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next row has landed
         __syncthreads();                     // ... every wave's; and nobody still reads the slots reloaded next
-        sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+        sb = sb + G >= NR ? sb + G - NR : sb + G;
     }
     epi(pacc, pyt, pxp, ppz, pok);
 }
 
-template <int PYB>
+template <int G, int PYB>
 int launch_ring_zs_k(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
                      const float* bias, float* y, uint8_t* amax, hipStream_t st) {
     RingParams P{x, rows, w, bias, y, amax, rg};
-    const size_t lds = (size_t)kRing * rg.SLOT * sizeof(float);
+    const size_t lds = (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_ring_zs<PYB, true>);
-        allow_big_lds(&k_conv_ring_zs<PYB, false>);
+        allow_big_lds(&k_conv_ring_zs<G, PYB, true>);
+        allow_big_lds(&k_conv_ring_zs<G, PYB, false>);
         attr = true;
     }
-    dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, 2 * B);
+    dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, G * B);
     if (amax)
-        hipLaunchKernelGGL((k_conv_ring_zs<PYB, true>), grid, dim3(512), lds, st, P);
+        hipLaunchKernelGGL((k_conv_ring_zs<G, PYB, true>), grid, dim3(512), lds, st, P);
     else
-        hipLaunchKernelGGL((k_conv_ring_zs<PYB, false>), grid, dim3(512), lds, st, P);
+        hipLaunchKernelGGL((k_conv_ring_zs<G, PYB, false>), grid, dim3(512), lds, st, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
 }
 
-// groups = 2: the widest y band whose ring fits 160 KiB (one 8-wave block per CU)
+// the widest y band whose ring fits 160 KiB (one 8-wave block per CU)
+template <int G>
 int launch_ring_zs(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
                    const float* bias, float* y, uint8_t* amax, hipStream_t st) {
     auto fits = [&](const RingGeom& rg) {
-        return (size_t)kRing * rg.SLOT * sizeof(float) <= 160 * 1024 &&
-               (rg.npiece + 7) / 8 <= ring_max_pieces<8, 1>();
+        return (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float) <= 160 * 1024 &&
+               (rg.npiece + 7) / 8 <= ring_max_pieces<CO / G, 1>();
     };
-    RingGeom rg = make_ring_geom_zs<8>(L, B);
-    if (fits(rg)) return launch_ring_zs_k<8>(rg, B, x, rows, w, bias, y, amax, st);
-    rg = make_ring_geom_zs<4>(L, B);
-    if (fits(rg)) return launch_ring_zs_k<4>(rg, B, x, rows, w, bias, y, amax, st);
-    rg = make_ring_geom_zs<2>(L, B);
-    if (fits(rg)) return launch_ring_zs_k<2>(rg, B, x, rows, w, bias, y, amax, st);
+    RingGeom rg = make_ring_geom_zs<G, 8>(L, B);
+    if (fits(rg)) return launch_ring_zs_k<G, 8>(rg, B, x, rows, w, bias, y, amax, st);
+    rg = make_ring_geom_zs<G, 4>(L, B);
+    if (fits(rg)) return launch_ring_zs_k<G, 4>(rg, B, x, rows, w, bias, y, amax, st);
+    rg = make_ring_geom_zs<G, 2>(L, B);
+    if (fits(rg)) return launch_ring_zs_k<G, 2>(rg, B, x, rows, w, bias, y, amax, st);
     return RT_ELIMIT;
 }
 
@@ -1566,18 +1578,17 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     }
     if (L->cin == 4) return launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     if (L->groups == 1) return launch_fwd_ring<16, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-    if (L->groups == 2) {
-        // the z-shift ring kernel (RT_C3D_ZS=0: the dense ring kernel, A/B runs)
-        static const bool zs = [] {
-            const char* e = std::getenv("RT_C3D_ZS");
-            return !(e && e[0] == '0');
-        }();
-        if (zs && (int64_t)batch * 2 <= 65535) {
-            const int rc = launch_ring_zs(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-            if (rc != RT_ELIMIT) return rc;
-        }
-        return launch_fwd_ring<16, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    // grouped stages: the z-shift ring kernel (RT_C3D_ZS=0: the dense ring kernel, A/B runs)
+    static const bool zs = [] {
+        const char* e = std::getenv("RT_C3D_ZS");
+        return !(e && e[0] == '0');
+    }();
+    if (zs && (int64_t)batch * L->groups <= 65535) {
+        const int rc = L->groups == 2 ? launch_ring_zs<2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st)
+                                      : launch_ring_zs<4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+        if (rc != RT_ELIMIT) return rc;
     }
+    if (L->groups == 2) return launch_fwd_ring<16, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     return launch_fwd_ring<16, 4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
 }
 
