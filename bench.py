@@ -533,10 +533,15 @@ def main():
         t0 = time.perf_counter()
         tr.rollout()
         tr.compute_gae()
-        tr.update()
+        full_mb = int(cfg.update_epochs) * int(cfg.num_minibatches)
+        capped = bool(tr.max_minibatches) and tr.max_minibatches < full_mb
+        if not capped:
+            tr.update()
         torch.cuda.synchronize()
         barrier()
         di = max_over_ranks(time.perf_counter() - t0)
+        if capped:  # vision: rollout + GAE measured, the update's full_mb steps at the timed per-step cost
+            di += full_mb * du / n_upd
         if world > 1:  # the per-minibatch flat-gradient all-reduce alone (included in the update above)
             barrier()
             torch.cuda.synchronize()
@@ -547,7 +552,9 @@ def main():
             dar = max_over_ranks(time.perf_counter() - t0)
         upd = {"ppo_updates_per_s": n_upd / du, "ppo_update_ms": 1000 * du / n_upd,
                "minibatch_size_per_gpu": tr.minibatch_size, "update_minibatches_timed": n_upd,
-               "train_env_steps_per_s": total_envs * T / di, "train_iteration_s": di}
+               "train_env_steps_per_s": total_envs * T / di, "train_iteration_s": di,
+               "train_iteration": (f"rollout + GAE measured, {full_mb} minibatch steps at the timed "
+                                   f"{1000 * du / n_upd:.3f} ms each" if capped else "measured whole")}
         if world > 1:
             upd["update_allreduce_ms"] = 1000 * dar / n_upd
             upd["update_allreduce_bytes"] = 4 * tr.flat_grad.numel()
