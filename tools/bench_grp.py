@@ -1,6 +1,6 @@
 """Grouped C3D stage forwards (conv2 groups=2 on 31^3, conv3 groups=4 on
 14^3 -- the 64^3 vision shapes; --big: the 128^3 shapes 63^3 / 30^3) at batch
-B: ms per call, inference and training (argmax) variants.  RT_C3D_ZS=0
+B: ms per call, inference and training (argmax) variants and the data gradient.  RT_C3D_ZS=0
 selects the dense ring kernel (A/B)."""
 import ctypes
 import json
@@ -31,6 +31,21 @@ def main():
         y = torch.empty(B, 16, *od, device=dev)
         am = torch.empty(B, 16, *od, dtype=torch.uint8, device=dev)
         res = {}
+        gy = torch.randn_like(y)
+        dx = torch.empty_like(x)
+        _lib.check(L.rt_conv_relu_pool_fwd(ctypes.byref(layer), B, x.data_ptr(), None, w.data_ptr(), b.data_ptr(),
+                                           y.data_ptr(), am.data_ptr(), None), "fwd")
+
+        def fd():
+            _lib.check(L.rt_conv_relu_pool_dgrad(ctypes.byref(layer), B, w.data_ptr(), gy.data_ptr(), am.data_ptr(),
+                                                 dx.data_ptr(), None), "dgrad")
+        fd()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            fd()
+        torch.cuda.synchronize()
+        res["dgrad"] = 1e3 * (time.perf_counter() - t0) / 10
         for train in (False, True):
             def f():
                 _lib.check(L.rt_conv_relu_pool_fwd(ctypes.byref(layer), B, x.data_ptr(), None, w.data_ptr(),
