@@ -46,6 +46,10 @@ namespace {
 #ifndef RT_C3D_EXP
 #define RT_C3D_EXP 0
 #endif
+// weight-gradient ring slot stride residue (see make_ring_geom)
+#ifndef RT_WG_SR
+#define RT_WG_SR 12
+#endif
 
 constexpr int CO = 16;
 constexpr int kThreads = 512;      // weight-gradient kernel: 8 waves = position groups x column groups
@@ -395,7 +399,11 @@ struct RingGeom {
     int32_t ZC;        // pooled z rows per block (z chunk)
 };
 
-template <int CIN, int PYB, int VEC>
+// SR = slot stride residue (mod 32 dwords).  The forward relies on 16 (lanes
+// of one gather straddle two adjacent slots); the wgrad B gather spans 3 ring
+// slots per instruction, where 12 spreads them best (modelled: max bank
+// multiplicity 1.26-1.30 vs 1.43-1.56 at 16).
+template <int CIN, int PYB, int VEC, int SR = 16>
 RingGeom make_ring_geom(const rt_conv_layer* L, int B, int nthreads) {
     RingGeom r{};
     Geom& g = r.g;
@@ -418,7 +426,7 @@ RingGeom make_ring_geom(const rt_conv_layer* L, int B, int nthreads) {
     g.YS = round_mod((g.XL + VEC - 1) / VEC * VEC, 4);
     g.ZS = 0;
     g.CS = round_mod(g.YL * g.YS, 8);
-    r.SLOT = round_mod(CIN * g.CS, 16);
+    r.SLOT = round_mod(CIN * g.CS, SR);
     r.npiece = (r.SLOT + 64 * VEC - 1) / (64 * VEC);
     r.nyb = (g.PH + PYB - 1) / PYB;
     // z chunks: enough blocks to fill the chip a few times over (each chunk
@@ -486,6 +494,80 @@ struct RingLoader {
     }
 };
 
+// One output row of a ring kernel (the 2 conv z-planes of a pooled row, read
+// from ring slots sb.., the block's y band, full x): the items (2 tiles of
+// 2x2x4 positions: rows r < PYB times x-tile pairs xp) go round-robin to the
+// NW waves, each item one MFMA chain of nsteps k-steps in 9-step register
+// batches (one (channel quad, dz) each) read from LDS one batch ahead; the
+// PREVIOUS item's epilogue (pv) is issued between this item's MFMAs.
+struct RingPrev {
+    f4 acc[2];
+    int r, xp, k;
+    bool ok;
+};
+
+template <int CIN, int PYB, int NW, class Epi>
+__device__ __forceinline__ void ring_row(const float* xs, const float (&af)[nsteps<CIN>()], const Geom& g, int SLOT,
+                                         int sb, int k, int wave, int lane, RingPrev& pv, Epi&& epi) {
+    constexpr int NB = nsteps<CIN>() / 9;
+    const int c = lane & 15, gq = lane >> 4, zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
+    const int lane_xy = gq * g.CS + yc * g.YS + xc;
+    const int nxp = (g.XT + 1) / 2;
+    const int NI = (PYB * nxp + NW - 1) / NW;  // item rounds per row (all waves run NI)
+    int zoff[3];
+#pragma unroll
+    for (int dz = 0; dz < 3; ++dz) {
+        int sl = sb + zc + dz;
+        sl = sl >= kRing ? sl - kRing : sl;
+        zoff[dz] = sl * SLOT + lane_xy;
+    }
+    int r = 0, xp = wave;
+    while (xp >= nxp) {
+        xp -= nxp;
+        ++r;
+    }
+    for (int it = 0; it < NI; ++it) {
+        const bool ok = r < PYB;
+        const int rr = ok ? r : PYB - 1;
+        const int tb = 2 * rr * g.YS + 8 * xp;
+        float bv[2][2][9];
+        auto fetch = [&](float (&dst)[2][9], int bj) {
+            const int dz = bj % 3, j = bj / 3;
+            const int base = zoff[dz] + tb + j * 4 * g.CS;
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    dst[0][dy * 3 + dx] = xs[base + dy * g.YS + dx];
+                    dst[1][dy * 3 + dx] = xs[base + dy * g.YS + dx + 4];
+                }
+        };
+        fetch(bv[0], 0);
+        epi(pv.acc, pv.r, pv.xp, pv.k, pv.ok);  // the previous item's epilogue, between this item's MFMAs
+        f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+        for (int bj = 0; bj < NB; ++bj) {
+            if (bj + 1 < NB) fetch(bv[(bj + 1) & 1], bj + 1);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                acc[0] = mfma4(af[bj * 9 + q], bv[bj & 1][0][q], acc[0]);
+                acc[1] = mfma4(af[bj * 9 + q], bv[bj & 1][1][q], acc[1]);
+            }
+        }
+        pv.acc[0] = acc[0];
+        pv.acc[1] = acc[1];
+        pv.r = r;
+        pv.xp = xp;
+        pv.k = k;
+        pv.ok = ok;
+        xp += NW;
+        while (xp >= nxp) {
+            xp -= nxp;
+            ++r;
+        }
+    }
+}
+
 struct RingParams {
     const float* x;
     const int64_t* rows;  // sample b reads x row rows[b] (null: b)
@@ -500,7 +582,6 @@ template <int CIN, int G, int PYB, int VEC, int NTH, bool TRAIN>
 __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
     extern __shared__ float xs[];
     constexpr int NS = nsteps<CIN>();
-    constexpr int NB = NS / 9;           // 9-step batches: one (channel quad, dz) each
     constexpr int NW = NTH / 64;
     const Geom& g = P.rg.g;
     const int SLOT = P.rg.SLOT;
@@ -534,10 +615,6 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
         P.y + (int64_t)b * CO * chan, 0, CO * chan * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t asrd = __builtin_amdgcn_make_buffer_rsrc(
         TRAIN ? (void*)(P.amax + (int64_t)b * CO * chan) : (void*)P.y, 0, TRAIN ? CO * chan : 0, 0x00020000);
-    const int lane_xy = gq * g.CS + yc * g.YS + xc;
-    const int nxp = (g.XT + 1) / 2;
-    const int nitem = PYB * nxp;
-    const int NI = (nitem + NW - 1) / NW;  // item rounds per pooled row (all waves run NI)
 
     // epilogue of one item (tiles tx = 2xp, 2xp+1 of row r at pooled z pz)
     auto epi = [&](const f4 (&acc)[2], int r, int xp, int pz, bool ok) {
@@ -584,72 +661,19 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
     __builtin_amdgcn_s_waitcnt(0x0F70);
     __syncthreads();
 
-    f4 pacc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-    int pr = 0, pxp = 0, ppz = k0;
-    bool pok = false;
+    RingPrev pv{{{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}}, 0, 0, k0, false};
     int sb = 0;  // ring slot of plane 2k
     for (int k = k0; k < k1; ++k) {
         if (k + 1 < k1) {  // planes of the next pooled row -> the two free slots
             load_plane(2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4);
             load_plane(2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5);
         }
-        int zoff[3];
-#pragma unroll
-        for (int dz = 0; dz < 3; ++dz) {
-            int sl = sb + zc + dz;
-            sl = sl >= kRing ? sl - kRing : sl;
-            zoff[dz] = sl * SLOT + lane_xy;
-        }
-        int r = 0, xp = wave;
-        while (xp >= nxp) {
-            xp -= nxp;
-            ++r;
-        }
-        for (int it = 0; it < NI; ++it) {
-            const bool ok = r < PYB;
-            const int rr = ok ? r : PYB - 1;
-            const int tb = 2 * rr * g.YS + 8 * xp;
-            float bv[2][2][9];
-            auto fetch = [&](float (&dst)[2][9], int bj) {
-                const int dz = bj % 3, j = bj / 3;
-                const int base = zoff[dz] + tb + j * 4 * g.CS;
-#pragma unroll
-                for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                    for (int dx = 0; dx < 3; ++dx) {
-                        dst[0][dy * 3 + dx] = xs[base + dy * g.YS + dx];
-                        dst[1][dy * 3 + dx] = xs[base + dy * g.YS + dx + 4];
-                    }
-            };
-            fetch(bv[0], 0);
-            epi(pacc, pr, pxp, ppz, pok);  // the previous item's epilogue, between this item's MFMAs
-            f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-#pragma unroll
-            for (int bj = 0; bj < NB; ++bj) {
-                if (bj + 1 < NB) fetch(bv[(bj + 1) & 1], bj + 1);
-#pragma unroll
-                for (int q = 0; q < 9; ++q) {
-                    acc[0] = mfma4(af[bj * 9 + q], bv[bj & 1][0][q], acc[0]);
-                    acc[1] = mfma4(af[bj * 9 + q], bv[bj & 1][1][q], acc[1]);
-                }
-            }
-            pacc[0] = acc[0];
-            pacc[1] = acc[1];
-            pr = r;
-            pxp = xp;
-            ppz = k;
-            pok = ok;
-            xp += NW;
-            while (xp >= nxp) {
-                xp -= nxp;
-                ++r;
-            }
-        }
+        ring_row<CIN, PYB, NW>(xs, af, g, SLOT, sb, k, wave, lane, pv, epi);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next row has landed
         __syncthreads();                     // ... every wave's; and nobody still reads the slots reloaded next
         sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
     }
-    epi(pacc, pr, pxp, ppz, pok);
+    epi(pv.acc, pv.r, pv.xp, pv.k, pv.ok);
 }
 
 template <int CIN, int G, int PYB, int VEC, int NTH>
@@ -978,17 +1002,42 @@ __global__ __launch_bounds__(conv_threads<16>()) void k_conv_dgrad(DgradParams P
         const int px_hi = min((cx0 + g.XL - 1 + g.pw) >> 1, g.PW - 1);
         const int nz = pz_hi - pz_lo + 1, ny = py_hi - py_lo + 1, nx = px_hi + 1;
         const int nwin = CO * nz * ny * nx;
-        for (int i = threadIdx.x; i < nwin; i += NT) {
-            const int px = i % nx, py = py_lo + (i / nx) % ny, pz = pz_lo + (i / (nx * ny)) % nz,
-                      co = i / (nx * ny * nz);
-            const int64_t o = (((int64_t)b * CO + co) * g.PD + pz) * g.PH * g.PW + (int64_t)py * g.PW + px;
-            const int byte = P.am[o];
-            if (!(byte & 8)) continue;
-            const int k = byte & 7;
-            const int cz = 2 * pz - g.pd + (k >> 2), cy = 2 * py - g.ph + ((k >> 1) & 1), cx = 2 * px - g.pw + (k & 1);
-            const int zz = cz - cz0, yy = cy - cy0, xx = cx - cx0;
-            if (zz >= 0 && zz < g.ZL && yy >= 0 && yy < g.YL && xx >= 0 && xx < g.XL)
-                xs[co * g.CS + zz * g.ZS + yy * g.YS + xx] = P.dP[o];
+        // WU windows per thread in flight: the argmax byte and the gradient of
+        // a window are independent loads, so all 2*WU are issued before the
+        // first use (one scalar loop iteration per window took two dependent
+        // global round trips, and the block's MFMAs wait on this phase)
+        constexpr int WU = 8;
+        for (int i0 = threadIdx.x; i0 < nwin; i0 += NT * WU) {
+            int byte[WU], lds[WU];
+            float gv[WU];
+#pragma unroll
+            for (int u = 0; u < WU; ++u) {
+                const int i = i0 + u * NT;
+                byte[u] = 0;
+                gv[u] = 0.0f;
+                lds[u] = 0;
+                if (i < nwin) {
+                    const int px = i % nx, py = py_lo + (i / nx) % ny, pz = pz_lo + (i / (nx * ny)) % nz,
+                              co = i / (nx * ny * nz);
+                    const int64_t o = (((int64_t)b * CO + co) * g.PD + pz) * g.PH * g.PW + (int64_t)py * g.PW + px;
+                    byte[u] = P.am[o];
+                    gv[u] = P.dP[o];
+                    // LDS address of the window's (0,0,0) corner relative to the tile
+                    lds[u] = co * g.CS + (2 * pz - g.pd - cz0) * g.ZS + (2 * py - g.ph - cy0) * g.YS + (2 * px - g.pw - cx0);
+                    // pack the corner's tile coordinates for the range check below
+                    byte[u] |= ((2 * pz - g.pd - cz0 + 1) << 8) | ((2 * py - g.ph - cy0 + 1) << 16) |
+                               ((2 * px - g.pw - cx0 + 1) << 24);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < WU; ++u) {
+                const int bt = byte[u];
+                if (!(bt & 8)) continue;
+                const int k = bt & 7, kz = k >> 2, ky = (k >> 1) & 1, kx = k & 1;
+                const int zz = ((bt >> 8) & 255) - 1 + kz, yy = ((bt >> 16) & 255) - 1 + ky, xx = (bt >> 24) - 1 + kx;
+                if (zz >= 0 && zz < g.ZL && yy >= 0 && yy < g.YL && xx >= 0 && xx < g.XL)
+                    xs[lds[u] + kz * g.ZS + ky * g.YS + kx] = gv[u];
+            }
         }
     }
     float af[NS];
@@ -1433,6 +1482,195 @@ int launch_dgrad(const rt_conv_layer* L, int32_t B, const float* w, const float*
     return RT_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Data gradient, z-ring version (the launched one; pool padding 0, i.e. the
+// 16-channel stages).  dX = the full correlation of the sparse conv-output
+// gradient dY with the flipped, transposed weights, so the forward's ring
+// structure carries over: a block owns a y band of 2*PYB dX rows (full x) of
+// one sample and sweeps a chunk of ZC output rows (dX z-plane pairs 2k, 2k+1);
+// ring plane t = dY conv plane t - 2 (zero-padded), and the two planes of a
+// pair are the two conv planes of ONE pooled row, so a pair is built from
+// that row's pooling windows: each window writes its 2x2x2 block (the
+// gradient at its recorded maximum, zero elsewhere -- no separate zeroing
+// pass).  The argmax bytes and gradients of the next pair are loaded into
+// registers before the row's MFMAs and written to the two free slots after
+// them, so their latency hides behind the MFMA chains; one barrier per row.
+// (The tile version k_conv_dgrad re-staged a 4-plane halo per 2 output
+// planes and waited on its scatter before every tile.)
+constexpr int kDgMaxWin = 6;  // pooling windows per thread and plane pair
+
+struct DgradRingParams {
+    const float* w;     // stage weights [16][16/G][27]
+    const float* dP;    // [B][16][PD][PH][PW]
+    const uint8_t* am;  // same shape
+    float* dx;          // [B][16][D][H][W]
+    RingGeom rg;        // g: D,H,W = dX dims, PD,PH,PW = pooled dims, XT = x tiles of 4 over W
+};
+
+template <int G, int PYB, int NTH>
+__global__ __launch_bounds__(NTH) void k_conv_dgrad_ring(DgradRingParams P) {
+    extern __shared__ float xs[];
+    constexpr int NS = nsteps<16>(), NW = NTH / 64, MW = kDgMaxWin, cpg = CO / G;
+    const Geom& g = P.rg.g;
+    const int SLOT = P.rg.SLOT;
+    const int b = blockIdx.z, py0 = blockIdx.x * PYB, y0 = 2 * py0;
+    const int k0 = blockIdx.y * P.rg.ZC, k1 = min((g.D + 1) / 2, k0 + P.rg.ZC);
+    if (k0 >= k1) return;
+    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pplane = g.PH * g.PW, chan = g.PD * pplane;
+    const uint8_t* amb = P.am + (int64_t)b * CO * chan;
+    const float* dpb = P.dP + (int64_t)b * CO * chan;
+
+    // this thread's pooling windows of a plane pair (the same for every pair):
+    // window (co, pyl, pxw) covers LDS rows 2pyl.. and columns 2pxw..; pooled
+    // (py, px) = (py0 - 1 + pyl, pxw - 1), out-of-range windows write zeros
+    const int nxw = 2 * g.XT + 1, nwin = CO * (PYB + 1) * nxw;
+    int woff[MW], wlds[MW];
+#pragma unroll
+    for (int u = 0; u < MW; ++u) {
+        const int i = threadIdx.x + u * NTH;
+        const int pxw = i % nxw, rest = i / nxw, pyl = rest % (PYB + 1), co = rest / (PYB + 1);
+        const int px = pxw - 1, py = py0 - 1 + pyl;
+        wlds[u] = i < nwin ? co * g.CS + 2 * pyl * g.YS + 2 * pxw : -1;
+        woff[u] = i < nwin && px >= 0 && px < g.PW && py >= 0 && py < g.PH ? co * chan + py * g.PW + px : -1;
+    }
+    int bt[MW];
+    float gv[MW];
+    auto fetch_pair = [&](int m) {  // pair m = pooled row m - 1 -> registers
+        const int pz = m - 1;
+        const bool zok = pz >= 0 && pz < g.PD;
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const bool ok = zok && woff[u] >= 0;
+            const int o = woff[u] + pz * pplane;
+            bt[u] = ok ? amb[o] : 0;
+            gv[u] = ok ? dpb[o] : 0.0f;
+        }
+    };
+    auto store_pair = [&](int slot0) {  // registers -> slots slot0, slot0 + 1 (slot0 even: no wrap)
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            if (wlds[u] < 0) continue;
+            const int kk = bt[u] & 7;
+            const float v = (bt[u] & 8) ? gv[u] : 0.0f;
+#pragma unroll
+            for (int kz = 0; kz < 2; ++kz)
+#pragma unroll
+                for (int ky = 0; ky < 2; ++ky) {
+                    const int k2 = kz * 4 + ky * 2;
+                    *reinterpret_cast<float2*>(xs + (slot0 + kz) * SLOT + wlds[u] + ky * g.YS) =
+                        make_float2(kk == k2 ? v : 0.0f, kk == k2 + 1 ? v : 0.0f);
+                }
+        }
+    };
+
+    // A fragments: flipped taps, transposed channels (lane group = dY channel,
+    // row c = dX channel); zero across groups
+    float af[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int q = s % 27, co = 4 * (s / 27) + gq;
+        af[s] = c / cpg == co / cpg ? P.w[(co * cpg + c % cpg) * 27 + 26 - q] : 0.0f;
+    }
+    const int zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
+    const int cstride = g.D * g.H * g.W;
+    float* dxb = P.dx + ((int64_t)b * CO + 4 * gq) * cstride;
+    auto epi = [&](const f4 (&acc)[2], int r, int xp, int k, bool ok) {
+        const int z = 2 * k + zc, y = y0 + 2 * r + yc;
+        const bool vzy = ok && z < g.D && y < g.H;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int x = 8 * xp + 4 * u + xc;
+            if (vzy && x < g.W) {
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) dxb[rr * cstride + (z * g.H + y) * g.W + x] = acc[u][rr];
+            }
+        }
+    };
+
+    fetch_pair(k0);
+    store_pair(0);
+    fetch_pair(k0 + 1);
+    store_pair(2);
+    __syncthreads();
+    RingPrev pv{{{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}}, 0, 0, k0, false};
+    int sb = 0;  // ring slot of plane 2k
+    for (int k = k0; k < k1; ++k) {
+        const bool more = k + 1 < k1;
+        if (more) fetch_pair(k + 2);
+        ring_row<16, PYB, NW>(xs, af, g, SLOT, sb, k, wave, lane, pv, epi);
+        if (more) store_pair(sb + 4 >= kRing ? sb + 4 - kRing : sb + 4);  // the slots row k - 1 read last
+        __syncthreads();
+        sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+    }
+    epi(pv.acc, pv.r, pv.xp, pv.k, pv.ok);
+}
+
+template <int PYB>
+RingGeom make_dgrad_ring_geom(const rt_conv_layer* L, int B) {
+    RingGeom r{};
+    Geom& g = r.g;
+    g.D = L->in_dims[0];
+    g.H = L->in_dims[1];
+    g.W = L->in_dims[2];
+    g.cd = g.D - 2;
+    g.ch = g.H - 2;
+    g.cw = g.W - 2;
+    g.PD = g.cd / 2;
+    g.PH = g.ch / 2;
+    g.PW = g.cw / 2;
+    g.XT = (g.W + 3) / 4;
+    g.ZL = 4;
+    g.YL = 2 * PYB + 2;
+    g.XL = 4 * g.XT + 2;
+    g.YS = round_mod(g.XL, 4);
+    g.CS = round_mod(g.YL * g.YS, 8);
+    r.SLOT = round_mod(CO * g.CS, 16);
+    r.nyb = (g.H + 2 * PYB - 1) / (2 * PYB);
+    const int KD = (g.D + 1) / 2;
+    const int64_t per_chunk = (int64_t)r.nyb * B;
+    const int nzc = (int)std::min<int64_t>(KD, std::max<int64_t>(1, (4096 + per_chunk - 1) / per_chunk));
+    r.ZC = (KD + nzc - 1) / nzc;
+    return r;
+}
+
+constexpr int kDgradRingThreads = 512;
+
+template <int G, int PYB>
+int launch_dgrad_ring_k(const RingGeom& rg, int32_t B, const float* w, const float* dP, const uint8_t* am, float* dx,
+                        hipStream_t st) {
+    DgradRingParams P{w, dP, am, dx, rg};
+    const size_t lds = (size_t)kRing * rg.SLOT * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        allow_big_lds(&k_conv_dgrad_ring<G, PYB, kDgradRingThreads>);
+        attr = true;
+    }
+    dim3 grid(rg.nyb, ((rg.g.D + 1) / 2 + rg.ZC - 1) / rg.ZC, B);
+    hipLaunchKernelGGL((k_conv_dgrad_ring<G, PYB, kDgradRingThreads>), grid, dim3(kDgradRingThreads), lds, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+// the widest y band whose ring fits 160 KiB and whose windows fit the threads
+template <int G>
+int launch_dgrad_ring(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am, float* dx,
+                      hipStream_t st) {
+    auto fits = [&](const RingGeom& rg, int pyb) {
+        return (size_t)kRing * rg.SLOT * sizeof(float) <= 160 * 1024 &&
+               CO * (pyb + 1) * (2 * rg.g.XT + 1) <= kDgMaxWin * kDgradRingThreads;
+    };
+    RingGeom rg = make_dgrad_ring_geom<4>(L, B);
+    if (fits(rg, 4)) return launch_dgrad_ring_k<G, 4>(rg, B, w, dP, am, dx, st);
+    rg = make_dgrad_ring_geom<2>(L, B);
+    if (fits(rg, 2)) return launch_dgrad_ring_k<G, 2>(rg, B, w, dP, am, dx, st);
+    rg = make_dgrad_ring_geom<1>(L, B);
+    if (fits(rg, 1)) return launch_dgrad_ring_k<G, 1>(rg, B, w, dP, am, dx, st);
+    return RT_ELIMIT;
+}
+
 constexpr int kWgradBlocks = 512;
 
 template <int CIN, int PZB, int PYB>
@@ -1519,7 +1757,7 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
     constexpr int PY_BIG = CIN == 4 ? 4 : 2;
 #define RT_WG_TRY(PYB_, VEC_)                                                                          \
     {                                                                                                 \
-        RingGeom rg = make_ring_geom<CIN, PYB_, VEC_>(L, B, kThreads);                                \
+        RingGeom rg = make_ring_geom<CIN, PYB_, VEC_, RT_WG_SR>(L, B, kThreads);                      \
         rg.g.PYB_tiles = PYB_ * rg.g.XT;                                                              \
         if (rc == RT_ELIMIT && fits(rg, VEC_))                                                        \
             rc = go(rg, [&](const RingGeom& r, int gz) {                                              \
@@ -1621,6 +1859,17 @@ extern "C" int rt_conv_relu_pool_dgrad(const rt_conv_layer* L, int32_t batch, co
     if (bad_layer(L) || L->cin != 16 || batch < 1 || batch > 65535 || !w_d || !dy_d || !argmax_d || !dx_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_dgrad: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // the ring kernel (RT_C3D_DGR=0: the tile kernel, A/B runs)
+    static const bool ring = [] {
+        const char* e = std::getenv("RT_C3D_DGR");
+        return !(e && e[0] == '0');
+    }();
+    if (ring && L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0) {
+        const int rc = L->groups == 1   ? launch_dgrad_ring<1>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
+                       : L->groups == 2 ? launch_dgrad_ring<2>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
+                                        : launch_dgrad_ring<4>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
+        if (rc != RT_ELIMIT) return rc;
+    }
     if (L->groups == 1) return launch_dgrad<1, 1, 2>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
     if (L->groups == 2) return launch_dgrad<2, 1, 2>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
     return launch_dgrad<4, 1, 2>(L, batch, w_d, dy_d, argmax_d, dx_d, st);

@@ -15,6 +15,8 @@ STAGES = [  # cin, groups, dims, pool_pad, batch
     (16, 2, (31, 31, 31), (0, 0, 0), 4),
     (16, 4, (14, 14, 14), (0, 0, 0), 5),
     (16, 1, (9, 12, 11), (1, 0, 1), 3),
+    (16, 2, (11, 21, 63), (0, 0, 0), 2),  # data-gradient ring: 2-row y band (63-wide planes)
+    (16, 1, (12, 13, 10), (0, 0, 0), 3),
 ]
 
 
@@ -171,8 +173,8 @@ def test_conv_relu_pool_backward(cin, groups, dims, pad, B):
     if dx is not None:
         d = (dx.cpu().double() - xr.grad).abs()
         scale = float(xr.grad.abs().max())
-        assert float((d <= 1e-4 * scale).double().mean()) > 0.999
-        assert float(d.norm() / xr.grad.norm()) < 1e-3
+        assert float(d.max()) <= 2e-5 * scale, (float(d.max()), scale)
+        assert float(d.norm() / xr.grad.norm()) < 1e-5
 
 
 def test_features_extractor_matches_torch_modules():
