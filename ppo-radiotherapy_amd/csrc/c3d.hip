@@ -1671,6 +1671,227 @@ int launch_dgrad_ring(const rt_conv_layer* L, int32_t B, const float* w, const f
     return RT_ELIMIT;
 }
 
+// Data gradient of the grouped stages in the z-shift form on the same ring:
+// one group per block, a tile is D[m = position][n = (ci, s)] over a 4(y) x
+// 4(x) patch of the scattered dY planes, columns = the group's dX channels x
+// the tile row's G dX z-planes s, k = (tz' in 0..G+1, dY channel quad, ty, tx):
+// B = Wext[(tz', co, ty, tx)][(ci, s)] = W[co][ci][2 - (tz' - s)][2 - ty][2 - tx]
+// in registers (zero outside the 3 taps) -- the forward z-shift kernel's MFMA
+// mapping with flipped, transposed weights (1.33x / 2x the useful work for
+// groups 2 / 4 instead of 2x / 4x).  Planes come from the pooling-window
+// scatter of k_conv_dgrad_ring, G/2 pooled rows per tile row.
+template <int G, int PYB>
+__global__ __launch_bounds__(512) void k_conv_dgrad_ring_zs(DgradRingParams P) {
+    extern __shared__ float xs[];
+    constexpr int CPG = CO / G, NW = 8, NTH = 512, ZX = G + 2, KS = CPG * ZX * 9 / 4, NB = KS / 9;
+    constexpr int NR = ring_zs_slots<G>(), QPB = CPG / 4, MW = kDgMaxWin, HP = G / 2;
+    static_assert(PYB % 2 == 0, "4-row y tiles");
+    const Geom& g = P.rg.g;
+    const int SLOT = P.rg.SLOT;
+    const int grp = blockIdx.z % G, b = blockIdx.z / G, py0 = blockIdx.x * PYB, y0 = 2 * py0;
+    const int k0 = blockIdx.y * P.rg.ZC, k1 = min((g.D + 1) / 2, k0 + P.rg.ZC);
+    if (k0 >= k1) return;
+    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pplane = g.PH * g.PW, chan = g.PD * pplane;
+    const uint8_t* amb = P.am + ((int64_t)b * CO + grp * CPG) * chan;
+    const float* dpb = P.dP + ((int64_t)b * CO + grp * CPG) * chan;
+
+    // this thread's pooling windows of a plane pair (the group's channels)
+    const int nxw = 2 * g.XT + 1, nwin = CPG * (PYB + 1) * nxw;
+    int woff[MW], wlds[MW];
+#pragma unroll
+    for (int u = 0; u < MW; ++u) {
+        const int i = threadIdx.x + u * NTH;
+        const int pxw = i % nxw, rest = i / nxw, pyl = rest % (PYB + 1), co = rest / (PYB + 1);
+        const int px = pxw - 1, py = py0 - 1 + pyl;
+        wlds[u] = i < nwin ? co * g.CS + 2 * pyl * g.YS + 2 * pxw : -1;
+        woff[u] = i < nwin && px >= 0 && px < g.PW && py >= 0 && py < g.PH ? co * chan + py * g.PW + px : -1;
+    }
+    auto fetch_pair = [&](int m, int (&bt)[MW], float (&gv)[MW]) {  // pair m = pooled row m - 1
+        const int pz = m - 1;
+        const bool zok = pz >= 0 && pz < g.PD;
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const bool ok = zok && woff[u] >= 0;
+            const int o = woff[u] + pz * pplane;
+            bt[u] = ok ? amb[o] : 0;
+            gv[u] = ok ? dpb[o] : 0.0f;
+        }
+    };
+    auto store_pair = [&](int slot0, const int (&bt)[MW], const float (&gv)[MW]) {  // slot0 even: no wrap
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            if (wlds[u] < 0) continue;
+            const int kk = bt[u] & 7;
+            const float v = (bt[u] & 8) ? gv[u] : 0.0f;
+#pragma unroll
+            for (int kz = 0; kz < 2; ++kz)
+#pragma unroll
+                for (int ky = 0; ky < 2; ++ky) {
+                    const int k2 = kz * 4 + ky * 2;
+                    *reinterpret_cast<float2*>(xs + (slot0 + kz) * SLOT + wlds[u] + ky * g.YS) =
+                        make_float2(kk == k2 ? v : 0.0f, kk == k2 + 1 ? v : 0.0f);
+                }
+        }
+    };
+
+    // B = Wext: k-step st = 9 bj + q, batch bj = (tz', dY channel quad), q = (ty, tx); lane group = dY channel
+    const int ci_l = c / G, sz = c % G;
+    float bw[KS];
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+        const int bj = st / 9, q = st % 9, tz = bj / QPB, co = 4 * (bj % QPB) + gq, dz = tz - sz;
+        bw[st] = (dz >= 0 && dz < 3) ? P.w[((grp * CPG + co) * CPG + ci_l) * 27 + (2 - dz) * 9 + 8 - q] : 0.0f;
+    }
+    const int cstride = g.D * g.H * g.W;
+    float* dxb = P.dx + ((int64_t)b * CO + grp * CPG + ci_l) * cstride;
+    const int lane_xy = gq * g.CS + (c >> 2) * g.YS + (c & 3);
+    constexpr int NYT = PYB / 2;
+    const int nxp = (g.XT + 1) / 2;
+    const int nitem = NYT * nxp;
+    const int NI = (nitem + NW - 1) / NW;
+
+    // epilogue: lane (c, g) holds dX channel ci_l, plane 2k + sz, row 4yt + g, x = 4tx .. 4tx + 3
+    auto epi = [&](const f4 (&acc)[2], int yt, int xp, int k, bool ok) {
+        const int z = 2 * k + sz, y = y0 + 4 * yt + gq;
+        const bool vzy = ok && z < g.D && y < g.H;
+        float* row = dxb + (z * g.H + y) * g.W;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int x = 8 * xp + 4 * u + r;
+                if (vzy && x < g.W) row[x] = acc[u][r];
+            }
+    };
+
+    {  // prologue: pairs k0 .. k0 + G/2 -> slots 0 .. ZX - 1
+        int bt[MW];
+        float gv[MW];
+#pragma unroll
+        for (int j = 0; j <= HP; ++j) {
+            fetch_pair(k0 + j, bt, gv);
+            store_pair(2 * j, bt, gv);
+        }
+    }
+    __syncthreads();
+
+    int bt[HP][MW];
+    float gv[HP][MW];
+    f4 pacc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+    int pyt = 0, pxp = 0, pk = k0;
+    bool pok = false;
+    int sb = 0;  // ring slot of plane 2k
+    for (int k = k0; k < k1; k += HP) {  // one tile row = G dX planes
+        const bool more = k + HP < k1;
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < HP; ++j) fetch_pair(k + HP + 1 + j, bt[j], gv[j]);
+        }
+        int zoff[ZX];
+#pragma unroll
+        for (int t = 0; t < ZX; ++t) {
+            int sl = sb + t;
+            sl = sl >= NR ? sl - NR : sl;
+            zoff[t] = sl * SLOT + lane_xy;
+        }
+        for (int i = 0; i < NI; ++i) {
+            const int it = wave + NW * i;
+            const bool ok = it < nitem;
+            const int itc = ok ? it : nitem - 1;
+            const int yt = itc / nxp, xp = itc - yt * nxp;
+            const int tb = 4 * yt * g.YS + 8 * xp;
+            float bv[2][2][9];
+            auto fetch = [&](float (&dst)[2][9], int bj) {
+                const int base = zoff[bj / QPB] + (bj % QPB) * 4 * g.CS + tb;
+#pragma unroll
+                for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+                    for (int tx = 0; tx < 3; ++tx) {
+                        dst[0][ty * 3 + tx] = xs[base + ty * g.YS + tx];
+                        dst[1][ty * 3 + tx] = xs[base + ty * g.YS + tx + 4];
+                    }
+            };
+            fetch(bv[0], 0);
+            epi(pacc, pyt, pxp, pk, pok);  // the previous item's epilogue, between this item's MFMAs
+            f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+            for (int bj = 0; bj < NB; ++bj) {
+                if (bj + 1 < NB) fetch(bv[(bj + 1) & 1], bj + 1);
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    acc[0] = mfma4(bv[bj & 1][0][q], bw[bj * 9 + q], acc[0]);
+                    acc[1] = mfma4(bv[bj & 1][1][q], bw[bj * 9 + q], acc[1]);
+                }
+            }
+            pacc[0] = acc[0];
+            pacc[1] = acc[1];
+            pyt = yt;
+            pxp = xp;
+            pk = k;
+            pok = ok;
+        }
+        if (more) {  // the next tile row's pairs -> the slots the previous tile row read last
+#pragma unroll
+            for (int j = 0; j < HP; ++j) {
+                const int sl = sb + ZX + 2 * j;
+                store_pair(sl >= NR ? sl - NR : sl, bt[j], gv[j]);
+            }
+        }
+        __syncthreads();
+        sb = sb + G >= NR ? sb + G - NR : sb + G;
+    }
+    epi(pacc, pyt, pxp, pk, pok);
+}
+
+template <int G, int PYB>
+RingGeom make_dgrad_ring_geom_zs(const rt_conv_layer* L, int B) {
+    RingGeom r = make_dgrad_ring_geom<PYB>(L, B);
+    Geom& g = r.g;
+    g.CS = round_mod(g.YL * g.YS, 16);
+    r.SLOT = round_mod(CO / G * g.CS, 16);
+    const int KD = (g.D + 1) / 2;
+    const int64_t per_chunk = (int64_t)r.nyb * B * G;
+    const int nzc = (int)std::min<int64_t>(KD, std::max<int64_t>(1, (4096 + per_chunk - 1) / per_chunk));
+    r.ZC = (KD + nzc - 1) / nzc;
+    r.ZC = (r.ZC + G / 2 - 1) / (G / 2) * (G / 2);  // whole tile rows per chunk
+    return r;
+}
+
+template <int G, int PYB>
+int launch_dgrad_ring_zs_k(const RingGeom& rg, int32_t B, const float* w, const float* dP, const uint8_t* am,
+                           float* dx, hipStream_t st) {
+    DgradRingParams P{w, dP, am, dx, rg};
+    const size_t lds = (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        allow_big_lds(&k_conv_dgrad_ring_zs<G, PYB>);
+        attr = true;
+    }
+    dim3 grid(rg.nyb, ((rg.g.D + 1) / 2 + rg.ZC - 1) / rg.ZC, G * B);
+    hipLaunchKernelGGL((k_conv_dgrad_ring_zs<G, PYB>), grid, dim3(512), lds, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+template <int G>
+int launch_dgrad_ring_zs(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am,
+                         float* dx, hipStream_t st) {
+    auto fits = [&](const RingGeom& rg, int pyb) {
+        return (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float) <= 160 * 1024 &&
+               CO / G * (pyb + 1) * (2 * rg.g.XT + 1) <= kDgMaxWin * 512;
+    };
+    RingGeom rg = make_dgrad_ring_geom_zs<G, 8>(L, B);
+    if (fits(rg, 8)) return launch_dgrad_ring_zs_k<G, 8>(rg, B, w, dP, am, dx, st);
+    rg = make_dgrad_ring_geom_zs<G, 4>(L, B);
+    if (fits(rg, 4)) return launch_dgrad_ring_zs_k<G, 4>(rg, B, w, dP, am, dx, st);
+    rg = make_dgrad_ring_geom_zs<G, 2>(L, B);
+    if (fits(rg, 2)) return launch_dgrad_ring_zs_k<G, 2>(rg, B, w, dP, am, dx, st);
+    return RT_ELIMIT;
+}
+
 constexpr int kWgradBlocks = 512;
 
 template <int CIN, int PZB, int PYB>
@@ -1864,7 +2085,18 @@ extern "C" int rt_conv_relu_pool_dgrad(const rt_conv_layer* L, int32_t batch, co
         const char* e = std::getenv("RT_C3D_DGR");
         return !(e && e[0] == '0');
     }();
-    if (ring && L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0) {
+    // grouped stages: the z-shift form (RT_C3D_DGZS=0: the dense ring kernel, A/B runs)
+    static const bool zs = [] {
+        const char* e = std::getenv("RT_C3D_DGZS");
+        return !(e && e[0] == '0');
+    }();
+    const bool pad0 = L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0;
+    if (ring && zs && pad0 && L->groups > 1 && (int64_t)batch * L->groups <= 65535) {
+        const int rc = L->groups == 2 ? launch_dgrad_ring_zs<2>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
+                                      : launch_dgrad_ring_zs<4>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
+        if (rc != RT_ELIMIT) return rc;
+    }
+    if (ring && pad0) {
         const int rc = L->groups == 1   ? launch_dgrad_ring<1>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
                        : L->groups == 2 ? launch_dgrad_ring<2>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
                                         : launch_dgrad_ring<4>(L, batch, w_d, dy_d, argmax_d, dx_d, st);

@@ -4,6 +4,8 @@ build.
 
     python tools/build_variant.py NAME c3d.hip -DRT_C3D_EXP=1 [...]
     -> _variants/librtenv_NAME.so
+    python tools/build_variant.py NAME c3d.hip --rev HEAD [...]
+    (the source as of a git revision: before/after A/B of an edit)
 """
 import os
 import subprocess
@@ -16,13 +18,28 @@ from ppo_radiotherapy_amd import build as B  # noqa: E402
 
 def main():
     name, src_base, extra = sys.argv[1], sys.argv[2], sys.argv[3:]
+    rev = None
+    if "--rev" in extra:
+        i = extra.index("--rev")
+        rev = extra[i + 1]
+        del extra[i:i + 2]
     B.build()
     src = [s for s in B.SRCS if os.path.basename(s) == src_base][0]
     vdir = os.path.join(B.REPO, "_variants")
     os.makedirs(vdir, exist_ok=True)
+    csrc = src
+    if rev:  # compile the revision's text next to the source (same include paths)
+        csrc = os.path.join(os.path.dirname(src), f"_rev_{name}_{src_base}")
+        with open(csrc, "w") as f:
+            f.write(subprocess.run(["git", "-C", B.REPO, "show", f"{rev}:{os.path.relpath(src, B.REPO)}"],
+                                   check=True, capture_output=True, text=True).stdout)
     obj = os.path.join(vdir, f"{name}_{os.path.splitext(src_base)[0]}.o")
-    subprocess.run([B.hipcc(), *B.HIPCC_FLAGS, *B.EXTRA_FLAGS.get(src, []), *extra, "-I",
-                    os.path.join(B.REPO, "include"), "-c", src, "-o", obj], check=True)
+    try:
+        subprocess.run([B.hipcc(), *B.HIPCC_FLAGS, *B.EXTRA_FLAGS.get(src, []), *extra, "-I",
+                        os.path.join(B.REPO, "include"), "-c", csrc, "-o", obj], check=True)
+    finally:
+        if rev:
+            os.remove(csrc)
     objs = [obj if s == src else os.path.join(B.OBJ_DIR, os.path.splitext(os.path.basename(s))[0] + ".o")
             for s in B.SRCS]
     out = os.path.join(vdir, f"librtenv_{name}.so")
