@@ -46,6 +46,10 @@ namespace {
 #ifndef RT_C3D_EXP
 #define RT_C3D_EXP 0
 #endif
+// widest y band of the z-shift weight gradient (A/B builds)
+#ifndef RT_WZ_MAXPYB
+#define RT_WZ_MAXPYB 2
+#endif
 // weight-gradient ring slot stride residue (see make_ring_geom)
 #ifndef RT_WG_SR
 #define RT_WG_SR 12
@@ -1275,32 +1279,31 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P)
         const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
         const uint8_t* amb = P.am + ((int64_t)b * CO + c) * chan;
         const float* dpb = P.dP + ((int64_t)b * CO + c) * chan;
-        int abyte[2][kWgMaxTiles];
-        float ad[2][kWgMaxTiles];
+        // one register per tile: tile i's dY of row k + 1 is loaded as soon as
+        // row k has consumed it (a rolling prefetch; a second buffer loaded at
+        // the row start measured 18 % slower in the z-shift kernel)
+        int abyte[kWgMaxTiles];
+        float ad[kWgMaxTiles];
         // lane (c, g) of tile t: channel c at the 4 positions 4q + g, all in pooled window px = 2tx + (g >> 1)
-        auto load_a = [&](int k, int (&byte)[kWgMaxTiles], float (&d)[kWgMaxTiles]) {
-#pragma unroll
-            for (int i = 0; i < kWgMaxTiles; ++i) {
-                const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
-                const int py = py0 + r, px = 2 * tx + (gq >> 1);
-                const bool ok = i < ntw && py < g.PH && px < g.PW;
-                const int o = (k * g.PH + py) * g.PW + px;
-                byte[i] = ok ? amb[o] : 0;
-                d[i] = ok ? dpb[o] : 0.0f;
-            }
+        auto load_a = [&](int k, int i) {
+            const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
+            const int py = py0 + r, px = 2 * tx + (gq >> 1);
+            const bool ok = i < ntw && py < g.PH && px < g.PW;
+            const int o = (k * g.PH + py) * g.PW + px;
+            abyte[i] = ok ? amb[o] : 0;
+            ad[i] = ok ? dpb[o] : 0.0f;
         };
         __syncthreads();  // the previous sample's ring reads are done
 #pragma unroll
         for (int i = 0; i < 4; ++i) ld.load(xb, P.rg, xs, i, i, wave, lane);
-        load_a(0, abyte[0], ad[0]);
+#pragma unroll
+        for (int i = 0; i < kWgMaxTiles; ++i) load_a(0, i);
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
         int sb = 0;
-        // one pooled row; the register buffer parity is compile-time (no dynamic indexing)
-        auto step = [&](int k, auto parity) {
-            constexpr int cur = decltype(parity)::value;
-            if (k + 1 < g.PD) {
-                load_a(k + 1, abyte[cur ^ 1], ad[cur ^ 1]);
+        for (int k = 0; k < g.PD; ++k) {
+            const bool more = k + 1 < g.PD;
+            if (more) {
                 ld.load(xb, P.rg, xs, 2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4, wave, lane);
                 ld.load(xb, P.rg, xs, 2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5, wave, lane);
             }
@@ -1315,11 +1318,12 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P)
                 }
 #pragma unroll
             for (int i = 0; i < kWgMaxTiles; ++i) {
-                if (i >= ntw) break;
+                if (i >= ntw) continue;
                 const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
                 const int toff = 2 * r * g.YS + 4 * tx;
-                const int byte = abyte[cur][i];
-                const float d = ad[cur][i];
+                const int byte = abyte[i];
+                const float d = ad[i];
+                if (more) load_a(k + 1, i);
                 float bv[4][kWgradTiles];
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
@@ -1338,10 +1342,6 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P)
             __builtin_amdgcn_s_waitcnt(0x0F70);
             __syncthreads();
             sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
-        };
-        for (int k = 0; k < g.PD; k += 2) {
-            step(k, std::integral_constant<int, 0>{});
-            if (k + 1 < g.PD) step(k + 1, std::integral_constant<int, 1>{});
         }
     }
     // D (lane (c, g)): rows co = 4g + r, column 16T + c; the WP position
@@ -1361,6 +1361,153 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P)
 #pragma unroll
         for (int k = 1; k < WP; ++k) v += R[k * REG + i];
         out[i] = v;
+    }
+}
+
+// Weight gradient of the groups = 2 stage in the z-shift form (one ring of all
+// 16 channels, as k_conv_wgrad_ring): D[m = (co, s)][n = (ci, tz', ty, tx)] =
+// sum over the (y, x) positions of a pooled row of dY[co][2k + s][y][x] *
+// X[ci][2k + tz'][y + ty][x + tx], per group (rows = its 8 output channels x
+// the row's 2 conv planes s, columns = its 8 input channels x 4 ring planes x
+// 9 in-plane taps = 18 column tiles); dW[co][ci][tz] = sum_s D[(co, s)][(ci,
+// tz + s)].  A position tile is 2 rows x 4 x of one plane pair (2 k-steps, z
+// folded into the rows): 2 x 36 column tiles x 2 k-steps per 16 dense
+// positions against 28 x 4 in the dense form (1.56x fewer MFMAs).  Lane (c, g)
+// holds row (co = c >> 1, s = c & 1) at positions x = 4tx + g, one pooling
+// window per tile as in the dense kernel.  db by VALU sums of the A values.
+// Waves: 4 column groups (group = wc / 2, tiles (wc % 2) * 9 ..) x 2 position groups.
+constexpr int kWzTiles = 9;
+
+template <int PYB, int MT>
+__global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring_zs(WgradRingParams P) {
+    extern __shared__ float xs[];
+    constexpr int G = 2, CPG = CO / G, NW = kThreads / 64, WC = 4, WP = NW / WC, NCOL = CPG * 36;
+    const Geom& g = P.rg.g;
+    const int SLOT = P.rg.SLOT;
+    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wc = wave % WC, wp = wave / WC, grp = wc / 2, t0 = (wc % 2) * kWzTiles;
+    const bool dbw = wc % 2 == 0;  // the waves that also sum db (one per group and position group)
+    const int py0 = blockIdx.x * PYB;
+    const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
+    RingLoader<16, 1, NW> ld;
+    ld.init(P.rg, y0, x0, wave, lane);
+    // column 16(t0 + T) + c of the group = (ci, tz', ty, tx): in-plane LDS offset and ring plane tz'
+    int kin[kWzTiles], kdz[kWzTiles];
+#pragma unroll
+    for (int T = 0; T < kWzTiles; ++T) {
+        const int n = 16 * (t0 + T) + c, ci = n / 36, rem = n % 36, q9 = rem % 9;
+        kin[T] = (grp * CPG + ci) * g.CS + (q9 / 3) * g.YS + q9 % 3;
+        kdz[T] = rem / 9;
+    }
+    f4 acc[kWzTiles];
+#pragma unroll
+    for (int T = 0; T < kWzTiles; ++T) acc[T] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    float dbacc = 0.0f;
+    const int ntile = PYB * g.XT;
+    const int ntw = (ntile - wp + WP - 1) / WP;
+    const int chan = g.PD * g.PH * g.PW;
+    const int co = grp * CPG + (c >> 1), sz = c & 1;
+    for (int b = blockIdx.z; b < P.B; b += gridDim.z) {
+        const int64_t srow = P.rows ? P.rows[b] : b;
+        const float* xb = P.x + srow * (int64_t)CO * g.D * g.H * g.W;
+        const uint8_t* amb = P.am + ((int64_t)b * CO + co) * chan;
+        const float* dpb = P.dP + ((int64_t)b * CO + co) * chan;
+        // one register per tile: tile i's dY of row k + 1 is loaded as soon as
+        // row k has consumed it (a rolling prefetch without a second buffer)
+        int abyte[MT];
+        float ad[MT];
+        // lane (c, g) of tile t = (r, tx): window (co, k, py0 + r, 2tx + (g >> 1))
+        auto load_a = [&](int k, int i) {
+            const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
+            const int py = py0 + r, px = 2 * tx + (gq >> 1);
+            const bool ok = i < ntw && py < g.PH && px < g.PW;
+            const int o = (k * g.PH + py) * g.PW + px;
+            abyte[i] = ok ? amb[o] : 0;
+            ad[i] = ok ? dpb[o] : 0.0f;
+        };
+        __syncthreads();  // the previous sample's ring reads are done
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ld.load(xb, P.rg, xs, i, i, wave, lane);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) load_a(0, i);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+        int sb = 0;
+        for (int k = 0; k < g.PD; ++k) {
+            const bool more = k + 1 < g.PD;
+            if (more) {
+                ld.load(xb, P.rg, xs, 2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4, wave, lane);
+                ld.load(xb, P.rg, xs, 2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5, wave, lane);
+            }
+            int kaddr[kWzTiles];
+#pragma unroll
+            for (int T = 0; T < kWzTiles; ++T) {
+                int sl = sb + kdz[T];
+                sl = sl >= kRing ? sl - kRing : sl;
+                kaddr[T] = sl * SLOT + gq + kin[T];
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                if (i >= ntw) continue;  // (not break: a multi-exit loop of 16 stays rolled)
+                const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
+                const int toff = 2 * r * g.YS + 4 * tx;
+                const int byte = abyte[i];
+                const float d = ad[i];
+                if (more) load_a(k + 1, i);
+                float bv[2][kWzTiles];
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+#pragma unroll
+                    for (int T = 0; T < kWzTiles; ++T) bv[q][T] = xs[kaddr[T] + toff + q * g.YS];
+                float a[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q)  // k-step q = conv row 2r + q; window rank (s, q, g & 1)
+                    a[q] = ((byte & 8) && (byte & 7) == sz * 4 + q * 2 + (gq & 1)) ? d : 0.0f;
+                if (dbw) dbacc += a[0] + a[1];
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+#pragma unroll
+                    for (int T = 0; T < kWzTiles; ++T) acc[T] = mfma4(a[q], bv[q][T], acc[T]);
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            __syncthreads();
+            sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+        }
+    }
+    // D (lane (c, g)): row m = 4g + r = (co, s), column 16(t0 + T) + c of the
+    // group -> LDS [WP][G][16][NCOL], db lanes -> [WP][G][64]; then the s pairs,
+    // position groups (and db lanes) are summed in a fixed order
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    constexpr int NCT = ncol_tiles<16>();
+    float* out = P.part + (size_t)blk * (CO * NCT * 16);
+    __syncthreads();
+    float* R = xs;
+    float* Rdb = xs + WP * G * 16 * NCOL;
+#pragma unroll
+    for (int T = 0; T < kWzTiles; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) R[((wp * G + grp) * 16 + 4 * gq + r) * NCOL + 16 * (t0 + T) + c] = acc[T][r];
+    if (dbw) Rdb[(wp * G + grp) * 64 + lane] = dbacc;
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * CPG * CPG * 27; i += kThreads) {
+        const int gg = i / (CPG * CPG * 27), rem = i % (CPG * CPG * 27), col = rem / (CPG * 27),
+                  rem2 = rem % (CPG * 27), cil = rem2 / 27, q = rem2 % 27;
+        float v = 0.0f;
+#pragma unroll
+        for (int w2 = 0; w2 < WP; ++w2)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+                v += R[((w2 * G + gg) * 16 + 2 * col + s2) * NCOL + cil * 36 + (q / 9 + s2) * 9 + q % 9];
+        out[(gg * CPG + col) * (NCT * 16) + (gg * CPG + cil) * 27 + q] = v;
+    }
+    if (threadIdx.x < CO) {
+        const int gg = threadIdx.x / CPG, col = threadIdx.x % CPG;
+        float v = 0.0f;
+        for (int w2 = 0; w2 < WP; ++w2)
+            for (int l = 0; l < 4; ++l)
+                for (int s2 = 0; s2 < 2; ++s2) v += Rdb[(w2 * G + gg) * 64 + 16 * l + 2 * col + s2];
+        out[threadIdx.x * (NCT * 16) + 16 * 27] = v;
     }
 }
 
@@ -1953,6 +2100,22 @@ int launch_wgrad_ring_k(const RingGeom& rg, int32_t B, int gz, const float* x, c
 
 constexpr int kWgradRingBlocks = 512;
 
+template <int PYB, int MT>
+int launch_wgrad_ring_zs_k(const RingGeom& rg, int32_t B, int gz, const float* x, const int64_t* rows,
+                           const float* dP, const uint8_t* am, float* ws, hipStream_t st) {
+    WgradRingParams P{x, rows, dP, am, ws, B, rg};
+    constexpr int WP = kThreads / 64 / 4;
+    const size_t lds =
+        std::max((size_t)kRing * rg.SLOT, (size_t)WP * 2 * 16 * (CO / 2 * 36) + WP * 2 * 64) * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        allow_big_lds(&k_conv_wgrad_ring_zs<PYB, MT>);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_conv_wgrad_ring_zs<PYB, MT>), dim3(rg.nyb, 1, gz), dim3(kThreads), lds, st, P);
+    return RT_OK;
+}
+
 template <int CIN>
 int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                       const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
@@ -1976,6 +2139,32 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
         return launch(rg, gz);
     };
     constexpr int PY_BIG = CIN == 4 ? 4 : 2;
+    // groups = 2 with no pool padding: the z-shift kernel (RT_C3D_WGZS=0: the dense one, A/B runs)
+    static const bool zs_env = [] {
+        const char* e = std::getenv("RT_C3D_WGZS");
+        return !(e && e[0] == '0');
+    }();
+    const bool zs = zs_env && L->groups == 2 && L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0;
+    if constexpr (CIN == 16) {
+        // z-shift: wider y bands (more MFMA work per row barrier), up to 16 tiles per wave
+        auto zs_fits = [&](const RingGeom& rg, int pyb, int mt) {
+            const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * 2 * 16 * (CO / 2 * 36) + WP * 2 * 64);
+            return lds * sizeof(float) <= budget && (rg.npiece + 7) / 8 <= ring_max_pieces<16, 1>() &&
+                   (pyb * rg.g.XT + WP - 1) / WP <= mt;
+        };
+#define RT_WZ_TRY(PYB_, MT_)                                                                          \
+    if (zs && rc == RT_ELIMIT) {                                                                      \
+        RingGeom rg = make_ring_geom<CIN, PYB_, 1, RT_WG_SR>(L, B, kThreads);                         \
+        if (zs_fits(rg, PYB_, MT_))                                                                   \
+            rc = go(rg, [&](const RingGeom& r, int gz) {                                              \
+                return launch_wgrad_ring_zs_k<PYB_, MT_>(r, B, gz, x, rows, dP, am, ws, st);          \
+            });                                                                                       \
+    }
+        if (RT_WZ_MAXPYB >= 4) RT_WZ_TRY(4, 16)
+        RT_WZ_TRY(2, 8)
+        RT_WZ_TRY(1, 8)
+#undef RT_WZ_TRY
+    }
 #define RT_WG_TRY(PYB_, VEC_)                                                                          \
     {                                                                                                 \
         RingGeom rg = make_ring_geom<CIN, PYB_, VEC_, RT_WG_SR>(L, B, kThreads);                      \
