@@ -46,6 +46,10 @@ namespace {
 #ifndef RT_C3D_EXP
 #define RT_C3D_EXP 0
 #endif
+// waves per SIMD the ring weight gradient is compiled for (A/B builds)
+#ifndef RT_WG_WPE
+#define RT_WG_WPE 2
+#endif
 // widest y band of the z-shift weight gradient (A/B builds)
 #ifndef RT_WZ_MAXPYB
 #define RT_WZ_MAXPYB 2
@@ -1234,7 +1238,7 @@ struct WgradRingParams {
 };
 
 template <int CIN, int PYB, int VEC>
-__global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WG_WPE))) void k_conv_wgrad_ring(WgradRingParams P) {
     extern __shared__ float xs[];
     constexpr int NW = kThreads / 64;
     constexpr int NCT = ncol_tiles<CIN>();
@@ -1251,21 +1255,21 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P)
     const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
     RingLoader<CIN, VEC, NW> ld;
     ld.init(P.rg, y0, x0, wave, lane);
-    // column 16(t0c + T) + c = (ci, tap): in-plane LDS offset and dz, or a constant B
-    int kin[kWgradTiles], kdz[kWgradTiles];
-    float kconst[kWgradTiles];
+    // column 16(t0c + T) + c = (ci, tap): 4 * (in-plane LDS offset + g) + dz
+    // (one register per tile), or a constant B.  Only the wave's last tile
+    // can hold constants (columns CIN*27 .. NCT*16-1: conv1's tile 6, the
+    // 16-channel stages' tile 27), so one register carries them.
+    int kpk[kWgradTiles];
+    float kconst = -1.0f;  // tile kWgradTiles-1: -1 = gather, else the constant B value
 #pragma unroll
     for (int T = 0; T < kWgradTiles; ++T) {
         const int k = 16 * (t0c + T) + c;
         if (k < CIN * 27) {
             const int ci = k / 27, q = k % 27;
-            kin[T] = ci * g.CS + ((q / 3) % 3) * g.YS + q % 3;
-            kdz[T] = q / 9;
-            kconst[T] = -1.0f;
+            kpk[T] = (ci * g.CS + ((q / 3) % 3) * g.YS + q % 3 + gq) * 4 + q / 9;
         } else {
-            kin[T] = 0;
-            kdz[T] = 0;
-            kconst[T] = k == CIN * 27 ? 1.0f : 0.0f;
+            kpk[T] = gq * 4;
+            if (T == kWgradTiles - 1) kconst = k == CIN * 27 ? 1.0f : 0.0f;
         }
     }
     f4 acc[kWgradTiles];
@@ -1307,14 +1311,16 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P)
                 ld.load(xb, P.rg, xs, 2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4, wave, lane);
                 ld.load(xb, P.rg, xs, 2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5, wave, lane);
             }
-            int kaddr[4][kWgradTiles];
+            // per z-plane of the tile (q >> 1); the y half (q & 1) joins the
+            // wave-uniform tile offset
+            int kaddr[2][kWgradTiles];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int h = 0; h < 2; ++h)
 #pragma unroll
                 for (int T = 0; T < kWgradTiles; ++T) {
-                    int sl = sb + (q >> 1) + kdz[T];
+                    int sl = sb + h + (kpk[T] & 3);
                     sl = sl >= kRing ? sl - kRing : sl;
-                    kaddr[q][T] = sl * SLOT + (q & 1) * g.YS + gq + kin[T];
+                    kaddr[h][T] = sl * SLOT + (kpk[T] >> 2);
                 }
 #pragma unroll
             for (int i = 0; i < kWgMaxTiles; ++i) {
@@ -1324,20 +1330,22 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring(WgradRingParams P)
                 const int byte = abyte[i];
                 const float d = ad[i];
                 if (more) load_a(k + 1, i);
-                float bv[4][kWgradTiles];
+                // B gathered per z half (RT_WG_WPE 4: fewer live registers)
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
+                for (int h = 0; h < 2; ++h) {
+                    float bv[2][kWgradTiles];
 #pragma unroll
-                    for (int T = 0; T < kWgradTiles; ++T)
-                        bv[q][T] = kconst[T] < 0.0f ? xs[kaddr[q][T] + toff] : kconst[T];
-                float a[4];
+                    for (int q = 0; q < 2; ++q)
 #pragma unroll
-                for (int q = 0; q < 4; ++q)  // position n = 4q + g: zc = q >> 1, yc = q & 1, xc = g
-                    a[q] = ((byte & 8) && (byte & 7) == ((q >> 1) * 4 + (q & 1) * 2 + (gq & 1))) ? d : 0.0f;
+                        for (int T = 0; T < kWgradTiles; ++T)
+                            bv[q][T] = (T < kWgradTiles - 1 || kconst < 0.0f) ? xs[kaddr[h][T] + toff + q * g.YS] : kconst;
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
+                    for (int q = 0; q < 2; ++q) {  // position n = 4(2h + q) + g: zc = h, yc = q, xc = g
+                        const float a = ((byte & 8) && (byte & 7) == h * 4 + q * 2 + (gq & 1)) ? d : 0.0f;
 #pragma unroll
-                    for (int T = 0; T < kWgradTiles; ++T) acc[T] = mfma4(a[q], bv[q][T], acc[T]);
+                        for (int T = 0; T < kWgradTiles; ++T) acc[T] = mfma4(a, bv[q][T], acc[T]);
+                    }
+                }
             }
             __builtin_amdgcn_s_waitcnt(0x0F70);
             __syncthreads();
