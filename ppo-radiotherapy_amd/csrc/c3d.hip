@@ -1086,6 +1086,29 @@ constexpr int ncol_tiles() {
     return (CIN * 27 + 1 + 15) / 16;
 }
 constexpr int kWgradTiles = 7;  // column tiles per wave
+// ring weight gradient: column tiles per wave.  RT_WG_KT4=4 (A/B builds) runs
+// conv1's 7 tiles padded to 8 as 2 column groups of 4 x 4 position groups:
+// 122 VGPRs, 4 waves per SIMD (2 blocks per CU) instead of 2, but +1/7 MFMAs,
+// twice the dY loads and narrower y bands -- measured 15 % slower
+#ifndef RT_WG_KT4
+#define RT_WG_KT4 7
+#endif
+template <int CIN>
+constexpr int wg_kt() {
+    return CIN == 4 ? RT_WG_KT4 : kWgradTiles;
+}
+template <int CIN>
+constexpr int wg_wc() {  // column groups
+    return (ncol_tiles<CIN>() + wg_kt<CIN>() - 1) / wg_kt<CIN>();
+}
+template <int CIN>
+constexpr int wg_nct() {  // padded column tiles: a partial row holds 16 * wg_nct columns
+    return wg_wc<CIN>() * wg_kt<CIN>();
+}
+template <int CIN>
+constexpr int wg_wpe() {
+    return wg_kt<CIN>() < kWgradTiles ? 4 : RT_WG_WPE;
+}
 
 struct WgradParams {
     const float* x;
@@ -1238,19 +1261,22 @@ struct WgradRingParams {
 };
 
 template <int CIN, int PYB, int VEC>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WG_WPE))) void k_conv_wgrad_ring(WgradRingParams P) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VEC == 4 ? wg_wpe<CIN>() : RT_WG_WPE))) void k_conv_wgrad_ring(WgradRingParams P) {
     extern __shared__ float xs[];
     constexpr int NW = kThreads / 64;
-    constexpr int NCT = ncol_tiles<CIN>();
-    constexpr int WC = NCT / kWgradTiles;  // column groups (1 for conv1, 4 for the 16-channel stages)
-    constexpr int WP = NW / WC;            // position groups
-    static_assert(NCT % kWgradTiles == 0, "column tiles");
+    constexpr int KT = wg_kt<CIN>();      // column tiles per wave
+    constexpr int NCT = wg_nct<CIN>();    // padded column tiles
+    constexpr int WC = wg_wc<CIN>();      // column groups (2 for conv1, 4 for the 16-channel stages)
+    constexpr int WP = NW / WC;           // position groups
+    // trailing tiles of a wave that can hold constant columns (k >= CIN*27)
+    constexpr int KC = NCT * 16 - CIN * 27 > 16 ? 2 : 1;
+    static_assert(NW % WC == 0 && KC <= KT, "column tiles");
     const Geom& g = P.rg.g;
     const int SLOT = P.rg.SLOT;
     const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wc = wave % WC, wp = wave / WC;
-    const int t0c = wc * kWgradTiles;
+    const int t0c = wc * KT;
     const int py0 = blockIdx.x * PYB;
     const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
     RingLoader<CIN, VEC, NW> ld;
@@ -1259,22 +1285,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WG_
     // (one register per tile), or a constant B.  Only the wave's last tile
     // can hold constants (columns CIN*27 .. NCT*16-1: conv1's tile 6, the
     // 16-channel stages' tile 27), so one register carries them.
-    int kpk[kWgradTiles];
-    float kconst = -1.0f;  // tile kWgradTiles-1: -1 = gather, else the constant B value
+    int kpk[KT];
+    float kconst[KC];  // tiles KT-KC..: -1 = gather, else the constant B value
 #pragma unroll
-    for (int T = 0; T < kWgradTiles; ++T) {
+    for (int j = 0; j < KC; ++j) kconst[j] = -1.0f;
+#pragma unroll
+    for (int T = 0; T < KT; ++T) {
         const int k = 16 * (t0c + T) + c;
         if (k < CIN * 27) {
             const int ci = k / 27, q = k % 27;
             kpk[T] = (ci * g.CS + ((q / 3) % 3) * g.YS + q % 3 + gq) * 4 + q / 9;
         } else {
             kpk[T] = gq * 4;
-            if (T == kWgradTiles - 1) kconst = k == CIN * 27 ? 1.0f : 0.0f;
+            if (T >= KT - KC) kconst[T - (KT - KC)] = k == CIN * 27 ? 1.0f : 0.0f;
         }
     }
-    f4 acc[kWgradTiles];
+    f4 acc[KT];
 #pragma unroll
-    for (int T = 0; T < kWgradTiles; ++T) acc[T] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int T = 0; T < KT; ++T) acc[T] = f4{0.0f, 0.0f, 0.0f, 0.0f};
     const int ntile = PYB * g.XT;                     // position tiles per pooled row
     const int ntw = (ntile - wp + WP - 1) / WP;       // this wave's: t = wp + WP * i
     const int chan = g.PD * g.PH * g.PW;
@@ -1313,11 +1341,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WG_
             }
             // per z-plane of the tile (q >> 1); the y half (q & 1) joins the
             // wave-uniform tile offset
-            int kaddr[2][kWgradTiles];
+            int kaddr[2][KT];
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
-                for (int T = 0; T < kWgradTiles; ++T) {
+                for (int T = 0; T < KT; ++T) {
                     int sl = sb + h + (kpk[T] & 3);
                     sl = sl >= kRing ? sl - kRing : sl;
                     kaddr[h][T] = sl * SLOT + (kpk[T] >> 2);
@@ -1333,17 +1361,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WG_
                 // B gathered per z half (RT_WG_WPE 4: fewer live registers)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    float bv[2][kWgradTiles];
+                    float bv[2][KT];
 #pragma unroll
                     for (int q = 0; q < 2; ++q)
 #pragma unroll
-                        for (int T = 0; T < kWgradTiles; ++T)
-                            bv[q][T] = (T < kWgradTiles - 1 || kconst < 0.0f) ? xs[kaddr[h][T] + toff + q * g.YS] : kconst;
+                        for (int T = 0; T < KT; ++T)
+                            bv[q][T] = (T < KT - KC || kconst[T >= KT - KC ? T - (KT - KC) : 0] < 0.0f)
+                                           ? xs[kaddr[h][T] + toff + q * g.YS]
+                                           : kconst[T >= KT - KC ? T - (KT - KC) : 0];
 #pragma unroll
                     for (int q = 0; q < 2; ++q) {  // position n = 4(2h + q) + g: zc = h, yc = q, xc = g
                         const float a = ((byte & 8) && (byte & 7) == h * 4 + q * 2 + (gq & 1)) ? d : 0.0f;
 #pragma unroll
-                        for (int T = 0; T < kWgradTiles; ++T) acc[T] = mfma4(a, bv[q][T], acc[T]);
+                        for (int T = 0; T < KT; ++T) acc[T] = mfma4(a, bv[q][T], acc[T]);
                     }
                 }
             }
@@ -1360,7 +1390,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WG_
     __syncthreads();
     float* R = xs;
 #pragma unroll
-    for (int T = 0; T < kWgradTiles; ++T)
+    for (int T = 0; T < KT; ++T)
 #pragma unroll
         for (int r = 0; r < 4; ++r) R[wp * REG + (4 * gq + r) * (NCT * 16) + 16 * (t0c + T) + c] = acc[T][r];
     __syncthreads();
@@ -2094,8 +2124,8 @@ template <int CIN, int PYB, int VEC>
 int launch_wgrad_ring_k(const RingGeom& rg, int32_t B, int gz, const float* x, const int64_t* rows,
                         const float* dP, const uint8_t* am, float* ws, hipStream_t st) {
     WgradRingParams P{x, rows, dP, am, ws, B, rg};
-    constexpr int NCT = ncol_tiles<CIN>();
-    constexpr int WC = NCT / kWgradTiles, WP = (kThreads / 64) / WC;
+    constexpr int NCT = wg_nct<CIN>();
+    constexpr int WC = wg_wc<CIN>(), WP = (kThreads / 64) / WC;
     const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * CO * NCT * 16) * sizeof(float);
     static bool attr = false;
     if (!attr) {
@@ -2127,8 +2157,8 @@ int launch_wgrad_ring_zs_k(const RingGeom& rg, int32_t B, int gz, const float* x
 template <int CIN>
 int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                       const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
-    constexpr int NCT = ncol_tiles<CIN>();
-    constexpr int WC = NCT / kWgradTiles, WP = (kThreads / 64) / WC;
+    constexpr int NCT = wg_nct<CIN>();
+    constexpr int WC = wg_wc<CIN>(), WP = (kThreads / 64) / WC;
     const size_t budget = (CIN == 4 ? 80 : 160) * 1024;
     const bool vec4 = RT_C3D_EXP != 4 && CIN == 4 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
@@ -2186,10 +2216,12 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
         if (vec4) {
             RT_WG_TRY(PY_BIG, 4)
             RT_WG_TRY(PY_BIG / 2, 4)
+            RT_WG_TRY(PY_BIG / 4, 4)
         }
     }
     RT_WG_TRY(PY_BIG, 1)
     RT_WG_TRY(PY_BIG / 2, 1)
+    if constexpr (PY_BIG / 4 >= 1) RT_WG_TRY(PY_BIG / 4, 1)
 #undef RT_WG_TRY
     if (rc != RT_OK) return rc == RT_ELIMIT ? rt_internal_fail(RT_ELIMIT, "rt_conv_wgrad: ring exceeds LDS") : rc;
     const int nout = CO * (L->cin / L->groups) * 27 + CO;
@@ -2251,8 +2283,8 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
 extern "C" int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* L, int32_t batch) {
     if (bad_layer(L) || batch < 1) return 0;
     if (RT_C3D_EXP != 3) {  // ring: at most kWgradRingBlocks partial rows (one per block)
-        if (L->cin == 4) return (int64_t)kWgradRingBlocks * CO * ncol_tiles<4>() * 16;
-        return (int64_t)kWgradRingBlocks * CO * ncol_tiles<16>() * 16;
+        if (L->cin == 4) return (int64_t)kWgradRingBlocks * CO * wg_nct<4>() * 16;
+        return (int64_t)kWgradRingBlocks * CO * wg_nct<16>() * 16;
     }
     if (L->cin == 4) return (int64_t)wgrad_blocks<4, 2, 4>(L, batch) * CO * ncol_tiles<4>() * 16;
     return (int64_t)wgrad_blocks<16, 1, 2>(L, batch) * CO * ncol_tiles<16>() * 16;
