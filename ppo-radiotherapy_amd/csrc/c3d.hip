@@ -872,35 +872,48 @@ __global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
             const int itc = ok ? it : nitem - 1;
             const int yt = itc / nxp, xp = itc - yt * nxp;
             const int tb = 4 * yt * g.YS + 8 * xp;
+            // wave-uniform padding skips: a y tile past the last pooled row stores
+            // nothing (no MFMAs), an item whose second x tile is past XT runs one
+            // accumulator
+            const bool live = ok && py0 + 2 * yt < g.PH;
+            const bool two = 2 * xp + 1 < g.XT;
             float bv[2][2][9];
-            auto fetch = [&](float (&dst)[2][9], int bj) {
+            auto fetch = [&](float (&dst)[2][9], int bj, auto two_t) {
                 const int base = zoff[bj / QPB] + (bj % QPB) * 4 * g.CS + tb;
 #pragma unroll
                 for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
                     for (int tx = 0; tx < 3; ++tx) {
                         dst[0][ty * 3 + tx] = xs[base + ty * g.YS + tx];
-                        dst[1][ty * 3 + tx] = xs[base + ty * g.YS + tx + 4];
+                        if constexpr (decltype(two_t)::value) dst[1][ty * 3 + tx] = xs[base + ty * g.YS + tx + 4];
                     }
             };
-            fetch(bv[0], 0);
+            fetch(bv[0], 0, std::true_type{});
             epi(pacc, pyt, pxp, ppz, pok);  // the previous item's epilogue, between this item's MFMAs
             f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+            auto mloop = [&](auto two_t) {
 #pragma unroll
-            for (int bj = 0; bj < NB; ++bj) {
-                if (bj + 1 < NB) fetch(bv[(bj + 1) & 1], bj + 1);
+                for (int bj = 0; bj < NB; ++bj) {
+                    if (bj + 1 < NB) fetch(bv[(bj + 1) & 1], bj + 1, two_t);
 #pragma unroll
-                for (int q = 0; q < 9; ++q) {
-                    acc[0] = mfma4(bv[bj & 1][0][q], bw[bj * 9 + q], acc[0]);
-                    acc[1] = mfma4(bv[bj & 1][1][q], bw[bj * 9 + q], acc[1]);
+                    for (int q = 0; q < 9; ++q) {
+                        acc[0] = mfma4(bv[bj & 1][0][q], bw[bj * 9 + q], acc[0]);
+                        if constexpr (decltype(two_t)::value) acc[1] = mfma4(bv[bj & 1][1][q], bw[bj * 9 + q], acc[1]);
+                    }
                 }
+            };
+            if (live) {
+                if (two)
+                    mloop(std::true_type{});
+                else
+                    mloop(std::false_type{});
             }
             pacc[0] = acc[0];
             pacc[1] = acc[1];
             pyt = yt;
             pxp = xp;
             ppz = k;
-            pok = ok;
+            pok = live;
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next row has landed
         __syncthreads();                     // ... every wave's; and nobody still reads the slots reloaded next
@@ -1354,6 +1367,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VEC ==
             for (int i = 0; i < kWgMaxTiles; ++i) {
                 if (i >= ntw) continue;
                 const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
+                if (py0 + r >= g.PH) continue;  // a tile row past the last pooled row: A = 0, no MFMAs
                 const int toff = 2 * r * g.YS + 4 * tx;
                 const int byte = abyte[i];
                 const float d = ad[i];
@@ -1489,6 +1503,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring_zs(WgradRingParams
             for (int i = 0; i < MT; ++i) {
                 if (i >= ntw) continue;  // (not break: a multi-exit loop of 16 stays rolled)
                 const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
+                if (py0 + r >= g.PH) continue;  // a tile row past the last pooled row: A = 0, no MFMAs
                 const int toff = 2 * r * g.YS + 4 * tx;
                 const int byte = abyte[i];
                 const float d = ad[i];
