@@ -46,6 +46,12 @@ namespace {
 #ifndef RT_C3D_EXP
 #define RT_C3D_EXP 0
 #endif
+// blocks the z-shift forward / data-gradient grids aim for when they split z into
+// chunks (A/B builds): 2048 (no split at 512 samples) beat 4096 / 8192 -- a block
+// that sweeps the whole depth pays its weight load and ring prologue once
+#ifndef RT_ZS_BLOCKS
+#define RT_ZS_BLOCKS 2048
+#endif
 // waves per SIMD the ring weight gradient is compiled for (A/B builds)
 #ifndef RT_WG_WPE
 #define RT_WG_WPE 2
@@ -749,7 +755,7 @@ RingGeom make_ring_geom_zs(const rt_conv_layer* L, int B) {
     r.npiece = (r.SLOT + 63) / 64;
     r.nyb = (g.PH + PYB - 1) / PYB;
     const int64_t per_chunk = (int64_t)r.nyb * B * G;
-    int nzc = (int)std::min<int64_t>(g.PD, std::max<int64_t>(1, (4096 + per_chunk - 1) / per_chunk));
+    int nzc = (int)std::min<int64_t>(g.PD, std::max<int64_t>(1, (RT_ZS_BLOCKS + per_chunk - 1) / per_chunk));
     r.ZC = (g.PD + nzc - 1) / nzc;
     r.ZC = (r.ZC + G / 2 - 1) / (G / 2) * (G / 2);  // whole tiles (G / 2 pooled rows each) per chunk
     return r;
@@ -2053,7 +2059,7 @@ RingGeom make_dgrad_ring_geom_zs(const rt_conv_layer* L, int B) {
     r.SLOT = round_mod(CO / G * g.CS, 16);
     const int KD = (g.D + 1) / 2;
     const int64_t per_chunk = (int64_t)r.nyb * B * G;
-    const int nzc = (int)std::min<int64_t>(KD, std::max<int64_t>(1, (4096 + per_chunk - 1) / per_chunk));
+    const int nzc = (int)std::min<int64_t>(KD, std::max<int64_t>(1, (RT_ZS_BLOCKS + per_chunk - 1) / per_chunk));
     r.ZC = (KD + nzc - 1) / nzc;
     r.ZC = (r.ZC + G / 2 - 1) / (G / 2) * (G / 2);  // whole tile rows per chunk
     return r;

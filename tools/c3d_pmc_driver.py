@@ -1,5 +1,5 @@
 """Runs each C3D stage kernel a few times at 64^3 (batch 64) -- a target for
-rocprofv3 --pmc (tools/bench_c3d_kernels.py times them)."""
+rocprofv3 --pmc (tools/bench_c3d_kernels.py times them); C3D_PMC_B sets the batch."""
 import ctypes
 import os
 import sys
@@ -10,10 +10,10 @@ import torch  # noqa: E402
 
 from ppo_radiotherapy_amd import _lib  # noqa: E402
 
-B = 64
+B = int(os.environ.get("C3D_PMC_B", "64"))
 dev = torch.device("cuda")
 L = _lib.load()
-for cin, groups, dims in [(4, 1, (64, 64, 64)), (16, 2, (31, 31, 31))]:
+for cin, groups, dims in [(4, 1, (64, 64, 64)), (16, 2, (31, 31, 31)), (16, 4, (14, 14, 14))]:
     x = torch.rand((B, cin, *dims), device=dev)
     w = torch.randn((16, cin // groups, 3, 3, 3), device=dev) * 0.1
     b = torch.randn(16, device=dev) * 0.1
@@ -30,7 +30,7 @@ for cin, groups, dims in [(4, 1, (64, 64, 64)), (16, 2, (31, 31, 31))]:
                                 am.data_ptr(), None)
         L.rt_conv_relu_pool_wgrad(ctypes.byref(lay), B, x.data_ptr(), None, gy.data_ptr(), am.data_ptr(),
                                   dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(), None)
-        if cin == 16:
+        if cin == 16:  # the grouped stages also get the data gradient
             dx = torch.empty_like(x)
             L.rt_conv_relu_pool_dgrad(ctypes.byref(lay), B, w.data_ptr(), gy.data_ptr(), am.data_ptr(),
                                       dx.data_ptr(), None)
