@@ -2157,7 +2157,11 @@ int launch_wgrad_ring_k(const RingGeom& rg, int32_t B, int gz, const float* x, c
     return RT_OK;
 }
 
-constexpr int kWgradRingBlocks = 512;
+// weight-gradient ring grids: at most this many blocks (samples looped per block; A/B builds)
+#ifndef RT_WG_BLOCKS
+#define RT_WG_BLOCKS 512
+#endif
+constexpr int kWgradRingBlocks = RT_WG_BLOCKS;
 
 template <int PYB, int MT>
 int launch_wgrad_ring_zs_k(const RingGeom& rg, int32_t B, int gz, const float* x, const int64_t* rows,
