@@ -77,6 +77,10 @@ class PPOTrainer:
         self.agent = agent
         self.device = torch.device(device)
         self.rank, self.world = rank, world
+        # the collective code path (all-reduces between the update kernels): on
+        # exactly when world > 1; tests/test_gpu_rccl.py forces it at world 1 to run
+        # the RCCL calls against the single-call update on one GPU
+        self.collective = world > 1
         self.gen = generator
         N, T = env.num_envs, int(cfg.num_steps)
         self.N, self.T = N, T
@@ -337,14 +341,14 @@ class PPOTrainer:
 
     # ------------------------------------------------------------------ update
     def _allreduce_(self, t: torch.Tensor, average: bool = True):
-        if self.world > 1:
+        if self.collective:
             dist.all_reduce(t)
             if average:
                 t.div_(self.world)
         return t
 
     def _norm_adv(self, adv: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if not self.collective:
             return (adv - adv.mean()) / (adv.std() + 1e-8)
         a = adv.double()
         s = torch.stack([a.sum(), (a * a).sum(), torch.tensor(float(a.numel()), dtype=torch.float64,
@@ -450,7 +454,7 @@ class PPOTrainer:
             self.record_perms.append(perm.clone())
         if not self.cfg.norm_adv:
             return perm, None
-        if self.world > 1:
+        if self.collective:
             # this rank's (sum, sum of squares) per minibatch -> ONE all-reduce
             # of [n_mb, 2] f64 -> global (mean, std) over mbs x world rows
             _lib.check(L.rt_ppo_adv_sums(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, n_mb,
@@ -487,7 +491,7 @@ class PPOTrainer:
         for _ in range(int(self.cfg.update_epochs)):
             perm, adv = self._epoch_perm_stats(L, stream, n_mb)
             k = n_mb if not self.max_minibatches else min(n_mb, self.max_minibatches - done)
-            if self.world == 1:
+            if not self.collective:
                 _lib.check(L.rt_ppo_update(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch), perm.data_ptr(),
                                            mbs, k, _lib.ptr(adv), hp, self.flat_param.data_ptr(),
                                            self.flat_grad.data_ptr(), self._exp_avg.data_ptr(),
