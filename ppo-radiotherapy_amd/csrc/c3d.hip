@@ -56,6 +56,12 @@ namespace {
 #ifndef RT_WG_WPE
 #define RT_WG_WPE 2
 #endif
+// dense ring weight gradient: 1 = the next row's dY operands loaded into a
+// second register set at the row start (beside the plane DMA) instead of the
+// rolling one-register-per-tile prefetch (A/B builds)
+#ifndef RT_WG_DYB
+#define RT_WG_DYB 0
+#endif
 // widest y band of the z-shift weight gradient (A/B builds)
 #ifndef RT_WZ_MAXPYB
 #define RT_WZ_MAXPYB 2
@@ -1335,15 +1341,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VEC ==
         // the row start measured 18 % slower in the z-shift kernel)
         int abyte[kWgMaxTiles];
         float ad[kWgMaxTiles];
+#if RT_WG_DYB
+        int abyte2[kWgMaxTiles] = {};
+        float ad2[kWgMaxTiles] = {};
+#endif
         // lane (c, g) of tile t: channel c at the 4 positions 4q + g, all in pooled window px = 2tx + (g >> 1)
-        auto load_a = [&](int k, int i) {
+        auto load_to = [&](int k, int i, int (&ab)[kWgMaxTiles], float (&av)[kWgMaxTiles]) {
             const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
             const int py = py0 + r, px = 2 * tx + (gq >> 1);
             const bool ok = i < ntw && py < g.PH && px < g.PW;
             const int o = (k * g.PH + py) * g.PW + px;
-            abyte[i] = ok ? amb[o] : 0;
-            ad[i] = ok ? dpb[o] : 0.0f;
+            ab[i] = ok ? amb[o] : 0;
+            av[i] = ok ? dpb[o] : 0.0f;
         };
+        auto load_a = [&](int k, int i) { load_to(k, i, abyte, ad); };
         __syncthreads();  // the previous sample's ring reads are done
 #pragma unroll
         for (int i = 0; i < 4; ++i) ld.load(xb, P.rg, xs, i, i, wave, lane);
@@ -1357,6 +1368,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VEC ==
             if (more) {
                 ld.load(xb, P.rg, xs, 2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4, wave, lane);
                 ld.load(xb, P.rg, xs, 2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5, wave, lane);
+#if RT_WG_DYB
+#pragma unroll
+                for (int i = 0; i < kWgMaxTiles; ++i) load_to(k + 1, i, abyte2, ad2);
+#endif
             }
             // per z-plane of the tile (q >> 1); the y half (q & 1) joins the
             // wave-uniform tile offset
@@ -1377,7 +1392,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VEC ==
                 const int toff = 2 * r * g.YS + 4 * tx;
                 const int byte = abyte[i];
                 const float d = ad[i];
-                if (more) load_a(k + 1, i);
+                if (!RT_WG_DYB && more) load_a(k + 1, i);
                 // B gathered per z half (RT_WG_WPE 4: fewer live registers)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -1400,6 +1415,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VEC ==
             __builtin_amdgcn_s_waitcnt(0x0F70);
             __syncthreads();
             sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+#if RT_WG_DYB
+#pragma unroll
+            for (int i = 0; i < kWgMaxTiles; ++i) {
+                abyte[i] = abyte2[i];
+                ad[i] = ad2[i];
+            }
+#endif
         }
     }
     // D (lane (c, g)): rows co = 4g + r, column 16T + c; the WP position
