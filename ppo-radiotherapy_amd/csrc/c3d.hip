@@ -62,6 +62,17 @@ namespace {
 #ifndef RT_WG_DYB
 #define RT_WG_DYB 0
 #endif
+// z-shift forward: widest y band tried first, and (when defined) waves per SIMD
+// it is compiled for (A/B builds: 4 pooled rows at 4 waves per SIMD = two
+// blocks per CU measured 1.59 vs 1.34 ms for conv2, 4 rows at 2 waves 1.47)
+#ifndef RT_ZS_FWD_MAXPYB
+#define RT_ZS_FWD_MAXPYB 8
+#endif
+#ifdef RT_ZS_FWD_WPE
+#define RT_ZS_FWD_ATTR __attribute__((amdgpu_waves_per_eu(RT_ZS_FWD_WPE)))
+#else
+#define RT_ZS_FWD_ATTR
+#endif
 // widest y band of the z-shift weight gradient (A/B builds)
 #ifndef RT_WZ_MAXPYB
 #define RT_WZ_MAXPYB 2
@@ -774,7 +785,7 @@ constexpr int ring_zs_slots() {
 }
 
 template <int G, int PYB, bool TRAIN>
-__global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
+__global__ __launch_bounds__(512) RT_ZS_FWD_ATTR void k_conv_ring_zs(RingParams P) {
     extern __shared__ float xs[];
     constexpr int CPG = CO / G, NW = 8, ZX = G + 2, KS = CPG * ZX * 9 / 4, NB = KS / 9, NR = ring_zs_slots<G>();
     constexpr int QPB = CPG / 4;  // channel quads per plane: batch bj = (tz' = bj / QPB, quad bj % QPB)
@@ -964,7 +975,7 @@ int launch_ring_zs(const rt_conv_layer* L, int32_t B, const float* x, const int6
                (rg.npiece + 7) / 8 <= ring_max_pieces<CO / G, 1>();
     };
     RingGeom rg = make_ring_geom_zs<G, 8>(L, B);
-    if (fits(rg)) return launch_ring_zs_k<G, 8>(rg, B, x, rows, w, bias, y, amax, st);
+    if (RT_ZS_FWD_MAXPYB >= 8 && fits(rg)) return launch_ring_zs_k<G, 8>(rg, B, x, rows, w, bias, y, amax, st);
     rg = make_ring_geom_zs<G, 4>(L, B);
     if (fits(rg)) return launch_ring_zs_k<G, 4>(rg, B, x, rows, w, bias, y, amax, st);
     rg = make_ring_geom_zs<G, 2>(L, B);
