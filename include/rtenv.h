@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTENV_ABI_VERSION 1
+#define RTENV_ABI_VERSION 2  /* 2: rt_env_config.struct_size (first member) */
 
 enum {
     RT_OK = 0,
@@ -84,6 +84,11 @@ enum {
 };
 
 typedef struct {
+    /* size handshake: the caller sets struct_size = sizeof(rt_env_config) BEFORE
+     * rt_env_config_default / rt_env_create; both return RT_EINVAL without
+     * touching the struct when it differs, so a binding with a stale (shorter or
+     * longer) declaration is rejected instead of overrun. */
+    uint32_t struct_size;
     /* geometry */
     int32_t grid[3];          /* D, H, W (LUNG_SHAPE, environment.py:30) */
     int32_t num_envs;         /* envs owned by this handle */
@@ -110,6 +115,8 @@ typedef struct {
     int32_t step_mode;        /* RT_STEP_DENSE (default) or RT_STEP_INCREMENTAL */
 } rt_env_config;
 
+/* Fill the reference's constants (environment.py:16-30); cfg->struct_size must
+ * already hold sizeof(rt_env_config) (kept; everything else is overwritten). */
 int rt_env_config_default(rt_env_config* cfg);
 
 int rt_env_create(const rt_env_config* cfg, int device, rt_env** out);
@@ -260,7 +267,8 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* step, float* obs_d, fl
  * are left in obs_d / terminated_d after the last step.  Same bits as
  * n_steps calls of rt_env_step_policy.  RT_EINVAL for a vision handle;
  * RT_ELIMIT if the persistent kernel's LDS layout cannot be built (callers
- * then step with rt_env_step_policy; not reached for the visionless MLP). */
+ * then step with rt_env_step_policy; not reached for the visionless MLP --
+ * tumours above its LDS share keep their sum plan in global scratch). */
 typedef struct rt_policy_rollout {
     rt_policy_step step;          /* storage row of the first step, its counter */
     int32_t n_steps;
@@ -272,10 +280,13 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* 
                           void* stream);
 /* Env groups of the dense-mode rt_env_rollout_policy: 2..4 (pipelined
  * library streams taking turns on k_dense in a ring; default 2), 1 (every
- * launch on the caller's stream) or 0 (one
- * persistent launch: each env's wave runs policy, march, the dense lung
- * reduction of its own row and the finish, step after step; the launch
- * returns RT_ELIMIT when the library's largest tumour does not fit). */
+ * launch on the caller's stream) or 0 (one persistent launch: each env's wave
+ * runs policy, march, the dense lung reduction of its own row and the finish,
+ * step after step).  Setting 0 allocates the persistent kernel's global plan
+ * scratch ([N][2 * largest tumour] f32) when the library's largest tumour
+ * exceeds its LDS share -- a setup call, not graph-capturable; the rollout
+ * returns RT_ELIMIT only when the per-wave LDS region cannot hold even the
+ * policy's activations. */
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:

@@ -47,8 +47,14 @@ class RtError(RuntimeError):
     pass
 
 
+ABI_VERSION = 2  # RTENV_ABI_VERSION of include/rtenv.h
+
+
 class RtEnvConfig(ctypes.Structure):
+    """rt_env_config (include/rtenv.h); struct_size is set on construction
+    (the library rejects a config whose struct_size != its sizeof)."""
     _fields_ = [
+        ("struct_size", ctypes.c_uint32),
         ("grid", ctypes.c_int32 * 3),
         ("num_envs", ctypes.c_int32),
         ("visionless", ctypes.c_int32),
@@ -70,6 +76,11 @@ class RtEnvConfig(ctypes.Structure):
         ("env_id_base", ctypes.c_int64),
         ("step_mode", ctypes.c_int32),
     ]
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if not self.struct_size:
+            self.struct_size = ctypes.sizeof(self)
 
 
 class RtPpoBatch(ctypes.Structure):
@@ -183,6 +194,8 @@ def load(build_if_missing: bool = True):
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    if L.rt_abi_version() != ABI_VERSION:
+        raise RtError(f"{LIB_PATH}: ABI {L.rt_abi_version()} != {ABI_VERSION} expected by this package (rebuild it)")
     _lib = L
     return L
 

@@ -714,8 +714,8 @@ int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* ro
     const size_t lds = (size_t)kRing * rg.SLOT * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, true>);
-        allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, false>);
+        if (const int rc_lds = allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, true>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, false>)) return rc_lds;
         attr = true;
     }
     dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, B);
@@ -952,8 +952,8 @@ int launch_ring_zs_k(const RingGeom& rg, int32_t B, const float* x, const int64_
     const size_t lds = (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_ring_zs<G, PYB, true>);
-        allow_big_lds(&k_conv_ring_zs<G, PYB, false>);
+        if (const int rc_lds = allow_big_lds(&k_conv_ring_zs<G, PYB, true>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_ring_zs<G, PYB, false>)) return rc_lds;
         attr = true;
     }
     dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, G * B);
@@ -985,34 +985,44 @@ int launch_ring_zs(const rt_conv_layer* L, int32_t B, const float* x, const int6
 
 // the forward: the widest y band whose ring fits the LDS budget (80 KiB: two
 // 8-wave blocks per CU for conv1; the 16-channel stages hold 2 waves per SIMD
-// by registers, one 8-wave block per CU, 160 KiB)
+// by registers, one 8-wave block per CU, 160 KiB).  Wider planes: conv1 takes
+// the whole 160 KiB (one block per CU), then one-row bands; RT_ELIMIT when even
+// that ring does not fit (the caller falls back to the tile kernel).
 template <int CIN, int G>
 int launch_fwd_ring(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
                     const float* bias, float* y, uint8_t* amax, hipStream_t st) {
     constexpr int NTH = 512;
-    const size_t budget = (CIN == 4 ? 80 : 160) * 1024;
     const bool vec4 = RT_C3D_EXP != 4 && CIN == 4 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    auto fits = [&](const RingGeom& rg, int vec) {
+    auto fits = [&](const RingGeom& rg, int vec, size_t budget) {
         return (size_t)kRing * rg.SLOT * sizeof(float) <= budget &&
                (rg.npiece + NTH / 64 - 1) / (NTH / 64) <= (vec == 4 ? ring_max_pieces<CIN, 4>()
                                                                    : ring_max_pieces<CIN, 1>()) &&
                rg.g.W >= vec;
     };
     constexpr int PY_BIG = CIN == 4 ? 4 : 2;
-    if constexpr (CIN == 4) {
-        if (!vec4) goto scalar;
-        RingGeom rg = make_ring_geom<CIN, PY_BIG, 4>(L, B, NTH);
-        if (fits(rg, 4)) return launch_ring<CIN, G, PY_BIG, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
-        rg = make_ring_geom<CIN, PY_BIG / 2, 4>(L, B, NTH);
-        if (fits(rg, 4)) return launch_ring<CIN, G, PY_BIG / 2, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+    for (const size_t budget : {(size_t)(CIN == 4 ? 80 : 160) * 1024, (size_t)160 * 1024}) {
+        if constexpr (CIN == 4) {
+            if (vec4) {
+                RingGeom rg = make_ring_geom<CIN, PY_BIG, 4>(L, B, NTH);
+                if (fits(rg, 4, budget)) return launch_ring<CIN, G, PY_BIG, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+                rg = make_ring_geom<CIN, PY_BIG / 2, 4>(L, B, NTH);
+                if (fits(rg, 4, budget))
+                    return launch_ring<CIN, G, PY_BIG / 2, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+            }
+        }
+        RingGeom rg = make_ring_geom<CIN, PY_BIG, 1>(L, B, NTH);
+        if (fits(rg, 1, budget)) return launch_ring<CIN, G, PY_BIG, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+        rg = make_ring_geom<CIN, PY_BIG / 2, 1>(L, B, NTH);
+        if (fits(rg, 1, budget)) return launch_ring<CIN, G, PY_BIG / 2, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+        if constexpr (PY_BIG / 4 >= 1) {
+            rg = make_ring_geom<CIN, PY_BIG / 4, 1>(L, B, NTH);
+            if (fits(rg, 1, budget))
+                return launch_ring<CIN, G, PY_BIG / 4, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+        }
+        if (CIN != 4) break;  // the 16-channel stages already tried the whole 160 KiB
     }
-scalar:
-    RingGeom rg = make_ring_geom<CIN, PY_BIG, 1>(L, B, NTH);
-    if (fits(rg, 1)) return launch_ring<CIN, G, PY_BIG, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
-    rg = make_ring_geom<CIN, PY_BIG / 2, 1>(L, B, NTH);
-    if (fits(rg, 1)) return launch_ring<CIN, G, PY_BIG / 2, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
-    return rt_internal_fail(RT_ELIMIT, "rt_conv: input plane ring exceeds LDS (grid too wide)");
+    return RT_ELIMIT;
 }
 
 // ---------------------------------------------------------------------------
@@ -1652,9 +1662,10 @@ __global__ __launch_bounds__(64 * kRedWaves) void k_wgrad_reduce(const float* pa
 }
 
 template <class K>
-void allow_big_lds(K* kern) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+int allow_big_lds(K* kern) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return e == hipSuccess ? RT_OK : rt_internal_fail(RT_EDEVICE, hipGetErrorString(e));
 }
 
 template <int CIN, int G, int PZB, int PYB>
@@ -1672,8 +1683,8 @@ int launch_fwd(const rt_conv_layer* L, int32_t B, const float* x, const int64_t*
     if (lds > 160 * 1024) return rt_internal_fail(RT_ELIMIT, "rt_conv: input tile exceeds LDS (grid too wide)");
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_relu_pool<CIN, G, PZB, PYB, true>);
-        allow_big_lds(&k_conv_relu_pool<CIN, G, PZB, PYB, false>);
+        if (const int rc_lds = allow_big_lds(&k_conv_relu_pool<CIN, G, PZB, PYB, true>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_relu_pool<CIN, G, PZB, PYB, false>)) return rc_lds;
         attr = true;
     }
     dim3 grid((P.g.PH + PYB - 1) / PYB, (P.g.PD + PZB - 1) / PZB, B);
@@ -1711,7 +1722,7 @@ int launch_dgrad(const rt_conv_layer* L, int32_t B, const float* w, const float*
     if (lds > 160 * 1024) return rt_internal_fail(RT_ELIMIT, "rt_conv_dgrad: tile exceeds LDS");
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_dgrad<G, PZB, PYB>);
+        if (const int rc_lds = allow_big_lds(&k_conv_dgrad<G, PZB, PYB>)) return rc_lds;
         attr = true;
     }
     dim3 grid((P.g.H + 2 * PYB - 1) / (2 * PYB), (P.g.D + 2 * PZB - 1) / (2 * PZB), B);
@@ -1883,7 +1894,7 @@ int launch_dgrad_ring_k(const RingGeom& rg, int32_t B, const float* w, const flo
     const size_t lds = (size_t)kRing * rg.SLOT * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_dgrad_ring<G, PYB, kDgradRingThreads>);
+        if (const int rc_lds = allow_big_lds(&k_conv_dgrad_ring<G, PYB, kDgradRingThreads>)) return rc_lds;
         attr = true;
     }
     dim3 grid(rg.nyb, ((rg.g.D + 1) / 2 + rg.ZC - 1) / rg.ZC, B);
@@ -2105,7 +2116,7 @@ int launch_dgrad_ring_zs_k(const RingGeom& rg, int32_t B, const float* w, const 
     const size_t lds = (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_dgrad_ring_zs<G, PYB>);
+        if (const int rc_lds = allow_big_lds(&k_conv_dgrad_ring_zs<G, PYB>)) return rc_lds;
         attr = true;
     }
     dim3 grid(rg.nyb, ((rg.g.D + 1) / 2 + rg.ZC - 1) / rg.ZC, G * B);
@@ -2161,7 +2172,7 @@ int launch_wgrad(const rt_conv_layer* L, int32_t B, const float* x, const int64_
     if (lds > 160 * 1024) return rt_internal_fail(RT_ELIMIT, "rt_conv_wgrad: tile exceeds LDS");
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_wgrad<CIN, PZB, PYB>);
+        if (const int rc_lds = allow_big_lds(&k_conv_wgrad<CIN, PZB, PYB>)) return rc_lds;
         attr = true;
     }
     hipLaunchKernelGGL((k_conv_wgrad<CIN, PZB, PYB>), dim3(nblk), dim3(kThreads), lds, st, P);
@@ -2183,7 +2194,7 @@ int launch_wgrad_ring_k(const RingGeom& rg, int32_t B, int gz, const float* x, c
     const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * CO * NCT * 16) * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_wgrad_ring<CIN, PYB, VEC>);
+        if (const int rc_lds = allow_big_lds(&k_conv_wgrad_ring<CIN, PYB, VEC>)) return rc_lds;
         attr = true;
     }
     hipLaunchKernelGGL((k_conv_wgrad_ring<CIN, PYB, VEC>), dim3(rg.nyb, 1, gz), dim3(kThreads), lds, st, P);
@@ -2205,7 +2216,7 @@ int launch_wgrad_ring_zs_k(const RingGeom& rg, int32_t B, int gz, const float* x
         std::max((size_t)kRing * rg.SLOT, (size_t)WP * 2 * 16 * (CO / 2 * 36) + WP * 2 * 64) * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        allow_big_lds(&k_conv_wgrad_ring_zs<PYB, MT>);
+        if (const int rc_lds = allow_big_lds(&k_conv_wgrad_ring_zs<PYB, MT>)) return rc_lds;
         attr = true;
     }
     hipLaunchKernelGGL((k_conv_wgrad_ring_zs<PYB, MT>), dim3(rg.nyb, 1, gz), dim3(kThreads), lds, st, P);
@@ -2217,7 +2228,7 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
                       const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
     constexpr int NCT = wg_nct<CIN>();
     constexpr int WC = wg_wc<CIN>(), WP = (kThreads / 64) / WC;
-    const size_t budget = (CIN == 4 ? 80 : 160) * 1024;
+    size_t budget = (CIN == 4 ? 80 : 160) * 1024;  // conv1 retries with 160 KiB below (wide planes)
     const bool vec4 = RT_C3D_EXP != 4 && CIN == 4 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     auto fits = [&](const RingGeom& rg, int vec) {
@@ -2270,18 +2281,21 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
                 return launch_wgrad_ring_k<CIN, PYB_, VEC_>(r, B, gz, x, rows, dP, am, ws, st);       \
             });                                                                                       \
     }
-    if constexpr (CIN == 4) {
-        if (vec4) {
-            RT_WG_TRY(PY_BIG, 4)
-            RT_WG_TRY(PY_BIG / 2, 4)
-            RT_WG_TRY(PY_BIG / 4, 4)
+    for (int pass = 0; pass < (CIN == 4 ? 2 : 1) && rc == RT_ELIMIT; ++pass) {
+        if (pass) budget = 160 * 1024;
+        if constexpr (CIN == 4) {
+            if (vec4) {
+                RT_WG_TRY(PY_BIG, 4)
+                RT_WG_TRY(PY_BIG / 2, 4)
+                RT_WG_TRY(PY_BIG / 4, 4)
+            }
         }
+        RT_WG_TRY(PY_BIG, 1)
+        RT_WG_TRY(PY_BIG / 2, 1)
+        if constexpr (PY_BIG / 4 >= 1) RT_WG_TRY(PY_BIG / 4, 1)
     }
-    RT_WG_TRY(PY_BIG, 1)
-    RT_WG_TRY(PY_BIG / 2, 1)
-    if constexpr (PY_BIG / 4 >= 1) RT_WG_TRY(PY_BIG / 4, 1)
 #undef RT_WG_TRY
-    if (rc != RT_OK) return rc == RT_ELIMIT ? rt_internal_fail(RT_ELIMIT, "rt_conv_wgrad: ring exceeds LDS") : rc;
+    if (rc != RT_OK) return rc;  // RT_ELIMIT: the caller falls back to the tile kernel
     const int nout = CO * (L->cin / L->groups) * 27 + CO;
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((nout + 63) / 64), dim3(64 * kRedWaves), 0, st, (const float*)ws, nblk, L->cin,
                        L->groups, NCT * 16, dw, db);
@@ -2297,6 +2311,27 @@ bool bad_layer(const rt_conv_layer* L) {
     for (int a = 0; a < 3; ++a)
         if (L->in_dims[a] < 4 || L->pool_pad[a] < 0 || L->pool_pad[a] > 1) return true;
     return false;
+}
+
+// the one-region-per-block tile kernels (before the plane rings; kept as the
+// fallback for planes too wide for a ring and for A/B builds)
+int fwd_tile(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
+             const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+    if (L->cin == 4) return launch_fwd<4, 1, 2, 4>(L, B, x, rows, w, bias, y, amax, st);
+    if (L->groups == 1) return launch_fwd<16, 1, 1, 2>(L, B, x, rows, w, bias, y, amax, st);
+    if (L->groups == 2) return launch_fwd<16, 2, 1, 2>(L, B, x, rows, w, bias, y, amax, st);
+    return launch_fwd<16, 4, 1, 2>(L, B, x, rows, w, bias, y, amax, st);
+}
+
+int64_t wgrad_tile_ws(const rt_conv_layer* L, int32_t B) {
+    if (L->cin == 4) return (int64_t)wgrad_blocks<4, 2, 4>(L, B) * CO * ncol_tiles<4>() * 16;
+    return (int64_t)wgrad_blocks<16, 1, 2>(L, B) * CO * ncol_tiles<16>() * 16;
+}
+
+int wgrad_tile(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dy,
+               const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
+    if (L->cin == 4) return launch_wgrad<4, 2, 4>(L, B, x, rows, dy, am, dw, db, ws, ws_floats, st);
+    return launch_wgrad<16, 1, 2>(L, B, x, rows, dy, am, dw, db, ws, ws_floats, st);
 }
 
 }  // namespace
@@ -2316,36 +2351,38 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     if (bad_layer(L) || batch < 1 || batch > 65535 || !x_d || !w_d || !b_d || !y_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_fwd: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (RT_C3D_EXP == 3) {  // the previous one-region-per-block forward (A/B builds)
-        if (L->cin == 4) return launch_fwd<4, 1, 2, 4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-        if (L->groups == 1) return launch_fwd<16, 1, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-        if (L->groups == 2) return launch_fwd<16, 2, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-        return launch_fwd<16, 4, 1, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    if (RT_C3D_EXP == 3) return fwd_tile(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);  // A/B builds
+    int rc = RT_ELIMIT;
+    if (L->cin == 4) {
+        rc = launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    } else if (L->groups == 1) {
+        rc = launch_fwd_ring<16, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    } else {
+        // grouped stages: the z-shift ring kernel (RT_C3D_ZS=0: the dense ring kernel, A/B runs)
+        static const bool zs = [] {
+            const char* e = std::getenv("RT_C3D_ZS");
+            return !(e && e[0] == '0');
+        }();
+        if (zs && (int64_t)batch * L->groups <= 65535)
+            rc = L->groups == 2 ? launch_ring_zs<2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st)
+                                : launch_ring_zs<4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+        if (rc == RT_ELIMIT)
+            rc = L->groups == 2 ? launch_fwd_ring<16, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st)
+                                : launch_fwd_ring<16, 4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     }
-    if (L->cin == 4) return launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-    if (L->groups == 1) return launch_fwd_ring<16, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-    // grouped stages: the z-shift ring kernel (RT_C3D_ZS=0: the dense ring kernel, A/B runs)
-    static const bool zs = [] {
-        const char* e = std::getenv("RT_C3D_ZS");
-        return !(e && e[0] == '0');
-    }();
-    if (zs && (int64_t)batch * L->groups <= 65535) {
-        const int rc = L->groups == 2 ? launch_ring_zs<2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st)
-                                      : launch_ring_zs<4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-        if (rc != RT_ELIMIT) return rc;
-    }
-    if (L->groups == 2) return launch_fwd_ring<16, 2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-    return launch_fwd_ring<16, 4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    if (rc != RT_ELIMIT) return rc;
+    // planes too wide for any plane ring: the one-region-per-block tile kernel
+    // (its region is 2 pooled z rows x 4 or 2 pooled y rows, so it fits where
+    // the 6-plane ring does not)
+    return fwd_tile(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
 }
 
 extern "C" int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* L, int32_t batch) {
     if (bad_layer(L) || batch < 1) return 0;
-    if (RT_C3D_EXP != 3) {  // ring: at most kWgradRingBlocks partial rows (one per block)
-        if (L->cin == 4) return (int64_t)kWgradRingBlocks * CO * wg_nct<4>() * 16;
-        return (int64_t)kWgradRingBlocks * CO * wg_nct<16>() * 16;
-    }
-    if (L->cin == 4) return (int64_t)wgrad_blocks<4, 2, 4>(L, batch) * CO * ncol_tiles<4>() * 16;
-    return (int64_t)wgrad_blocks<16, 1, 2>(L, batch) * CO * ncol_tiles<16>() * 16;
+    // ring: at most kWgradRingBlocks partial rows (one per block); the tile
+    // kernel (fallback for planes too wide for the ring) may need more
+    const int64_t ring = (int64_t)kWgradRingBlocks * CO * (L->cin == 4 ? wg_nct<4>() : wg_nct<16>()) * 16;
+    return std::max(ring, wgrad_tile_ws(L, batch));
 }
 
 extern "C" int rt_conv_relu_pool_wgrad(const rt_conv_layer* L, int32_t batch, const float* x_d, const int64_t* rows_d,
@@ -2355,11 +2392,12 @@ extern "C" int rt_conv_relu_pool_wgrad(const rt_conv_layer* L, int32_t batch, co
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_wgrad: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (RT_C3D_EXP != 3) {
-        if (L->cin == 4) return launch_wgrad_ring<4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
-        return launch_wgrad_ring<16>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+        const int rc = L->cin == 4
+                           ? launch_wgrad_ring<4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st)
+                           : launch_wgrad_ring<16>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+        if (rc != RT_ELIMIT) return rc;
     }
-    if (L->cin == 4) return launch_wgrad<4, 2, 4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
-    return launch_wgrad<16, 1, 2>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+    return wgrad_tile(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
 }
 
 extern "C" int rt_conv_relu_pool_dgrad(const rt_conv_layer* L, int32_t batch, const float* w_d, const float* dy_d,

@@ -1867,9 +1867,19 @@ int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h) {
 
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
+static int check_config_size(const rt_env_config* cfg) {
+    if (cfg->struct_size != sizeof(rt_env_config))
+        return fail(RT_EINVAL, "rt_env_config.struct_size is " + std::to_string(cfg->struct_size) + ", expected " +
+                                   std::to_string(sizeof(rt_env_config)) +
+                                   " (set it to sizeof(rt_env_config); the binding's declaration may be stale)");
+    return RT_OK;
+}
+
 int rt_env_config_default(rt_env_config* cfg) {
     if (!cfg) return fail(RT_EINVAL, "cfg is NULL");
+    if (int rc = check_config_size(cfg)) return rc;
     std::memset(cfg, 0, sizeof(*cfg));
+    cfg->struct_size = sizeof(rt_env_config);
     cfg->grid[0] = 67;
     cfg->grid[1] = 43;
     cfg->grid[2] = 70;
@@ -1891,6 +1901,7 @@ int rt_env_config_default(rt_env_config* cfg) {
 int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     if (!cfg || !out) return fail(RT_EINVAL, "NULL argument");
     *out = nullptr;
+    if (int rc = check_config_size(cfg)) return rc;
     if (cfg->num_envs < 1) return fail(RT_EINVAL, "num_envs must be >= 1");
     if (!cfg->lungs_h || !cfg->tumour_voxels_h || !cfg->tumour_offsets_h || cfg->n_tumours < 1)
         return fail(RT_EINVAL, "lungs / tumour library missing");
@@ -2096,7 +2107,10 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         (rc = dev_alloc(env, &env->part_cnt, (size_t)N * env->slices)) ||
         (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices)) ||
         (rc = dev_alloc(env, &st.lung_cnt, N)) || (rc = dev_alloc(env, &st.lung_sum, N)) ||
-        (env->rollout_wpb && env->rollout_cap < max_n &&
+        // the persistent rollout's plan slots for tumours above its LDS share:
+        // incremental handles (their default rollout); dense handles allocate
+        // them in rt_env_set_rollout_groups(env, 0), the only way they reach it
+        (env->incremental && env->rollout_wpb && env->rollout_cap < max_n &&
          (rc = dev_alloc(env, &env->gscratch, (size_t)N * 2 * max_n)))) {
         free_env(env);
         return rc;
@@ -2210,10 +2224,12 @@ FinishParams finish_params(const rt_env* env, float* obs, float* reward, uint8_t
 // handle, and a later handle (bigger tumour library, vision hash) may need more
 // than 64 KiB.  The limit does not reserve LDS; occupancy follows each launch's
 // actual request.
-void allow_lds(const void* kernel, bool& raised) {
-    if (raised) return;
-    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+int allow_lds(const void* kernel, bool& raised) {
+    if (raised) return RT_OK;
+    const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return fail(RT_EDEVICE, std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(e));
     raised = true;
+    return RT_OK;
 }
 
 // k_dense / k_dense_vis (skipped in incremental mode) then k_finish
@@ -2259,7 +2275,7 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
     fp.e_begin = e0;
     fp.N = e1;
     static bool big_lds = false;
-    allow_lds(reinterpret_cast<const void*>(&k_finish), big_lds);
+    if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_finish), big_lds)) return rc_lds;
     hipLaunchKernelGGL(k_finish, dim3((n + fp.wpb - 1) / fp.wpb), dim3(64 * fp.wpb), env->finish_smem, stream, fp);
     RT_LAUNCH_CHECK("k_finish");
     if (ev) (void)hipEventRecord(ev[3], stream);
@@ -2327,7 +2343,7 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* ps, float* obs_d, floa
     const dim3 grid((env->N + Q.wpb - 1) / Q.wpb), block(64 * Q.wpb);
     if (env->incremental) {
         static bool big = false;
-        allow_lds(reinterpret_cast<const void*>(&k_step_policy<true>), big);
+        if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_step_policy<true>), big)) return rc_lds;
         hipLaunchKernelGGL(k_step_policy<true>, grid, block, env->fused_smem, s, bp, fp, Q);
         RT_LAUNCH_CHECK("k_step_policy");
         if (ev)
@@ -2335,7 +2351,7 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* ps, float* obs_d, floa
         return RT_OK;
     }
     static bool big = false;
-    allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), big);
+    if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), big)) return rc_lds;
     hipLaunchKernelGGL(k_step_policy<false>, grid, block, env->fused_smem, s, bp, fp, Q);
     RT_LAUNCH_CHECK("k_step_policy");
     return launch_dense_finish(env, obs_d, reward_d, terminated_d, info_d, s, ev);
@@ -2376,7 +2392,7 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
         }
     }
     static bool big = false;
-    allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), big);
+    if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_step_policy<false>), big)) return rc_lds;
     PolicyStepParams Q{};
     for (int i = 0; i < rtpol::kTensors; ++i) {
         if (!ps->params[i]) return fail(RT_EINVAL, "rt_env_rollout_policy: NULL parameter");
@@ -2432,6 +2448,14 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups) {
     if (!env || groups < 0 || groups > kMaxRolloutGroups)
         return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups must be 0 (persistent) or 1..4");
+    if (groups == 0 && env->visionless && env->rollout_wpb && env->rollout_cap < env->max_tvox && !env->gscratch) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        RT_HIP(hipSetDevice(env->device));
+        const int rc = dev_alloc(env, &env->gscratch, (size_t)env->N * 2 * env->max_tvox);
+        (void)hipSetDevice(cur);
+        if (rc) return rc;
+    }
     env->rollout_groups = groups;
     return RT_OK;
 }
@@ -2470,17 +2494,19 @@ static int rollout_persistent(rt_env* env, const rt_policy_rollout* r, float* ob
     FinishParams fp = finish_params(env, obs_d, nullptr, terminated_d, nullptr);
     fp.max_tvox = env->rollout_cap;
     fp.wave_lds = env->rollout_wave_lds;
+    if (env->rollout_cap < env->max_tvox && !env->gscratch)
+        return fail(RT_EINVAL, "rt_env_rollout_policy: persistent rollout scratch missing (rollout groups 0 not set)");
     fp.gscratch = env->gscratch;
     fp.gscratch_stride = 2 * (int64_t)env->max_tvox;
     const dim3 grid((env->N + Q.wpb - 1) / Q.wpb), block(64 * Q.wpb);
     RolloutArgs A{bp, fp, R};
     if (env->incremental) {
         static bool big = false;
-        allow_lds(reinterpret_cast<const void*>(&k_rollout_policy<false>), big);
+        if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_rollout_policy<false>), big)) return rc_lds;
         hipLaunchKernelGGL(k_rollout_policy<false>, grid, block, env->rollout_smem, s, A);
     } else {
         static bool big = false;
-        allow_lds(reinterpret_cast<const void*>(&k_rollout_policy<true>), big);
+        if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_rollout_policy<true>), big)) return rc_lds;
         hipLaunchKernelGGL(k_rollout_policy<true>, grid, block, env->rollout_smem, s, A);
     }
     RT_LAUNCH_CHECK("k_rollout_policy");
@@ -2616,6 +2642,7 @@ int rt_debug_pose(const int32_t grid[3], int32_t m, const double* pos_d, const d
     if (m < 0 || !pos_d || !dir_d || !action_d || !out_d) return fail(RT_EINVAL, "bad argument");
     if (m == 0) return RT_OK;
     rt_env_config cfg;
+    cfg.struct_size = sizeof(cfg);
     rt_env_config_default(&cfg);
     Consts C = make_consts(cfg);
     hipLaunchKernelGGL(k_debug_pose, dim3((m + 63) / 64), dim3(64), 0, as_stream(stream), G, C, m, pos_d,

@@ -347,16 +347,25 @@ class PPOTrainer:
                 t.div_(self.world)
         return t
 
-    def _norm_adv(self, adv: torch.Tensor) -> torch.Tensor:
+    def _adv_stats(self, adv: torch.Tensor):
+        """(mean, unbiased std) of a minibatch's advantages (train.py:215-218).
+        World 1: torch's own f32 statistics, as the reference.  Collective: the
+        statistics of the UNION of the ranks' minibatches (the single-process
+        minibatch the DP update stands for), from one f64 all-reduce of
+        [sum, sum of squares, count]."""
         if not self.collective:
-            return (adv - adv.mean()) / (adv.std() + 1e-8)
+            return adv.mean(), adv.std()
         a = adv.double()
         s = torch.stack([a.sum(), (a * a).sum(), torch.tensor(float(a.numel()), dtype=torch.float64,
                                                                device=a.device)])
         self._allreduce_(s, average=False)
         mean = s[0] / s[2]
         var = (s[1] - s[2] * mean * mean) / (s[2] - 1.0)
-        return (adv - mean.float()) / (var.clamp_min(0).sqrt().float() + 1e-8)
+        return mean.float(), var.clamp_min(0).sqrt().float()
+
+    def _norm_adv(self, adv: torch.Tensor) -> torch.Tensor:
+        mean, std = self._adv_stats(adv)
+        return (adv - mean) / (std + 1e-8)
 
     def _minibatch_loss_backward(self, mb, adv_mean=None, adv_std=None):
         """train.py:200-246 for one minibatch: losses, then backward into the
@@ -364,12 +373,13 @@ class PPOTrainer:
         cfg.micro_batch set (vision: C3D activations of a whole minibatch do not
         fit), the minibatch is processed in slices whose gradients accumulate;
         each slice's loss is weighted by its share, so the gradient equals the
-        full-minibatch one (advantage statistics are those of the minibatch)."""
+        full-minibatch one.  The advantage statistics are taken once, before
+        the slices, over the whole minibatch -- over the union of the ranks'
+        minibatches when the update is collective (_adv_stats)."""
         micro = int(getattr(self.cfg, "micro_batch", 0) or 0)
         if micro and mb.numel() > micro:
             if self.cfg.norm_adv and adv_mean is None:
-                a = self._b_adv[mb]
-                adv_mean, adv_std = a.mean(), a.std()
+                adv_mean, adv_std = self._adv_stats(self._b_adv[mb])
             self.flat_grad.zero_()
             acc = None
             n = mb.numel()
@@ -528,6 +538,8 @@ class PPOTrainer:
         n_mb = 0
         for _ in range(int(self.cfg.update_epochs)):
             perm = torch.randperm(self.batch_size, device=dev, generator=self.gen)
+            if self.record_perms is not None:  # test hook: the epochs' minibatch rows
+                self.record_perms.append(perm.clone())
             for start in range(0, self.batch_size, self.minibatch_size):
                 mb = perm[start:start + self.minibatch_size]
                 st = self._minibatch_loss_backward(mb)
@@ -557,7 +569,9 @@ class PPOTrainer:
                          1 - (y_true - y_pred).var(unbiased=False) / var_y)
         parts = [vals, ev.double().reshape(1)]
         if getattr(self, "_last_stats", None) is not None:
-            parts.append(self._last_stats.double())
+            # losses / KL / clipfrac of this rank's minibatches: averaged over
+            # the ranks, so the logged scalars are global like the episode stats
+            parts.append(self._allreduce_(self._last_stats.double().clone()))
         parts.append(per_step.reshape(-1))
         host = torch.cat(parts).cpu().numpy()
         steps = host[-per_step.numel():].reshape(per_step.shape)
@@ -648,6 +662,10 @@ class PPOTrainer:
             self._exp_avg_sq.copy_(a["exp_avg_sq"])
             self._adam_step = int(a["step"])
         rng = d.get("rng")
+        if rng is None and ("gen" in d or "host_gen" in d) and self.world == 1 and int(d.get("world", 1)) == 1:
+            # checkpoints written before the per-rank list kept the (single)
+            # rank's states at the top level: continue them
+            rng = [{k: d[k] for k in ("gen", "host_gen") if k in d}]
         if rng is not None and len(rng) == self.world:
             mine = rng[self.rank]
             if self.gen is not None and "gen" in mine:
@@ -655,6 +673,10 @@ class PPOTrainer:
             if self.fused_update and "host_gen" in mine:
                 self._host_gen.set_state(mine["host_gen"].cpu())
         else:
+            import warnings
+
+            warnings.warn(f"checkpoint holds no sampling/shuffle generator state for rank {self.rank} of "
+                          f"world {self.world}: streams re-derived from (seed, rank, iteration)")
             self._reseed_rngs(self.iteration)
 
     def train_iteration(self, iteration: int, num_iterations: int) -> IterStats:

@@ -7,25 +7,38 @@ from ppo_radiotherapy_amd import _lib, spaces
 
 
 class FakeVecEnv:
-    def __init__(self, num_envs, seed=0, device="cpu"):
+    """obs_shape (9,): a smooth visionless toy; a 4-D obs_shape: vision-shaped
+    observations (fresh uniform volumes every step) for the C3D agent.
+    `reward_scale` lets data-parallel tests give ranks different advantage
+    distributions (rank-local statistics then differ from the union's)."""
+
+    def __init__(self, num_envs, seed=0, device="cpu", obs_shape=(9,), reward_scale=1.0):
         self.num_envs = num_envs
         self.device = torch.device(device)
-        self.single_observation_space = spaces.Box(0.0, 1.0, (9,), np.float32)
+        self.obs_shape = tuple(obs_shape)
+        self.vision = len(self.obs_shape) == 4
+        self.reward_scale = float(reward_scale)
+        self.single_observation_space = spaces.Box(0.0, 1.0, self.obs_shape, np.float32)
         self.single_action_space = spaces.Box(-1.0, 1.0, (6,), np.float32)
         self.g = torch.Generator().manual_seed(seed)
-        self.obs = torch.zeros(num_envs, 9)
+        self.obs = torch.zeros(num_envs, *self.obs_shape)
         self.t = torch.zeros(num_envs, dtype=torch.int64)
         self.info = torch.zeros(num_envs, _lib.INFO_W)
 
     def reset(self, seed=None, options=None):
-        self.obs = torch.rand(self.num_envs, 9, generator=self.g) * 2 - 1
+        self.obs = torch.rand(self.num_envs, *self.obs_shape, generator=self.g) * 2 - 1
         self.t.zero_()
         return self.obs, {}
 
     def step(self, actions, info_out=None):
         a = actions.clamp(-1, 1)
-        self.obs = (self.obs * 0.9 + 0.1 * torch.cat([a, a[:, :3]], 1)).contiguous()
-        reward = -(self.obs[:, :3] ** 2).sum(1)
+        if self.vision:
+            self.obs = torch.rand(self.num_envs, *self.obs_shape, generator=self.g)
+            reward = -(a[:, :3] ** 2).sum(1) + self.obs[:, 0].mean((1, 2, 3))
+        else:
+            self.obs = (self.obs * 0.9 + 0.1 * torch.cat([a, a[:, :3]], 1)).contiguous()
+            reward = -(self.obs[:, :3] ** 2).sum(1)
+        reward = reward * self.reward_scale
         self.t += 1
         term = self.t >= 7
         info = self.info if info_out is None else info_out

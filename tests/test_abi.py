@@ -71,7 +71,41 @@ def test_config_defaults_are_reference_constants():
     assert c.tumour_dose_threshold == np.float32(0.9) and c.min_angle_z == math.pi / 4
     assert c.movement_speed == 0.2 and c.rotation_speed == 0.5
     assert (c.lung_dose_reward, c.tumour_dose_reward, c.distance_reward) == (-1.0, 10.0, -1.0)
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == 2
+    assert c.struct_size == ctypes.sizeof(_lib.RtEnvConfig)
+
+
+def test_config_size_handshake_rejects_stale_declarations():
+    """rt_env_config.struct_size: a declaration without it (ABI 1: the first
+    member is grid[0]) or without a trailing member (the round-2 INTEGRATION.md
+    snippet lacked step_mode) is refused with RT_EINVAL before anything is
+    written -- the bytes past the caller's struct stay untouched."""
+    L = _lib.load()
+    full = ctypes.sizeof(_lib.RtEnvConfig)
+    for size in (0, full - 8, full + 8):
+        buf = (ctypes.c_uint8 * (full + 32))()
+        ctypes.memset(buf, 0xCD, len(buf))
+        c = _lib.RtEnvConfig.from_buffer(buf)
+        c.struct_size = size
+        assert L.rt_env_config_default(c) == -1, size
+        assert b"struct_size" in L.rt_last_error()
+        assert bytes(buf)[4:] == b"\xcd" * (len(buf) - 4)
+        h = ctypes.c_void_p()
+        assert L.rt_env_create(c, 0, h) == -1 and h.value is None
+
+
+def test_integration_binding_struct_is_the_library_struct():
+    """INTEGRATION_binding.py declares rt_env_config by hand (a foreign
+    binding): same fields, size and offsets as the production mirror, which
+    test_struct_layout_matches_header pins to the header."""
+    sys.path.insert(0, REPO)
+    import INTEGRATION_binding as B
+
+    assert [f[0] for f in B.RtEnvConfig._fields_] == [f[0] for f in _lib.RtEnvConfig._fields_]
+    assert ctypes.sizeof(B.RtEnvConfig) == ctypes.sizeof(_lib.RtEnvConfig)
+    for f, _ in B.RtEnvConfig._fields_:
+        assert getattr(B.RtEnvConfig, f).offset == getattr(_lib.RtEnvConfig, f).offset
+    assert B.RTENV_ABI_VERSION == _lib.load().rt_abi_version()
 
 
 def test_error_paths_do_not_abort():

@@ -17,6 +17,11 @@ STAGES = [  # cin, groups, dims, pool_pad, batch
     (16, 1, (9, 12, 11), (1, 0, 1), 3),
     (16, 2, (11, 21, 63), (0, 0, 0), 2),  # data-gradient ring: 2-row y band (63-wide planes)
     (16, 1, (12, 13, 10), (0, 0, 0), 3),
+    # planes wider than the 80 KiB conv1 ring: the 160 KiB ring, one-row bands
+    (4, 1, (6, 10, 160), (0, 0, 0), 2),
+    (4, 1, (5, 7, 258), (1, 1, 0), 1),
+    (16, 2, (6, 9, 79), (0, 0, 0), 2),
+    (16, 1, (6, 7, 101), (0, 0, 0), 2),
 ]
 
 
@@ -177,17 +182,19 @@ def test_conv_relu_pool_backward(cin, groups, dims, pad, B):
         assert float(d.norm() / xr.grad.norm()) < 1e-5
 
 
-def test_features_extractor_matches_torch_modules():
+@pytest.mark.parametrize("shape,B", [((4, 34, 27, 40), 6), ((4, 22, 23, 160), 2)])
+def test_features_extractor_matches_torch_modules(shape, B):
     """FeaturesExtractor3D on the GPU (fused kernels) vs its own torch modules
-    on the CPU in float64: features and every parameter gradient."""
+    on the CPU in float64: features and every parameter gradient (the second
+    shape: a grid 160 voxels wide, beyond the conv1 ring's 80 KiB band)."""
     from ppo_radiotherapy_amd.networks import FeaturesExtractor3D
 
     torch.manual_seed(0)
-    fe = FeaturesExtractor3D((4, 34, 27, 40), 64)
-    ref = FeaturesExtractor3D((4, 34, 27, 40), 64).double()
+    fe = FeaturesExtractor3D(shape, 64)
+    ref = FeaturesExtractor3D(shape, 64).double()
     ref.load_state_dict({k: v.double() for k, v in fe.state_dict().items()})
     fe = fe.cuda()
-    x = torch.rand((6, 4, 34, 27, 40))
+    x = torch.rand((B, *shape))
     f = fe(x.cuda())
     fr = ref(x.double())
     torch.testing.assert_close(f.cpu().double(), fr, rtol=1e-4, atol=1e-5)

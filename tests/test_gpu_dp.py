@@ -172,3 +172,108 @@ def test_fused_update_data_parallel_two_ranks():
     assert moved > 1e-3, moved
     assert err <= 2e-3 * moved, (err, moved)
     assert np.abs(got - want).max() <= 2e-5, np.abs(got - want).max()
+
+
+# --- vision agent (configs[4]'s split): C3D kernels + micro-batched autograd update
+VIS_GRID, VIS_ENVS, VIS_T, VIS_MB, VIS_MICRO = (32, 32, 32), 8, 8, 2, 12
+VIS_HP = dict(clip_coef=0.1, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5, lr=3e-4)
+
+
+def _vision_worker(rank, world, port, q):
+    import _rtpkg  # noqa: F401
+    import torch.distributed as dist
+    from types import SimpleNamespace
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import dp_ref
+    from ppo_radiotherapy_amd import assets
+    from ppo_radiotherapy_amd.networks import PPO_3DCNN
+    from ppo_radiotherapy_amd.ppo import PPOTrainer, broadcast_parameters
+    from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        lib = assets.synthetic_library(VIS_GRID, 50, 0)
+        env = RadiotherapyVecEnv(VIS_ENVS, visionless=False, library=lib, seed=21 + rank,
+                                 env_id_base=VIS_ENVS * rank)
+        torch.manual_seed(200 + rank)
+        agent = PPO_3DCNN((4, *VIS_GRID), (6,), 64).cuda()
+        broadcast_parameters(agent)
+        cfg = SimpleNamespace(num_steps=VIS_T, num_minibatches=VIS_MB, update_epochs=2, learning_rate=VIS_HP["lr"],
+                              anneal_lr=False, gamma=0.99, gae_lambda=0.95, norm_adv=True,
+                              clip_coef=VIS_HP["clip_coef"], clip_vloss=True, ent_coef=VIS_HP["ent_coef"],
+                              vf_coef=VIS_HP["vf_coef"], max_grad_norm=VIS_HP["max_grad_norm"], seed=rank,
+                              micro_batch=VIS_MICRO)
+        tr = PPOTrainer(cfg, env, agent, "cuda", rank=rank, world=world,
+                        generator=torch.Generator(device="cuda").manual_seed(rank))
+        assert not tr.fused_update and tr.compact_obs and tr.collective
+        tr.reset()
+        tr.train_iteration(1, 2)  # Adam state off zero
+        tr.rollout()
+        tr.compute_gae()
+        tr._bind_batch()
+        sd0 = {k: v.detach().cpu().numpy().copy() for k, v in agent.state_dict().items()}
+        opt0 = dp_ref.optimizer_state_numpy(tr.optimizer)
+        batch = dp_ref.trainer_batch(tr)
+        tr.record_perms = []
+        tr.update()
+        torch.cuda.synchronize()
+        flat = torch.cat([p.detach().reshape(-1) for p in tr.params]).cpu().numpy()
+        q.put((rank, flat, sd0, opt0, batch, [p.cpu().numpy() for p in tr.record_perms]))
+        env.close()
+        dist.destroy_process_group()
+    except Exception as exc:  # surfaced by the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc() + repr(exc), None, None, None, None))
+
+
+def test_vision_micro_batched_update_data_parallel_two_ranks():
+    """PPO_3DCNN on the HIP env and the C3D kernels, two gloo ranks on the one
+    GPU, micro_batch < minibatch (train.py:215-218 across ranks): replicas
+    identical AND equal to a single-process f64 update of the union batch
+    (tests/dp_ref.py); rank-local advantage statistics would fail it."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import dp_ref
+    from ppo_radiotherapy_amd.networks import PPO_3DCNN
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_vision_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    deadline = time.time() + 300
+    while len(res) < world and time.time() < deadline:
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert len(res) == world, res
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert not isinstance(r[1], str), r[1]
+    np.testing.assert_array_equal(res[0][1], res[1][1])  # replicas identical
+    args = (res[0][2], res[0][3], [r[4] for r in res], [r[5] for r in res], VIS_MB, VIS_HP)
+    want = dp_ref.union_update_f64(PPO_3DCNN((4, *VIS_GRID), (6,), 64), *args)
+    local = dp_ref.union_update_f64(PPO_3DCNN((4, *VIS_GRID), (6,), 64), *args, local_norm=True)
+    p0 = np.concatenate([v.reshape(-1) for v in res[0][2].values()]).astype(np.float64)
+    got = res[0][1].astype(np.float64)
+    moved = np.linalg.norm(want - p0)
+    err = np.linalg.norm(got - want)
+    assert moved > 1e-3, moved
+    assert err <= 5e-3 * moved, (err, moved)
+    assert np.linalg.norm(local - want) > 10 * err, (np.linalg.norm(local - want), err)

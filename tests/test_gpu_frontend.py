@@ -203,3 +203,44 @@ def test_export_trajectory_format(tmp_path, golden):
     nz = np.flatnonzero(d["dose"].ravel())
     np.testing.assert_array_equal(nz, z["dose_idx"][z["dose_off"][0]:z["dose_off"][1]])
     env.close()
+
+
+def test_train_cli_vision_reference_grid(tmp_path, capsys):
+    """The reference's vision entry point, `python train.py --config-file
+    configs/vision.yaml` (train.py:102-106: PPO_3DCNN + agent.summary(),
+    configs/vision.yaml.template keys), run through the CLI at the reference
+    grid 67x43x70 -- odd dims, so the first pool pads (networks.py:18-20) --
+    on the C3D kernels, with the micro-batched update."""
+    import yaml
+
+    import train as train_mod
+
+    cfg = yaml.safe_load(open(os.path.join(REPO, "configs", "vision.yaml")))
+    cfg.update(dict(exp_name="vis", num_envs=4, num_steps=8, total_timesteps=64, num_minibatches=2,
+                    update_epochs=2, num_saves=1, micro_batch=6))
+    p = tmp_path / "vision.yaml"
+    yaml.safe_dump(cfg, open(p, "w"))
+    out = tmp_path / "out"
+    agent = train_mod.main(["--config-file", str(p), "--output-dir", str(out)])
+    printed = capsys.readouterr().out
+    assert "Observation shape:  (4, 67, 43, 70)" in printed  # agent.summary()
+    from ppo_radiotherapy_amd.networks import PPO_3DCNN
+
+    assert isinstance(agent, PPO_3DCNN)
+    assert agent.features_extractor.n_flatten == 2016  # the reference's dry-run flatten at 67x43x70
+    runs = os.listdir(out / "models")
+    assert len(runs) == 1
+    assert sorted(os.listdir(out / "models" / runs[0])) == ["vis_2.model"]
+    sd = torch.load(out / "models" / runs[0] / "vis_2.model", weights_only=True)
+    ref = PPO_3DCNN((4, 67, 43, 70), (6,), 64)
+    assert set(sd) == set(ref.state_dict())  # the reference's PPO_3DCNN keys
+    for k, v in ref.state_dict().items():
+        assert tuple(sd[k].shape) == tuple(v.shape), k
+    tb = out / "tensorboard" / runs[0]
+    files = os.listdir(tb)
+    if "scalars.jsonl" in files:
+        tags = {json.loads(x).get("tag") for x in open(tb / "scalars.jsonl")}
+        for t in ["charts/learning_rate", "losses/value_loss", "losses/policy_loss", "losses/entropy",
+                  "losses/approx_kl", "losses/clipfrac", "losses/explained_variance"]:
+            assert t in tags, t
+    assert all(torch.isfinite(p).all() for p in agent.parameters())

@@ -10,7 +10,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-sys.path.insert(0, os.path.dirname(__file__))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import _rtpkg  # noqa: E402,F401  (spawned workers do not run conftest)
 from fake_env import FakeVecEnv, torch_gae  # noqa: E402
@@ -242,3 +242,72 @@ def test_env_seed_folds_resume_iteration():
     assert env_seed(1, 0, 1) == 1 and env_seed(1, 3, 1) == 4
     assert env_seed(1, 0, 2) != env_seed(1, 0, 1) and env_seed(1, 0, 2) != env_seed(1, 0, 3)
     assert 0 <= env_seed(2 ** 64 - 1, 7, 5) < 2 ** 64
+
+
+# --- data-parallel update of the vision (C3D) agent with micro-batching -----
+# (the micro-batched path normalised advantages with rank-local
+# statistics; train.py:215-218 normalises over the whole minibatch, which in
+# the DP update is the union of the ranks' minibatches)
+VIS_SHAPE = (4, 22, 22, 22)  # 22 -> conv 20 -> pool 10 -> 8 -> 4 -> 2 -> 1
+VIS_HP = dict(clip_coef=0.1, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5, lr=3e-4)
+
+
+def _vision_dp_worker(rank, world, port, q):
+    import dp_ref
+    from ppo_radiotherapy_amd.networks import PPO_3DCNN
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(100 + rank)
+    agent = PPO_3DCNN(VIS_SHAPE, (6,), 64)
+    broadcast_parameters(agent)
+    env = FakeVecEnv(4, seed=rank, obs_shape=VIS_SHAPE, reward_scale=1.0 + 3.0 * rank)
+    cfg = _cfg(num_steps=8, num_minibatches=2, micro_batch=6, learning_rate=VIS_HP["lr"])  # 16-row mbs: 6+6+4
+    tr = PPOTrainer(cfg, env, agent, "cpu", rank, world, torch.Generator().manual_seed(rank), gae_fn=torch_gae)
+    tr.reset()
+    tr.rollout()
+    tr.compute_gae()
+    tr.update()  # moves the Adam state off zero
+    tr.rollout()
+    tr.compute_gae()
+    tr._bind_batch()
+    sd0 = {k: v.detach().numpy().copy() for k, v in agent.state_dict().items()}
+    opt0 = dp_ref.optimizer_state_numpy(tr.optimizer)
+    batch = dp_ref.trainer_batch(tr)
+    tr.record_perms = []
+    tr.update()
+    flat = torch.cat([p.detach().reshape(-1) for p in tr.params]).numpy().copy()
+    q.put((rank, flat, sd0, opt0, batch, [p.numpy().copy() for p in tr.record_perms]))
+    dist.destroy_process_group()
+
+
+def test_vision_micro_batched_update_data_parallel_gloo():
+    """Two gloo ranks, PPO_3DCNN, micro_batch < minibatch: the replicas equal a
+    single-process float64 update on the union batch (tests/dp_ref.py), and
+    that comparison is sensitive to rank-local advantage statistics."""
+    import dp_ref
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_vision_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0][1], res[1][1])  # replicas identical
+    from ppo_radiotherapy_amd.networks import PPO_3DCNN
+
+    args = (res[0][2], res[0][3], [r[4] for r in res], [r[5] for r in res], 2, VIS_HP)
+    want = dp_ref.union_update_f64(PPO_3DCNN(VIS_SHAPE, (6,), 64), *args)
+    local = dp_ref.union_update_f64(PPO_3DCNN(VIS_SHAPE, (6,), 64), *args, local_norm=True)
+    p0 = np.concatenate([v.reshape(-1) for v in res[0][2].values()]).astype(np.float64)
+    got = res[0][1].astype(np.float64)
+    moved = np.linalg.norm(want - p0)
+    err = np.linalg.norm(got - want)
+    assert moved > 1e-3, moved
+    assert err <= 2e-3 * moved, (err, moved)
+    assert np.linalg.norm(local - want) > 20 * err, (np.linalg.norm(local - want), err)
