@@ -41,8 +41,10 @@ Also reported:
                          grid and tumours, seed 1, default_rng(0) actions;
                          bounded sample); beside it the same on the box's core
                          share and the scalar C port
-  roofline.measured_copy_ceiling_GBps
-                         device copy bandwidth measured in the same run
+  roofline.measured_read_ceiling_GBps / measured_copy_ceiling_GBps
+                         HBM stream ceilings measured in the same run
+                         (rt_probe_stream: k_dense's non-temporal float4
+                         read sweep alone, and a float4 copy)
   c3d_mfma               configs[3]'s C3D feature extractor (the MFMA path,
                          north_star): its stage kernels on 512 vision
                          observations at 64^3, inference forward and the
@@ -183,35 +185,48 @@ def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int =
     with e % 100 == k at pre-roll step k (masked rt_env_reset), so every step
     of the window carries ~1 % of the envs through the t = 100 truncation
     autoreset (a RESET zeroes the env's whole dose row) -- the steady state of
-    a long run, which a window started right after reset() never reaches."""
+    a long run, which a window started right after reset() never reaches.
+    Nothing but the rollout calls runs inside the timed windows; the autoreset
+    count and the kernel times come from a fourth, instrumented window.  A
+    one-block rt_probe_stream launch before each window marks it in a
+    rocprofv3 kernel trace (tools/steady_trace.py)."""
     import torch
+
+    from ppo_radiotherapy_amd import _lib
+
+    L = _lib.load()
+    mark_buf = torch.zeros(4, device=dev)
+
+    def mark():
+        _lib.check(L.rt_probe_stream(mark_buf.data_ptr(), mark_buf.data_ptr(), 4, 0, 1, _lib.stream_handle()),
+                   "marker")
 
     N, T = env.num_envs, tr.T
     e_idx = torch.arange(N, device=dev)
     for k in range(100):
         env.reset(options={"mask": (e_idx % 100) == k})
         tr.rollout_steps(k % T, 1)
-    resets = torch.zeros((), dtype=torch.int64, device=dev)
     K = calls * T
-    # three back-to-back windows (the phases stay staggered): the median window
-    # is reported, a single window once read 16 % low on one of four runs
+    # three back-to-back windows (the phases stay staggered); the median is reported
     dts = []
     for _ in range(3):
-        resets.zero_()
+        mark()
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
         for _ in range(calls):
             tr.rollout_steps(0, T)
-            resets += (tr.infos[..., 16] == 0).sum()  # autoresets in these T steps (one tiny reduction per call)
         torch.cuda.synchronize()
         barrier()
         dts.append(max_over_ranks(time.perf_counter() - t0))
+    mark()
     dt = sorted(dts)[1]
-    # kernel times: a second window of the same length (the phases stay staggered), with HIP events
+    # kernel times and the autoreset count: a fourth window of the same length, with HIP events
+    resets = torch.zeros((), dtype=torch.int64, device=dev)
     env.kernel_timing(2 * K)
     for _ in range(calls):
         tr.rollout_steps(0, T)
+        resets += (tr.infos[..., 16] == 0).sum()  # autoresets in these T steps
     torch.cuda.synchronize()
     kms, kcalls = env.kernel_timing_read()
     env.kernel_timing(0)
@@ -266,25 +281,38 @@ def random_rmw_ceiling(dev, lib_obj, floats: int, lanes: int = 1 << 18, lines_pe
     return reps * lanes * lines_per_lane / sec
 
 
-def copy_ceiling(dev, gib: float = 2.0, reps: int = 10) -> float:
-    """Measured device-to-device copy bandwidth (STREAM copy: read + write
-    bytes / time), the achievable HBM ceiling beside the 8 TB/s spec."""
+def stream_ceilings(dev, lib_obj, gib: float = 4.0, reps: int = 8) -> dict:
+    """Measured HBM stream ceilings in the same run (rt_probe_stream, HIP
+    events on the stream the probe runs on): a READ sweep of non-temporal 16-B
+    loads -- k_dense's access shape, the ceiling its `frac_of_measured_ceiling`
+    is against -- and a COPY (read + write bytes), over a buffer 16x the
+    256 MiB Infinity Cache; best of three grid sizes."""
     import torch
+
+    from ppo_radiotherapy_amd import _lib
 
     n = int(gib * (1 << 30)) // 4
     src = torch.ones(n, dtype=torch.float32, device=dev)
     dst = torch.empty_like(src)
-    dst.copy_(src)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        dst.copy_(src)
-    e1.record()
-    torch.cuda.synchronize()
-    bw = 2 * 4 * n * reps / (e0.elapsed_time(e1) * 1e-3)
+    st = _lib.stream_handle()
+    out = {}
+    for mode, name, traffic in ((0, "read", 4 * n), (1, "copy", 8 * n)):
+        best = 0.0
+        for blocks in (1024, 2048, 4096):
+            def once():
+                _lib.check(lib_obj.rt_probe_stream(src.data_ptr(), dst.data_ptr(), n, mode, blocks, st), "probe")
+            once()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                once()
+            e1.record()
+            torch.cuda.synchronize()
+            best = max(best, traffic * reps / (e0.elapsed_time(e1) * 1e-3))
+        out[name] = best
     del src, dst
     torch.cuda.empty_cache()
-    return bw
+    return out
 
 
 def load_pmc(grid, envs, kernel="k_dense"):
@@ -616,9 +644,14 @@ def main():
     roof["step_frac_of_hbm"] = a.envs * 4 * Vl / (dt / K) / HBM_PEAK if not a.vision else None
     roof["timed_pass_ms_per_step"] = 1000 * dt_timed / K  # the instrumented pass (kernel times above)
     if rank == 0 and not a.env_only:
-        cbw = copy_ceiling(dev)
-        roof["measured_copy_ceiling_GBps"] = cbw / 1e9
-        roof["frac_of_measured_ceiling"] = achieved / cbw
+        from ppo_radiotherapy_amd import _lib
+
+        cel = stream_ceilings(dev, _lib.load())
+        roof["measured_read_ceiling_GBps"] = cel["read"] / 1e9
+        roof["measured_copy_ceiling_GBps"] = cel["copy"] / 1e9
+        roof["measured_ceiling_probe"] = ("rt_probe_stream over 4 GiB: non-temporal 16-B loads, 8 in flight per lane "
+                                          "(read: reduced; copy: + plain 16-B stores, read+write bytes)")
+        roof["frac_of_measured_ceiling"] = achieved / cel["read"]
 
     # ---------------- the other step formulation, same workload (policy in the loop)
     other = None

@@ -203,6 +203,13 @@ int rt_env_beam_list(rt_env* env, int32_t cap, int32_t* idx_d, float* w_d, int32
 int rt_probe_random_rmw(float* buf_d, int64_t n_floats, int32_t lanes, int32_t lines_per_lane, uint64_t seed,
                         void* stream);
 
+/* Measurement hook (bench.py): the HBM stream ceilings k_dense is priced
+ * against -- `blocks` x 256 threads sweep src_d (n_floats, 16-B aligned) with
+ * non-temporal 16-B loads, 8 in flight per lane.  mode 0 (READ): reduced to
+ * 4 * blocks floats written to dst_d; mode 1 (COPY): stored to dst_d (plain
+ * 16-B stores).  Time it with events on `stream`. */
+int rt_probe_stream(const float* src_d, float* dst_d, int64_t n_floats, int32_t mode, int32_t blocks, void* stream);
+
 /* Host-side evaluation of the correctly rounded sin/cos the pose kernel uses
  * for scipy's from_rotvec half angle (no device needed; parity hook). */
 int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h);

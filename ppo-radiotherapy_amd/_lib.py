@@ -161,6 +161,7 @@ def load(build_if_missing: bool = True):
         "rt_debug_pose": ([ctypes.POINTER(i32), i32, vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_env_beam_list": ([vp, i32, vp, vp, vp, vp], ctypes.c_int),
         "rt_probe_random_rmw": ([vp, i64, i32, i32, ctypes.c_uint64, vp], ctypes.c_int),
+        "rt_probe_stream": ([vp, vp, i64, i32, i32, vp], ctypes.c_int),
         "rt_host_sincos": ([i32, vp, vp, vp], ctypes.c_int),
         "rt_host_tumour_sum": ([i64, i32, vp, vp, vp], ctypes.c_int),
         "rt_gae": ([i32, i32, vp, vp, vp, vp, vp, f64, f64, vp, vp, vp], ctypes.c_int),

@@ -1516,6 +1516,43 @@ __global__ __launch_bounds__(256) void k_probe_rmw(float* buf, int64_t n_lines, 
     }
 }
 
+// HBM stream ceilings (measurement hook, bench.py): a grid-stride sweep of
+// non-temporal 16-B loads -- k_dense's access shape -- either reduced to one
+// value per block (READ) or stored to a second buffer (COPY), 8 loads in
+// flight per lane.
+template <bool COPY>
+__global__ __launch_bounds__(256) void k_probe_stream(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                      int64_t n4, float* __restrict__ sink) {
+    typedef float nf4 __attribute__((ext_vector_type(4)));
+    constexpr int U = 8;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    float acc = 0.0f;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        nf4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(src + i + u * stride));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (COPY)
+                *reinterpret_cast<nf4*>(dst + i + u * stride) = v[u];
+            else
+                acc += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+        }
+    }
+    for (; i < n4; i += stride) {
+        const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(src + i));
+        if constexpr (COPY)
+            *reinterpret_cast<nf4*>(dst + i) = v;
+        else
+            acc += (v.x + v.y) + (v.z + v.w);
+    }
+    if constexpr (!COPY) {
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if ((threadIdx.x & 63) == 0) sink[blockIdx.x * 4 + (threadIdx.x >> 6)] = acc;
+    }
+}
+
 // beam_voxels (draw_line.py:4-102) as raw splats in march order; -1 for the
 // reference's ValueError (direction norm < eps).
 __device__ int emit_beam_list(const Geom& G, const double p[3], const double d[3], int cap, int32_t* idx_row,
@@ -2623,6 +2660,23 @@ int rt_probe_random_rmw(float* buf_d, int64_t n_floats, int32_t lanes, int32_t l
     hipLaunchKernelGGL(k_probe_rmw, dim3(lanes / 256), dim3(256), 0, as_stream(stream), buf_d, n_floats / 32,
                        lines_per_lane, seed);
     RT_LAUNCH_CHECK("k_probe_rmw");
+    return RT_OK;
+}
+
+int rt_probe_stream(const float* src_d, float* dst_d, int64_t n_floats, int32_t mode, int32_t blocks, void* stream) {
+    if (!src_d || !dst_d || n_floats < 4 || n_floats % 4 || (mode != 0 && mode != 1) || blocks < 1 ||
+        (reinterpret_cast<uintptr_t>(src_d) & 15) || (reinterpret_cast<uintptr_t>(dst_d) & 15))
+        return fail(RT_EINVAL, "rt_probe_stream: bad argument");
+    if (mode == 0 && n_floats < (int64_t)blocks * 4)
+        return fail(RT_EINVAL, "rt_probe_stream: READ needs dst_d of >= 4 * blocks floats");
+    const float4* s4 = reinterpret_cast<const float4*>(src_d);
+    if (mode == 1)
+        hipLaunchKernelGGL(k_probe_stream<true>, dim3(blocks), dim3(256), 0, as_stream(stream), s4,
+                           reinterpret_cast<float4*>(dst_d), n_floats / 4, nullptr);
+    else
+        hipLaunchKernelGGL(k_probe_stream<false>, dim3(blocks), dim3(256), 0, as_stream(stream), s4, nullptr,
+                           n_floats / 4, dst_d);
+    RT_LAUNCH_CHECK("k_probe_stream");
     return RT_OK;
 }
 
