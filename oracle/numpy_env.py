@@ -17,9 +17,11 @@ EPS = 1e-6
 MIN_ANGLE = np.pi / 4
 
 
-def _raster(shape, pos, direction):
-    """Dense f32 beam volume (draw_line.py:4-102, NEP 50 f32 arithmetic)."""
-    out = np.zeros(shape, dtype=np.float32)
+def _raster(base, pos, direction):
+    """Dense f32 beam volume shaped like `base` (draw_line.py:4-102, NEP 50 f32
+    arithmetic; the output is allocated like the reference's, zeros_like)."""
+    shape = base.shape
+    out = np.zeros_like(base, dtype=np.float32)
     p = np.array(pos, dtype=np.float32)
     d = np.array(direction, dtype=np.float32)
     n = np.linalg.norm(d)
@@ -90,7 +92,14 @@ def _rotate(direction, rotvec):
 
 
 class NumpyEnv:
-    """Visionless RadiotherapyEnv dynamics on dense numpy volumes."""
+    """Visionless RadiotherapyEnv dynamics on dense numpy volumes.
+
+    Organised like the reference (environment.py:77-191): one method per
+    reward with the same full-volume temporaries and the same lifetimes (a
+    temporary lives until its method returns), the dose replaced by a new
+    clipped array every step -- so the allocator sees the reference's
+    sequence of 806 KB allocations and frees, which decides how many of them
+    land on freshly faulted pages (tools/calibrate_cpu.py)."""
 
     def __init__(self, lungs: np.ndarray, tumour: np.ndarray):
         self.shape = tuple(lungs.shape)
@@ -99,14 +108,17 @@ class NumpyEnv:
         self.set_tumour(tumour)
 
     def set_tumour(self, tumour):
-        self.tumours = np.clip(np.zeros_like(self.lungs) + tumour.astype(np.float32), 0.0, 1.0)
+        """environment.py:86-97: zeros_like + the loaded volume, clipped."""
+        vol = np.zeros_like(self.lungs, dtype=np.float32)
+        vol += tumour.astype(np.float32)
+        self.tumours = np.clip(vol, 0.0, 1.0)
 
     def reset(self, tumour=None):
         if tumour is not None:
             self.set_tumour(tumour)
         self.pos = self.S / 2
         self.dir = np.array([0.0, 1.0, 0.0])
-        self.dose = np.zeros_like(self.lungs)
+        self.dose = np.zeros_like(self.lungs, dtype=np.float32)
         self.t = 0
         return self._obs()
 
@@ -114,10 +126,44 @@ class NumpyEnv:
         return np.stack(np.where(self.tumours == 1.0), axis=-1)
 
     def _obs(self):
-        c = np.mean(self._tumour_coords(), axis=0)
-        return np.concatenate([self.pos / self.S * 2 - 1, self.dir, c / self.S * 2 - 1])
+        centre = np.mean(self._tumour_coords(), axis=0)
+        return np.concatenate([self.pos / self.S * 2 - 1, self.dir, centre / self.S * 2 - 1])
+
+    def _add_beam(self):
+        """environment.py:107-110."""
+        self.dose += _raster(self.lungs, self.pos, self.dir) * 0.1
+        self.dose = np.clip(self.dose, 0.0, 1.0)
+
+    def _tumour_reward(self):
+        """environment.py:164-171."""
+        on_tumour = self.dose * self.tumours
+        got, size = np.sum(on_tumour), np.sum(self.tumours)
+        return got / size * 10.0
+
+    def _lung_reward(self):
+        """environment.py:173-182."""
+        healthy = self.lungs * (1 - self.tumours)
+        on_lung = self.dose * healthy
+        over = on_lung > 0.2
+        n_over, n_lung = np.sum(over), np.sum(healthy)
+        return n_over / n_lung * -1.0
+
+    def _distance_reward(self):
+        """environment.py:150-162."""
+        coords = self._tumour_coords()
+        diff = coords - np.array(self.pos)
+        dist = np.linalg.norm(diff, axis=1)
+        near = diff[np.argmin(dist)]
+        return np.linalg.norm(near) / np.linalg.norm(self.S) * -1.0
+
+    def _irradiated(self):
+        """environment.py:184-191."""
+        on_tumour = self.dose * self.tumours
+        got, size = np.sum(on_tumour), np.sum(self.tumours)
+        return got / size >= 0.9
 
     def step(self, action):
+        """environment.py:193-243 (info as a flat array: RT_INFO_* order up to 16)."""
         self.t += 1
         tr = np.clip(action[:3], -1.0, 1.0) * self.S * 0.2
         rv = np.clip(action[3:6], -1.0, 1.0) * np.pi * 0.5
@@ -125,17 +171,13 @@ class NumpyEnv:
         self.pos = np.clip(raw, 0, self.S)
         os_t = np.abs(raw - self.pos)
         self.dir, os_r = _rotate(self.dir, rv)
-        self.dose += _raster(self.shape, self.pos, self.dir) * 0.1
-        self.dose = np.clip(self.dose, 0.0, 1.0)
-        t_ratio = np.sum(self.dose * self.tumours) / np.sum(self.tumours)
-        r_tum = t_ratio * 10.0
-        mask = self.lungs * (1 - self.tumours)
-        r_lung = np.sum(self.dose * mask > 0.2) / np.sum(mask) * -1.0
-        diff = self._tumour_coords() - self.pos
-        near = diff[np.argmin(np.linalg.norm(diff, axis=1))]
-        r_dist = np.linalg.norm(near) / np.linalg.norm(self.S) * -1.0
+        self._add_beam()
+        r_tum = self._tumour_reward()
+        r_lung = self._lung_reward()
+        r_dist = self._distance_reward()
         reward = r_tum + r_lung + r_dist
-        done = bool(np.sum(self.dose * self.tumours) / np.sum(self.tumours) >= 0.9 or self.t >= 100)
-        info = np.array([reward, r_tum, r_lung, r_dist, np.sum(self.dose * self.tumours),
-                         np.sum(self.dose * self.lungs), *os_t, os_r, *self.pos, *self.dir])
+        done = bool(self._irradiated() or self.t >= 100)
+        d_tum = float(np.sum(self.dose * self.tumours))
+        d_lung = float(np.sum(self.dose * self.lungs))
+        info = np.array([reward, r_tum, r_lung, r_dist, d_tum, d_lung, *os_t, os_r, *self.pos, *self.dir])
         return self._obs(), info, done

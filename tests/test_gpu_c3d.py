@@ -20,7 +20,6 @@ STAGES = [  # cin, groups, dims, pool_pad, batch
     # planes wider than the 80 KiB conv1 ring: the 160 KiB ring, one-row bands
     (4, 1, (6, 10, 160), (0, 0, 0), 2),
     (16, 2, (6, 9, 79), (0, 0, 0), 2),
-    (16, 1, (6, 7, 101), (0, 0, 0), 2),
 ]
 
 

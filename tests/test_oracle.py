@@ -65,11 +65,14 @@ def test_np_sum_emulation():
         assert O.np_sum_f32(sp) == np.sum(sp), n
 
 
-def _check_traj(z, lib):
+def _check_traj(z, lib, make=None, episodes=None):
+    make = make or O.OracleEnv
     lungs = lib.lungs.astype(np.float32)
     off = 0
     for e, tid in enumerate(z["tumour_id"]):
-        env = O.OracleEnv(lungs, lib.tumour_dense(int(tid)))
+        if episodes is not None and e >= episodes:
+            break
+        env = make(lungs, lib.tumour_dense(int(tid)))
         assert np.array_equal(env.reset(), z["obs0"][e])
         for t in range(int(z["ep_len"][e])):
             obs, info, done = env.step(z["actions"][e][t])
@@ -93,6 +96,15 @@ def _check_traj(z, lib):
 
 def test_env_trajectories_reference_grid(golden):
     _check_traj(golden("env_traj_ref.npz"), assets.reference_library())
+
+
+def test_numpy_port_trajectories_reference_grid(golden):
+    """oracle/numpy_env.py (the CPU baseline bench.py times) reproduces the
+    reference's trajectories: obs, every reward component, doses, done and
+    the final dose volume, bit for bit."""
+    from numpy_env import NumpyEnv
+
+    _check_traj(golden("env_traj_ref.npz"), assets.reference_library(), make=NumpyEnv, episodes=4)
 
 
 def test_env_trajectories_64(golden):
