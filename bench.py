@@ -155,8 +155,9 @@ def cpu_baseline(seconds: float):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     one = d["numpy"]["one_core"]
     out = {"value": one["value"], "unit": "env steps/s", "cores": 1, "kind": "port",
-           "sample": f"{one['steps']} visionless steps of one env, {d['config']} (oracle/numpy_env.py), "
-                     f"{one['seconds']:.1f} s on 1 pinned host core ({d['cpu_model']})",
+           "sample": f"{one['steps']} visionless steps of one env, {d['config']} (oracle/numpy_env.py, "
+                     f"calibrated to the reference: tools/calibrate_cpu.py), {one['seconds']:.1f} s on 1 pinned "
+                     f"host core ({d['cpu_model']}), allocator pinned (the reference's fault-free regime)",
            "cpu_model": d["cpu_model"], "cores_available": d["cores_available"], "cores_cap": d["cores_cap"]}
     if "all_cores" in d["numpy"]:
         out["all_cores"] = {k: d["numpy"]["all_cores"][k] for k in ("value", "cores", "steps")}
@@ -315,10 +316,28 @@ def stream_ceilings(dev, lib_obj, gib: float = 4.0, reps: int = 8) -> dict:
     return out
 
 
+PMC_FILE = os.path.join(REPO, "profiles", "r03", "r03_s2_k_dense_persist_pmc.json")
+
+
 def load_pmc(grid, envs, kernel="k_dense"):
-    """Per-launch HBM traffic of k_dense / k_dense_persist (`envs` per launch)
-    from the committed rocprofv3 PMC runs (tools/parse_pmc.py; gfx950
-    FETCH_SIZE x2 correction applied there)."""
+    """Per-launch HBM traffic (bytes) of the dense stream from the committed
+    rocprofv3 PMC runs, gfx950 FETCH_SIZE x2 correction applied there:
+    k_dense_persist (the pipelined rollout, 2048 envs per launch) from
+    tools/probe_dense_pmc.py + tools/dense_pmc_segments.py on the current
+    kernel -> {"value_window": B, "steady_window": B}; the older single-run
+    files (profiles/{kernel}_pmc.json) otherwise.  None when no run matches."""
+    if kernel == "k_dense_persist":
+        try:
+            with open(PMC_FILE) as f:
+                d = json.load(f)
+            if tuple(d["grid"]) == tuple(grid) and int(d["envs_per_launch"]) == envs:
+                seg = d["segments"]
+                return {"value_window": seg["value_window_20_steps"]["hbm_bytes_median"],
+                        "steady_window": seg["steady_window_64_steps"]["hbm_bytes_median"],
+                        "source": os.path.relpath(PMC_FILE, REPO)}
+        except Exception:
+            return None
+        return None
     p = os.path.join(REPO, "profiles", f"{kernel}_pmc.json")
     try:
         with open(p) as f:
@@ -485,13 +504,17 @@ def main():
     tr.reset()
     T = tr.T
 
-    # ---------------- warmup
-    run_steps(tr, a.warmup)
+    # ---------------- warmup: W untimed rollout steps around one untimed
+    # update (its kernels warm too), so the timed pass follows rollout steps
+    # as it does in a long run
     if a.update_minibatches:
         tr.max_minibatches = a.update_minibatches
+    w1 = a.warmup // 2 if not a.no_update and not a.env_only else a.warmup
+    run_steps(tr, w1)
     if not a.no_update and not a.env_only:
         tr.compute_gae()
         tr.update()
+        run_steps(tr, a.warmup - w1)
     torch.cuda.synchronize()
 
     # ---------------- timed rollout (or env-only)
@@ -627,9 +650,13 @@ def main():
         else:  # whole-handle grid launches (tools/gpu_dense_pmc.sh, bench.py --env-only)
             traffic = load_pmc(grid, a.envs)
     achieved = bytes_launch / (dense_ms * 1e-3)  # = per-launch bytes / per-launch duration (per step)
+    traffic_steady = traffic_src = None
+    if isinstance(traffic, dict):
+        traffic, traffic_steady, traffic_src = traffic["value_window"], traffic["steady_window"], traffic["source"]
     roof = {"bound": "hbm", "kernel": kernel_name, "achieved": achieved / 1e9,
             "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
-            "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch / launches,
+            "traffic": traffic, "traffic_steady_window": traffic_steady, "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": bytes_launch / launches,
             "kernel_ms": dense_ms / launches, "launches_per_step": launches, "k_dense_ms_per_step": dense_ms,
             "kernel_calls_timed": kcalls, "kernel_ms_all": kms, "env_step_ms": env_ms,
             "bytes_model": bytes_model,

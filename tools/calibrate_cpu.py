@@ -84,8 +84,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--cpu", type=int, default=2)
     ap.add_argument("--one", choices=["reference", "port"], help="(child) time one kind in this process")
+    ap.add_argument("--malloc", choices=["default", "pinned"], default="default",
+                    help="pinned: mallopt(M_MMAP_THRESHOLD 32 MiB, M_TRIM_THRESHOLD 64 MiB) before anything runs, "
+                         "so no full-volume temporary lands on freshly faulted pages (both kinds alike)")
     a = ap.parse_args()
     os.sched_setaffinity(0, {a.cpu})
+    if a.one and a.malloc == "pinned":
+        import ctypes
+
+        libc = ctypes.CDLL("libc.so.6")
+        assert libc.mallopt(-3, 32 << 20) == 1 and libc.mallopt(-1, 64 << 20) == 1
     if a.one:
         f0 = resource.getrusage(resource.RUSAGE_SELF).ru_minflt
         n0 = 0
@@ -97,13 +105,14 @@ def main():
     for _ in range(a.rounds):
         for kind in ("reference", "port"):
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", kind, "--seconds", str(a.seconds),
-                                  "--cpu", str(a.cpu), "--ref", a.ref], capture_output=True, text=True, check=True)
+                                  "--cpu", str(a.cpu), "--ref", a.ref, "--malloc", a.malloc],
+                                 capture_output=True, text=True, check=True)
             res[kind].append(json.loads(out.stdout.strip().splitlines()[-1]))
     r = float(np.median([x["steps_per_s"] for x in res["reference"]]))
     p = float(np.median([x["steps_per_s"] for x in res["port"]]))
     print(json.dumps({"reference": res["reference"], "port": res["port"], "reference_median": r,
                       "port_median": p, "port_over_reference": p / r, "within_15pct": abs(p / r - 1) <= 0.15,
-                      "cpu": a.cpu, "seconds_per_run": a.seconds, "process": "fresh per run",
+                      "cpu": a.cpu, "seconds_per_run": a.seconds, "process": "fresh per run", "malloc": a.malloc,
                       "config": "C1: reference grid + tumours, np.random.seed(1), default_rng(0) actions"}))
 
 

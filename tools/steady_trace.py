@@ -60,7 +60,7 @@ def main():
         lo, hi = ks[0][0], max(k[1] for k in ks)
         per = defaultdict(lambda: [0, 0.0])
         for s, e, n, _ in ks:
-            short = n.split("(")[0].split("<")[0].replace("void ", "").strip()
+            short = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:48].strip()
             per[short][0] += 1
             per[short][1] += (e - s) / 1e3
         dense = [(s, e) for s, e, n, _ in ks if "k_dense" in n]
