@@ -350,10 +350,15 @@ int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp_avg_d, flo
                  int64_t step, double lr, const rt_ppo_hparams* hp, float* workspace_d, void* stream);
 
 /* n_minibatches consecutive optimizer steps (rt_ppo_grad + rt_adam_step) on
- * the minibatches perm_d[i*mb_size, (i+1)*mb_size) of one epoch (single
- * process; data-parallel callers interleave rt_ppo_grad, the all-reduce and
- * rt_adam_step themselves).  params_d / grads_d are views of flat_param_d /
- * flat_grad_d; the first step is numbered step0. */
+ * the minibatches perm_d[i*mb_size, (i+1)*mb_size) -- of one epoch, or of
+ * several whose permutations lie back to back in perm_d (rt_ppo_shuffle_epochs),
+ * adv_stats_d then holding [n_minibatches][2] (single process; data-parallel
+ * callers interleave rt_ppo_grad, the all-reduce and rt_adam_step themselves).
+ * params_d / grads_d are views of flat_param_d / flat_grad_d; the first step
+ * is numbered step0.  Per minibatch: the gradient kernel, then ONE launch that
+ * reduces the column sums and whose last-arriving workgroup clips and runs
+ * Adam (k_ppo_reduce_adam; the same bits as rt_adam_step after rt_ppo_grad's
+ * reduce).  Its arrival counter lives in the workspace's last float. */
 int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
                   const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches, const float* adv_stats_d,
                   const rt_ppo_hparams* hp, float* flat_param_d, float* flat_grad_d, float* exp_avg_d,
@@ -366,6 +371,9 @@ int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_
  * using workspace_d (>= 128 * n_minibatches floats; rt_ppo_update's workspace
  * serves). */
 int rt_ppo_shuffle(int64_t n, uint64_t key, int64_t* perm_d, void* stream);
+/* n_epochs permutations in one launch: perm_d[e*n .. (e+1)*n) = rt_ppo_shuffle
+ * with keys_h[e] (host array) -- every epoch's shuffle of an update at once. */
+int rt_ppo_shuffle_epochs(int64_t n, int32_t n_epochs, const uint64_t* keys_h, int64_t* perm_d, void* stream);
 int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
                      float* stats_d, float* workspace_d, int64_t workspace_floats, void* stream);
 /* Data-parallel form of rt_ppo_adv_stats (train.py:215-218 over the union

@@ -1080,6 +1080,129 @@ __global__ __launch_bounds__(256) void k_adam(AdamParams P) {
     P.v[i] = v;
 }
 
+// ---- k_ppo_reduce + k_adam in one launch (single-process rt_ppo_update) -----
+// Every block reduces its 64 columns as k_ppo_reduce does; the block whose
+// arrival on a counter comes last then runs the clip and the Adam step of all
+// parameters (k_adam's arithmetic, same bits).  The hand-off is
+// MI355X_MICROARCH.md's first measured row (no release fence, whose L2
+// write-back made the first fused version slower): the gradient
+// and the norm partials are stored `sc1`, every wave waits for its stores
+// (`s_waitcnt vmcnt(0)`), a workgroup barrier, ONE lane's agent-scope atomic
+// add; the block whose add returns nblk - 1 reads them back with `sc1` loads
+// -- its adding wave after the add returned, the others after a workgroup
+// barrier.  One block per CU (the LDS request below), hipMalloc'd memory.
+// The counter (the workspace's last norm slot) is zeroed by rt_ppo_update
+// before its first launch and re-armed by the last block.
+struct ReduceAdamParams {
+    ReduceParams R;
+    AdamParams A;
+    unsigned* counter;
+};
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kReduceAdamLds = 96 * 1024;  // > 80 KiB: one block per CU (the hand-off's measured condition)
+
+__global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
+    extern __shared__ float dyn[];
+    float (*part)[kReduceCols] = reinterpret_cast<float (*)[kReduceCols]>(dyn);
+    __shared__ int last_s;
+    __shared__ float coef_s;
+    const ReduceParams& P = Q.R;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int p = blockIdx.x * kReduceCols + lane;
+    const bool ok = p < NP + NSTAT;
+    float x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int b = w + 16 * k;
+        x[k] = (ok && b < P.nblk) ? P.ws[(size_t)b * PSTRIDE + p] : 0.0f;
+    }
+#pragma unroll
+    for (int h = 8; h > 0; h >>= 1)
+#pragma unroll
+        for (int k = 0; k < h; ++k) x[k] += x[k + h];
+    part[w][lane] = x[0];
+    __syncthreads();
+    if (w == 0) {
+        float a = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a += part[k][lane];
+        float sq = 0.0f;
+        if (ok) {
+            if (p < NP) {
+                int t = 0;
+#pragma unroll
+                for (int k = 1; k < 13; ++k) t += p >= kTensorOff[k] ? 1 : 0;
+                if (t == 6) a += -P.ent_coef;
+                st_sc1(&P.grad.p[t][p - kTensorOff[t]], a);
+                sq = a * a;
+            } else {
+                const int k = p - NP;
+                float v = a * P.inv_n;
+                if (k == 1) v *= 0.5f;
+                P.stats[k] = v;
+                if (P.stats_accum) P.stats_accum[k] += v;
+            }
+        }
+        sq = wave_sum(sq);
+        if (lane == 0) st_sc1(&P.norm_part[blockIdx.x], sq);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last_s = __hip_atomic_fetch_add(Q.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned)(gridDim.x - 1);
+    __syncthreads();
+    if (!last_s) return;
+    // ---- the last block: clip coefficient, then Adam over all parameters
+    const AdamParams& A = Q.A;
+    if (threadIdx.x < 64) {
+        float t = 0.0f;
+        if (A.max_norm > 0.0f)
+            for (int k = threadIdx.x; k < A.n_part; k += 64) t += ld_sc1(&A.norm_part[k]);
+        t = wave_sum(t);
+        if (threadIdx.x == 0) {
+            coef_s = A.max_norm > 0.0f ? fminf(A.max_norm / (sqrtf(t) + 1e-6f), 1.0f) : 1.0f;
+            __hip_atomic_store(Q.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+        }
+    }
+    __syncthreads();
+    const float coef = coef_s;
+    constexpr int U = (NP + 1023) / 1024;  // 10 parameters per thread, loads in flight together
+    float g[U], m[U], v[U], q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = u * 1024 + threadIdx.x;
+        if (i < A.n) {
+            g[u] = ld_sc1(&A.grad[i]);
+            m[u] = A.m[i];
+            v[u] = A.v[i];
+            q[u] = A.param[i];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = u * 1024 + threadIdx.x;
+        if (i >= A.n) continue;
+        const float gc = g[u] * coef;
+        A.grad[i] = gc;
+        float mm = m[u];
+        mm = mm + A.lerp_w * (gc - mm);
+        float vv = v[u] * A.beta2;
+        vv = vv + A.one_minus_beta2 * gc * gc;
+        const float denom = sqrtf(vv) / A.bc2_sqrt + A.eps;
+        A.param[i] = q[u] + A.step_size * (mm / denom);
+        A.m[i] = mm;
+        A.v[i] = vv;
+    }
+}
+
 // ---- per-epoch shuffle and minibatch advantage statistics ------------------
 // A keyed pseudo-random permutation of [0, n): a 4-round Feistel network on
 // 2h bits (2^(2h) >= n) with cycle-walking, one index per thread -- replaces
@@ -1094,12 +1217,10 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     return x;
 }
 
-__global__ __launch_bounds__(256) void k_shuffle(int64_t n, int h, uint64_t key, int64_t* perm) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ uint32_t feistel_index(uint32_t i, int64_t n, int h, uint64_t key) {
     const uint32_t mask = (1u << h) - 1u;
     const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
-    uint32_t v = (uint32_t)i;
+    uint32_t v = i;
     do {
         uint32_t L = v >> h, R = v & mask;
 #pragma unroll
@@ -1111,7 +1232,23 @@ __global__ __launch_bounds__(256) void k_shuffle(int64_t n, int h, uint64_t key,
         }
         v = (L << h) | R;
     } while ((int64_t)v >= n);
-    perm[i] = v;
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_shuffle(int64_t n, int h, uint64_t key, int64_t* perm) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) perm[i] = feistel_index((uint32_t)i, n, h, key);
+}
+
+// every epoch's permutation in one launch: blockIdx.y = epoch, key keys[y]
+constexpr int kShuffleKeys = 32;
+struct ShuffleKeys {
+    uint64_t k[kShuffleKeys];
+};
+
+__global__ __launch_bounds__(256) void k_shuffle_epochs(int64_t n, int h, ShuffleKeys K, int64_t* perm) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) perm[(int64_t)blockIdx.y * n + i] = feistel_index((uint32_t)i, n, h, K.k[blockIdx.y]);
 }
 
 // [n_mb][2] = (mean, unbiased std) of adv over each minibatch of perm
@@ -1213,19 +1350,40 @@ bool rt_ppo_use_mfma() {
     return v != 0;
 }
 
+// RT_PPO_FUSED_ADAM=0: rt_ppo_update launches k_ppo_reduce + k_adam (A/B runs)
+bool use_reduce_adam() {
+    static const int v = [] {
+        const char* e = std::getenv("RT_PPO_FUSED_ADAM");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+}
+
+ReduceParams reduce_params(float* const* grads_d, int32_t mb, const rt_ppo_hparams* hp, float* ws_d,
+                           int64_t ws_floats, float* stats_d, float* accum_d) {
+    ReduceParams R{};
+    for (int i = 0; i < 13; ++i) R.grad.p[i] = grads_d[i];
+    R.ws = ws_d;
+    R.nblk = rt_ppo_use_mfma() ? grad_blocks(mb) : (mb + TS - 1) / TS;
+    R.stats = stats_d;
+    R.stats_accum = accum_d;
+    R.norm_part = ws_d + (ws_floats - kNormSlots);
+    R.inv_n = 1.0f / (float)mb;
+    R.ent_coef = hp->ent_coef;
+    return R;
+}
+
 int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* b,
                     const int64_t* idx_d, int32_t mb, const float* adv_stats_d, const rt_ppo_hparams* hp,
-                    float* ws_d, int64_t ws_floats, float* stats_d, float* accum_d, hipStream_t st) {
+                    float* ws_d, int64_t ws_floats, float* stats_d, float* accum_d, hipStream_t st,
+                    int with_reduce = 1) {
     const bool use_mfma = rt_ppo_use_mfma();
     const int nblk = use_mfma ? grad_blocks(mb) : (mb + TS - 1) / TS;
     if ((int64_t)nblk * PSTRIDE + kNormSlots > ws_floats)
         return rt_internal_fail(RT_EINVAL, "rt_ppo_grad: workspace too small");
     GradParams G{};
     ReduceParams R{};
-    for (int i = 0; i < 13; ++i) {
-        G.w.p[i] = params_d[i];
-        R.grad.p[i] = grads_d[i];
-    }
+    for (int i = 0; i < 13; ++i) G.w.p[i] = params_d[i];
     G.obs = b->obs;
     G.act = b->actions;
     G.logp = b->logprobs;
@@ -1245,14 +1403,8 @@ int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const r
         hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblk), dim3(MT), 0, st, G);
     else
         hipLaunchKernelGGL(k_ppo_grad, dim3(nblk), dim3(kThreads), 0, st, G);
-    R.ws = ws_d;
-    R.nblk = nblk;
-    R.stats = stats_d;
-    R.stats_accum = accum_d;
-    R.norm_part = ws_d + (ws_floats - kNormSlots);
-    R.inv_n = 1.0f / (float)mb;
-    R.ent_coef = hp->ent_coef;
-    hipLaunchKernelGGL(k_ppo_reduce, dim3(kReduceBlocks), dim3(1024), 0, st, R);
+    R = reduce_params(grads_d, mb, hp, ws_d, ws_floats, stats_d, accum_d);
+    if (with_reduce) hipLaunchKernelGGL(k_ppo_reduce, dim3(kReduceBlocks), dim3(1024), 0, st, R);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
@@ -1260,8 +1412,8 @@ int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const r
 
 // norm_part: the kReduceBlocks partials k_ppo_reduce left (fresh = true), or
 // scratch for k_gnorm over the (all-reduced) flat gradient
-int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step, double lr,
-                const rt_ppo_hparams* hp, float* norm_part, bool fresh, hipStream_t st) {
+AdamParams adam_params(int64_t n, float* p, float* g, float* m, float* v, int64_t step, double lr,
+                       const rt_ppo_hparams* hp, float* norm_part) {
     AdamParams A{};
     A.n = n;
     A.param = p;
@@ -1271,10 +1423,6 @@ int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step,
     A.max_norm = hp->max_grad_norm;
     A.norm_part = norm_part;
     A.n_part = kReduceBlocks;
-    if (A.max_norm > 0.0f && !fresh) {
-        const int64_t per = (n + kReduceBlocks - 1) / kReduceBlocks;
-        hipLaunchKernelGGL(k_gnorm, dim3(kReduceBlocks), dim3(256), 0, st, g, n, per, norm_part);
-    }
     const double b1 = hp->adam_beta1, b2 = hp->adam_beta2;
     // torch.optim.Adam (foreach): host-side scalars in double, applied in f32
     A.lerp_w = (float)(1.0 - b1);
@@ -1283,6 +1431,16 @@ int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step,
     A.step_size = (float)(-(lr / (1.0 - std::pow(b1, (double)step))));
     A.bc2_sqrt = (float)std::pow(1.0 - std::pow(b2, (double)step), 0.5);
     A.eps = hp->adam_eps;
+    return A;
+}
+
+int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step, double lr,
+                const rt_ppo_hparams* hp, float* norm_part, bool fresh, hipStream_t st) {
+    const AdamParams A = adam_params(n, p, g, m, v, step, lr, hp, norm_part);
+    if (A.max_norm > 0.0f && !fresh) {
+        const int64_t per = (n + kReduceBlocks - 1) / kReduceBlocks;
+        hipLaunchKernelGGL(k_gnorm, dim3(kReduceBlocks), dim3(256), 0, st, g, n, per, norm_part);
+    }
     hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
@@ -1340,17 +1498,41 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
     if (bad13(reinterpret_cast<const void* const*>(params_d)) || bad13(reinterpret_cast<const void* const*>(grads_d)) ||
         bad_batch(batch) || !perm_d || mb_size < 1 || n_minibatches < 1 || !hp || !flat_param_d || !flat_grad_d ||
         !exp_avg_d || !exp_avg_sq_d || n_flat != NP || step0 < 1 || !workspace_d || !stats_d ||
-        (hp->norm_adv && !adv_stats_d) || (int64_t)mb_size * n_minibatches > batch->batch_size)
+        (hp->norm_adv && !adv_stats_d) || mb_size > batch->batch_size)
         return rt_internal_fail(RT_EINVAL, "rt_ppo_update: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    float* norm_part = workspace_d + (workspace_floats - kNormSlots);
+    const bool fused = use_reduce_adam();
+    if (fused) {
+        static bool attr = false;
+        if (!attr) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_reduce_adam),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kReduceAdamLds);
+            if (e != hipSuccess) return rt_internal_fail(RT_EDEVICE, hipGetErrorString(e));
+            attr = true;
+        }
+        // the arrival counter: the workspace's last norm slot (unused by the partials)
+        const hipError_t e = hipMemsetAsync(norm_part + (kNormSlots - 1), 0, sizeof(unsigned), st);
+        if (e != hipSuccess) return rt_internal_fail(RT_EDEVICE, hipGetErrorString(e));
+    }
     for (int i = 0; i < n_minibatches; ++i) {
         int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
                                  adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,
-                                 stats_d, stats_accum_d, st);
+                                 stats_d, stats_accum_d, st, fused ? 0 : 1);
         if (rc) return rc;
-        rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp,
-                         workspace_d + (workspace_floats - kNormSlots), true, st);
-        if (rc) return rc;
+        if (!fused) {
+            rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part,
+                             true, st);
+            if (rc) return rc;
+            continue;
+        }
+        ReduceAdamParams Q{};
+        Q.R = reduce_params(grads_d, mb_size, hp, workspace_d, workspace_floats, stats_d, stats_accum_d);
+        Q.A = adam_params(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part);
+        Q.counter = reinterpret_cast<unsigned*>(norm_part + (kNormSlots - 1));
+        hipLaunchKernelGGL(k_ppo_reduce_adam, dim3(kReduceBlocks), dim3(1024), kReduceAdamLds, st, Q);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     }
     return RT_OK;
 }
@@ -1362,6 +1544,26 @@ extern "C" int rt_ppo_shuffle(int64_t n, uint64_t key, int64_t* perm_d, void* st
     const int h = (b + 1) / 2;
     hipLaunchKernelGGL(k_shuffle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), n, h, key, perm_d);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_ppo_shuffle_epochs(int64_t n, int32_t n_epochs, const uint64_t* keys_h, int64_t* perm_d,
+                                     void* stream) {
+    if (n < 1 || n > ((int64_t)1 << 31) || n_epochs < 1 || !keys_h || !perm_d)
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_shuffle_epochs: bad argument");
+    int b = 1;
+    while (((int64_t)1 << b) < n) ++b;
+    const int h = (b + 1) / 2;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    for (int e0 = 0; e0 < n_epochs; e0 += kShuffleKeys) {
+        const int ne = n_epochs - e0 < kShuffleKeys ? n_epochs - e0 : kShuffleKeys;
+        ShuffleKeys K{};
+        for (int j = 0; j < ne; ++j) K.k[j] = keys_h[e0 + j];
+        hipLaunchKernelGGL(k_shuffle_epochs, dim3((unsigned)((n + 255) / 256), (unsigned)ne), dim3(256), 0, st, n, h,
+                           K, perm_d + (int64_t)e0 * n);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;

@@ -171,12 +171,14 @@ class PPOTrainer:
                 clip_coef=float(cfg.clip_coef), clip_vloss=int(bool(cfg.clip_vloss)), norm_adv=int(bool(cfg.norm_adv)),
                 ent_coef=float(cfg.ent_coef), vf_coef=float(cfg.vf_coef), max_grad_norm=float(cfg.max_grad_norm),
                 adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
-            n_mb = self.batch_size // self.minibatch_size  # rt_ppo_adv_stats shares the workspace
-            self._ws = torch.empty(max(int(L.rt_ppo_workspace_floats(self.minibatch_size)), 128 * n_mb), **kw)
+            n_mb = self.batch_size // self.minibatch_size
+            E = max(1, int(cfg.update_epochs))
+            # rt_ppo_adv_stats (all epochs' minibatches at once) shares the workspace
+            self._ws = torch.empty(max(int(L.rt_ppo_workspace_floats(self.minibatch_size)), 128 * n_mb * E), **kw)
             self._norm_ws = torch.empty(256, **kw)
-            self._perm_buf = torch.empty(self.batch_size, dtype=torch.int64, **kw)
-            self._adv_stats_buf = torch.empty((self.batch_size // self.minibatch_size, 2), **kw)
-            self._adv_sums = torch.empty((self.batch_size // self.minibatch_size, 2), dtype=torch.float64, **kw)
+            self._perm_buf = torch.empty((E, self.batch_size), dtype=torch.int64, **kw)  # every epoch's shuffle
+            self._adv_stats_buf = torch.empty((E * n_mb, 2), **kw)
+            self._adv_sums = torch.empty((E * n_mb, 2), dtype=torch.float64, **kw)
             # epoch shuffle keys: a host generator seeded from the trainer's seed and rank
             self._host_gen = torch.Generator().manual_seed(int(getattr(cfg, "seed", 0)) * 7919 + 104729 * rank + 17)
         self.next_obs = None
@@ -453,40 +455,46 @@ class PPOTrainer:
                                self._b_adv.data_ptr(), self._b_ret.data_ptr(), self._b_val.data_ptr(),
                                self.batch_size)
 
-    def _epoch_perm_stats(self, L, stream, n_mb):
-        """One epoch's shuffle (rt_ppo_shuffle, keyed by a draw from the
-        trainer's generator) and minibatch advantage statistics
-        (rt_ppo_adv_stats; all-reduced sums when world > 1)."""
-        key = int(torch.randint(0, 2 ** 62, (1,), generator=self._host_gen).item())
-        perm = self._perm_buf
-        _lib.check(L.rt_ppo_shuffle(self.batch_size, key, perm.data_ptr(), stream), "rt_ppo_shuffle")
+    def _epochs_perm_stats(self, L, stream, n_mb: int, epochs: int):
+        """The shuffles of `epochs` epochs (rt_ppo_shuffle_epochs, one key per
+        epoch drawn in order from the trainer's generator, so epoch e has the
+        permutation a per-epoch draw would give) and the advantage statistics
+        of all their minibatches (rt_ppo_adv_stats; with world > 1 the sums are
+        all-reduced, once for all epochs) -- three launches per update instead
+        of three per epoch."""
+        keys = (ctypes.c_uint64 * epochs)(*[int(torch.randint(0, 2 ** 62, (1,), generator=self._host_gen).item())
+                                            for _ in range(epochs)])
+        perm = self._perm_buf[:epochs]
+        _lib.check(L.rt_ppo_shuffle_epochs(self.batch_size, epochs, keys, perm.data_ptr(), stream),
+                   "rt_ppo_shuffle_epochs")
         if self.record_perms is not None:  # test hook: the epochs' minibatch rows
-            self.record_perms.append(perm.clone())
+            self.record_perms.extend(p.clone() for p in perm)
         if not self.cfg.norm_adv:
             return perm, None
+        k = epochs * n_mb
+        stats = self._adv_stats_buf[:k]
         if self.collective:
             # this rank's (sum, sum of squares) per minibatch -> ONE all-reduce
-            # of [n_mb, 2] f64 -> global (mean, std) over mbs x world rows
-            _lib.check(L.rt_ppo_adv_sums(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, n_mb,
-                                         self._adv_sums.data_ptr(), self._ws.data_ptr(), self._ws.numel(), stream),
+            # of [k, 2] f64 -> global (mean, std) over mbs x world rows
+            sums = self._adv_sums[:k]
+            _lib.check(L.rt_ppo_adv_sums(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, k,
+                                         sums.data_ptr(), self._ws.data_ptr(), self._ws.numel(), stream),
                        "rt_ppo_adv_sums")
-            dist.all_reduce(self._adv_sums)
-            _lib.check(L.rt_ppo_adv_finalize(self._adv_sums.data_ptr(), self.minibatch_size * self.world, n_mb,
-                                             self._adv_stats_buf.data_ptr(), stream), "rt_ppo_adv_finalize")
-            return perm, self._adv_stats_buf
-        _lib.check(L.rt_ppo_adv_stats(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, n_mb,
-                                      self._adv_stats_buf.data_ptr(), self._ws.data_ptr(), self._ws.numel(),
-                                      stream), "rt_ppo_adv_stats")
-        return perm, self._adv_stats_buf
+            dist.all_reduce(sums)
+            _lib.check(L.rt_ppo_adv_finalize(sums.data_ptr(), self.minibatch_size * self.world, k,
+                                             stats.data_ptr(), stream), "rt_ppo_adv_finalize")
+            return perm, stats
+        _lib.check(L.rt_ppo_adv_stats(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, k,
+                                      stats.data_ptr(), self._ws.data_ptr(), self._ws.numel(), stream),
+                   "rt_ppo_adv_stats")
+        return perm, stats
 
     def _update_fused(self):
-        """train.py:183-248 through the fused kernels: per epoch one device
-        randperm and one (all-reduced) advantage-statistics reduction, then per
-        minibatch rt_ppo_grad + rt_adam_step (world 1: the whole epoch is one
+        """train.py:183-248 through the fused kernels: every epoch's shuffle and
+        (all-reduced) minibatch advantage statistics up front, then per
+        minibatch rt_ppo_grad + the clip/Adam step (world 1: all of it is ONE
         rt_ppo_update call; world > 1: RCCL all-reduce of the flat gradient
-        bucket between the two)."""
-        import ctypes
-
+        bucket between rt_ppo_grad and rt_adam_step)."""
         self._bind_batch()
         L = _lib.load()
         stream = _lib.stream_handle()
@@ -497,36 +505,36 @@ class PPOTrainer:
         lr = float(self.optimizer.param_groups[0]["lr"])
         n = self.flat_param.numel()
         self._ppo_accum.zero_()
-        done = 0
-        for _ in range(int(self.cfg.update_epochs)):
-            perm, adv = self._epoch_perm_stats(L, stream, n_mb)
-            k = n_mb if not self.max_minibatches else min(n_mb, self.max_minibatches - done)
-            if not self.collective:
-                _lib.check(L.rt_ppo_update(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch), perm.data_ptr(),
-                                           mbs, k, _lib.ptr(adv), hp, self.flat_param.data_ptr(),
-                                           self.flat_grad.data_ptr(), self._exp_avg.data_ptr(),
-                                           self._exp_avg_sq.data_ptr(), n, self._adam_step + 1, lr,
-                                           self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
-                                           self._ppo_accum.data_ptr(), stream), "rt_ppo_update")
-                self._adam_step += k
-            else:
-                for i in range(k):
-                    _lib.check(L.rt_ppo_grad(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch),
-                                             perm.data_ptr() + 8 * i * mbs, mbs,
-                                             None if adv is None else adv.data_ptr() + 8 * i, hp,
-                                             self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
-                                             self._ppo_accum.data_ptr(), stream), "rt_ppo_grad")
-                    self._allreduce_(self.flat_grad)
-                    self._adam_step += 1
-                    _lib.check(L.rt_adam_step(n, self.flat_param.data_ptr(), self.flat_grad.data_ptr(),
-                                              self._exp_avg.data_ptr(), self._exp_avg_sq.data_ptr(),
-                                              self._adam_step, lr, hp, self._norm_ws.data_ptr(), stream),
-                               "rt_adam_step")
-            done += k
-            if self.max_minibatches and done >= self.max_minibatches:
-                break
-        self._last_stats = torch.cat([self._ppo_stats[:5], (self._ppo_accum[5] / max(done, 1)).reshape(1)])
-        return done
+        total = int(self.cfg.update_epochs) * n_mb
+        if self.max_minibatches:
+            total = min(total, self.max_minibatches)
+        epochs = -(-total // n_mb)
+        if total < 1:
+            return 0
+        perm, adv = self._epochs_perm_stats(L, stream, n_mb, epochs)
+        if not self.collective:
+            _lib.check(L.rt_ppo_update(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch), perm.data_ptr(),
+                                       mbs, total, _lib.ptr(adv), hp, self.flat_param.data_ptr(),
+                                       self.flat_grad.data_ptr(), self._exp_avg.data_ptr(),
+                                       self._exp_avg_sq.data_ptr(), n, self._adam_step + 1, lr,
+                                       self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
+                                       self._ppo_accum.data_ptr(), stream), "rt_ppo_update")
+            self._adam_step += total
+        else:
+            for i in range(total):
+                _lib.check(L.rt_ppo_grad(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch),
+                                         perm.data_ptr() + 8 * i * mbs, mbs,
+                                         None if adv is None else adv.data_ptr() + 8 * i, hp,
+                                         self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
+                                         self._ppo_accum.data_ptr(), stream), "rt_ppo_grad")
+                self._allreduce_(self.flat_grad)
+                self._adam_step += 1
+                _lib.check(L.rt_adam_step(n, self.flat_param.data_ptr(), self.flat_grad.data_ptr(),
+                                          self._exp_avg.data_ptr(), self._exp_avg_sq.data_ptr(),
+                                          self._adam_step, lr, hp, self._norm_ws.data_ptr(), stream),
+                           "rt_adam_step")
+        self._last_stats = torch.cat([self._ppo_stats[:5], (self._ppo_accum[5] / total).reshape(1)])
+        return total
 
     def update(self):
         """train.py:183-248: update_epochs x num_minibatches optimizer steps."""

@@ -58,20 +58,15 @@ def test_update_matches_float64_reference(fused):
         return out
 
     torch.randperm = rp
-    if fused:  # the fused update shuffles with rt_ppo_shuffle: record those permutations
-        eps = e._epoch_perm_stats
-
-        def rec_eps(*a, **k):
-            perm, adv = eps(*a, **k)
-            rec.append(perm.cpu().clone())
-            return perm, adv
-
-        e._epoch_perm_stats = rec_eps
+    if fused:  # the fused update shuffles with rt_ppo_shuffle_epochs: record those permutations
+        e.record_perms = []
     try:
         e.update()
         e.update()
     finally:
         torch.randperm = orig
+    if fused:
+        rec.extend(p.cpu() for p in e.record_perms)
     torch.manual_seed(0)
     c = PPOTrainer(_cfg(), FakeVecEnv(256), PPO((9,), (6,), 64).double(), "cpu", gae_fn=torch_gae)
     for tc, te in zip((c.obs, c.actions, c.logprobs, c.advantages, c.returns, c.values),
@@ -291,6 +286,27 @@ def test_shuffle_is_a_permutation_and_adv_stats(n):
         torch.testing.assert_close(st, torch.stack([a.mean(1), a.std(1)], 1), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("n,epochs", [(1000, 3), (262144, 10), (77, 40)])
+def test_shuffle_epochs_equals_per_epoch_shuffles(n, epochs):
+    """rt_ppo_shuffle_epochs (every epoch of an update in one launch; more than
+    32 keys take several) = rt_ppo_shuffle per epoch with the same keys."""
+    import ctypes
+
+    from ppo_radiotherapy_amd import _lib
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = torch.device("cuda")
+    L = _lib.load()
+    keys = [(0x9E3779B97F4A7C15 * (e + 1)) & (2 ** 62 - 1) for e in range(epochs)]
+    got = torch.empty((epochs, n), dtype=torch.int64, device=dev)
+    _lib.check(L.rt_ppo_shuffle_epochs(n, epochs, (ctypes.c_uint64 * epochs)(*keys), got.data_ptr(), None), "epochs")
+    for e, k in enumerate(keys):
+        one = torch.empty(n, dtype=torch.int64, device=dev)
+        _lib.check(L.rt_ppo_shuffle(n, k, one.data_ptr(), None), "shuffle")
+        assert torch.equal(got[e], one), e
+
+
 def test_fused_checkpoint_resume_is_bitwise():
     """load_state_dict restores the parameters, the Adam moments and
     step and the epoch-shuffle stream bitwise (through torch.save /
@@ -318,3 +334,39 @@ def test_fused_checkpoint_resume_is_bitwise():
     torch.cuda.synchronize()
     assert torch.equal(a.flat_param, b.flat_param)
     assert torch.equal(a._exp_avg_sq, b._exp_avg_sq)
+
+
+_AB_SCRIPT = r"""
+import os, sys, hashlib
+sys.path[:0] = [{tests!r}, {repo!r}]
+import _rtpkg, torch
+import test_gpu_trainer as T
+tr = T._make(True)
+tr.update(); tr.update()
+torch.cuda.synchronize()
+h = hashlib.sha256()
+for t in (tr.flat_param, tr._exp_avg, tr._exp_avg_sq, tr.flat_grad, tr._ppo_stats, tr._ppo_accum):
+    h.update(t.detach().cpu().numpy().tobytes())
+print("HASH", h.hexdigest())
+"""
+
+
+def test_fused_reduce_adam_is_bitwise_the_three_kernel_update():
+    """rt_ppo_update's k_ppo_reduce_adam (one launch: column reduce, then the
+    last-arriving block clips and runs Adam over all parameters) leaves the
+    parameters, Adam moments, gradient and loss statistics bit-identical to
+    k_ppo_reduce + k_adam (RT_PPO_FUSED_ADAM=0) over 2 x 3 epochs x 4
+    minibatches -- same sums in the same order, handed off through sc1 memory."""
+    import subprocess
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = _AB_SCRIPT.format(tests=here, repo=os.path.dirname(here))
+    out = {}
+    for v in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                           env=dict(os.environ, RT_PPO_FUSED_ADAM=v))
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[v] = [x for x in r.stdout.splitlines() if x.startswith("HASH")][-1]
+    assert out["1"] == out["0"], out
