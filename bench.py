@@ -645,9 +645,9 @@ def main():
     else:
         dense_ms = kms["k_dense"]  # per step: the launches of all env groups
         kernel_name = "k_dense"
-        if launches > 1.5:  # pipelined: k_dense_persist over half the envs (tools/gpu_dense_persist_pmc.sh)
+        if launches > 1.5:  # pipelined: k_dense_persist over half the envs (tools/archive/gpu_dense_persist_pmc.sh)
             traffic = load_pmc(grid, a.envs // 2, "k_dense_persist")
-        else:  # whole-handle grid launches (tools/gpu_dense_pmc.sh, bench.py --env-only)
+        else:  # whole-handle grid launches (tools/archive/gpu_dense_pmc.sh, bench.py --env-only)
             traffic = load_pmc(grid, a.envs)
     achieved = bytes_launch / (dense_ms * 1e-3)  # = per-launch bytes / per-launch duration (per step)
     traffic_steady = traffic_src = None

@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${OUT:-kt}
 mkdir -p $OUT
-NOBENCH=1 OUT=${OUT#gpurun_out/} VARS=kt7 bash tools/gpu_c3d_var_ab.sh || exit 1
+NOBENCH=1 OUT=${OUT#gpurun_out/} VARS=kt7 bash tools/archive/gpu_c3d_var_ab.sh || exit 1
 for v in tree kt7; do
   if [ $v = tree ]; then unset RT_LIB_PATH; else export RT_LIB_PATH=$PWD/_variants/librtenv_$v.so; fi
   for gr in 64 128; do

@@ -1,4 +1,4 @@
-"""Summarise tools/gpu_c3d_ab.sh logs: per variant, per stage ms (min over passes)."""
+"""Summarise tools/archive/gpu_c3d_ab.sh logs: per variant, per stage ms (min over passes)."""
 import glob
 import json
 import os

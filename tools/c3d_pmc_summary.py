@@ -1,4 +1,4 @@
-"""Summarise tools/gpu_c3d_pmc.sh: per C3D kernel, median counters over dispatches,
+"""Summarise tools/archive/gpu_c3d_pmc.sh: per C3D kernel, median counters over dispatches,
 MFMA-busy fraction of SIMD cycles and the effective clock (GRBM_GUI_ACTIVE / 8 XCDs /
 kernel time), with the kernel times of the trace pass.
 
@@ -47,5 +47,5 @@ for k, cs in vals.items():
           f"salu/mfma {row.get('salu_per_mfma', 0):5.2f} wait_inst {m.get('SQ_WAIT_INST_ANY', 0) / max(m.get('SQ_WAVE_CYCLES', 1), 1):5.2f} "
           f"wait_any {m.get('SQ_WAIT_ANY', 0) / max(m.get('SQ_WAVE_CYCLES', 1), 1):5.2f}")
 if len(sys.argv) > 2:
-    json.dump({"source": "tools/gpu_c3d_pmc.sh over tools/c3d_pmc_driver.py (batch 64, 64^3 stage shapes)",
+    json.dump({"source": "tools/archive/gpu_c3d_pmc.sh over tools/c3d_pmc_driver.py (batch 64, 64^3 stage shapes)",
                "kernels": out}, open(sys.argv[2], "w"), indent=1)
