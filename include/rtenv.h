@@ -355,10 +355,8 @@ int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp_avg_d, flo
  * adv_stats_d then holding [n_minibatches][2] (single process; data-parallel
  * callers interleave rt_ppo_grad, the all-reduce and rt_adam_step themselves).
  * params_d / grads_d are views of flat_param_d / flat_grad_d; the first step
- * is numbered step0.  Per minibatch: the gradient kernel, then ONE launch that
- * reduces the column sums and whose last-arriving workgroup clips and runs
- * Adam (k_ppo_reduce_adam; the same bits as rt_adam_step after rt_ppo_grad's
- * reduce).  Its arrival counter lives in the workspace's last float. */
+ * is numbered step0.  Uses the workspace's last float as scratch (the arrival
+ * counter of the opt-in fused reduce + Adam launch, RT_PPO_FUSED_ADAM=1). */
 int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
                   const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches, const float* adv_stats_d,
                   const rt_ppo_hparams* hp, float* flat_param_d, float* flat_grad_d, float* exp_avg_d,

@@ -1080,7 +1080,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamParams P) {
     P.v[i] = v;
 }
 
-// ---- k_ppo_reduce + k_adam in one launch (single-process rt_ppo_update) -----
+// ---- k_ppo_reduce + k_adam in one launch (opt-in, RT_PPO_FUSED_ADAM=1) ------
 // Every block reduces its 64 columns as k_ppo_reduce does; the block whose
 // arrival on a counter comes last then runs the clip and the Adam step of all
 // parameters (k_adam's arithmetic, same bits).  The hand-off is
@@ -1350,11 +1350,14 @@ bool rt_ppo_use_mfma() {
     return v != 0;
 }
 
-// RT_PPO_FUSED_ADAM=0: rt_ppo_update launches k_ppo_reduce + k_adam (A/B runs)
+// RT_PPO_FUSED_ADAM=1: rt_ppo_update launches k_ppo_reduce_adam instead of
+// k_ppo_reduce + k_adam -- bitwise the same update, measured slower (13.1 us
+// vs 5.1 + 5.6: the last block's Adam over all 10,061 parameters is
+// VALU-bound on one CU), kept for A/B runs
 bool use_reduce_adam() {
     static const int v = [] {
         const char* e = std::getenv("RT_PPO_FUSED_ADAM");
-        return (e && e[0] == '0') ? 0 : 1;
+        return (e && e[0] == '1') ? 1 : 0;
     }();
     return v != 0;
 }

@@ -352,11 +352,12 @@ print("HASH", h.hexdigest())
 
 
 def test_fused_reduce_adam_is_bitwise_the_three_kernel_update():
-    """rt_ppo_update's k_ppo_reduce_adam (one launch: column reduce, then the
-    last-arriving block clips and runs Adam over all parameters) leaves the
-    parameters, Adam moments, gradient and loss statistics bit-identical to
-    k_ppo_reduce + k_adam (RT_PPO_FUSED_ADAM=0) over 2 x 3 epochs x 4
-    minibatches -- same sums in the same order, handed off through sc1 memory."""
+    """rt_ppo_update's opt-in k_ppo_reduce_adam (RT_PPO_FUSED_ADAM=1: one
+    launch, column reduce, then the last-arriving block clips and runs Adam
+    over all parameters) leaves the parameters, Adam moments, gradient and
+    loss statistics bit-identical to k_ppo_reduce + k_adam (the default) over
+    2 x 3 epochs x 4 minibatches -- same sums in the same order, handed off
+    through sc1 memory."""
     import subprocess
 
     if not torch.cuda.is_available():
