@@ -1613,6 +1613,167 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring_zs(WgradRingParams
     }
 }
 
+// ---- weight gradient through the pooling argmax (the launched one) ----------
+// dW[co][ci][tap] = sum over pooled windows w of dY[co][w] * X[ci][p(co, w) + tap],
+// p = the conv position the window's argmax names; db[co] = sum_w dY[co][w].
+// The dense form (k_conv_wgrad_ring) multiplies every conv position's
+// gradient, 7 of 8 of which the max-pool zeroed; here each (co, window) is
+// one 27-tap gather of its argmax patch, 1/8 of the multiply-adds, as f32
+// FMAs on the VALU with the patch read from the forward's plane ring.
+// Thread = (window stream s, output channel co, in-group input channel cig):
+// L = 16 * cin/G threads cover one window (one wave for conv1 and conv3, two
+// for conv2), NS = 512 / L windows in flight per block; acc[27] per thread,
+// summed over the streams through LDS in a fixed order at the end, then over
+// the blocks by k_wgrad_reduce (deterministic).  A row's (gradient, argmax)
+// pairs of the band are loaded into registers beside the next planes' DMA and
+// written to a double-buffered LDS row after the row's gathers, so the
+// row's one wait + barrier covers both.  LDS strides: YS = 4, CS = 8, SLOT =
+// 2 (mod 32 dwords) put conv1's 4 channels x 8 argmax offsets of a half-wave
+// (8 output channels) on 32 distinct banks, ring wrap included.
+constexpr int kWgSparseMaxG = 4;  // a band row holds <= 512 * 4 (channel, window) entries
+
+template <int CIN, int G, int PYB>
+__global__ __launch_bounds__(512) void k_conv_wgrad_sparse(WgradRingParams P) {
+    extern __shared__ float xs[];
+    constexpr int CPG = CIN / G;   // input channels per group
+    constexpr int L = CO * CPG;    // threads per window
+    constexpr int NS = 512 / L;    // window streams per block
+    constexpr int NW = 8;
+    const Geom& g = P.rg.g;
+    const int SLOT = P.rg.SLOT;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int sidx = tid / L, li = tid - sidx * L;
+    const int co = li / CPG, cig = li - co * CPG;
+    const int ci = (co / (CO / G)) * CPG + cig;
+    const int py0 = blockIdx.x * PYB;
+    const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
+    const int nwin = PYB * g.PW;  // windows of one pooled row of the band
+    const int chan = g.PD * g.PH * g.PW;
+    float* gbuf = xs + kRing * SLOT;                                   // [2][CO][nwin] gradient (0: inactive)
+    uint8_t* jbuf = reinterpret_cast<uint8_t*>(gbuf + 2 * CO * nwin);  // [2][CO][nwin] argmax index
+    RingLoader<CIN, 1, NW> ld;
+    ld.init(P.rg, y0, x0, wave, lane);
+    float acc[27];
+#pragma unroll
+    for (int q = 0; q < 27; ++q) acc[q] = 0.0f;
+    float dbacc = 0.0f;
+    // (gradient, argmax) entries of a band row per thread: entry e = tid + 512 i
+    // is (channel e / nwin, window e % nwin); its element offset in a sample
+    // is off[i] + k * PH * PW at pooled row k (-1: past the band / volume)
+    constexpr int MAXG = kWgSparseMaxG;
+    int off[MAXG];
+#pragma unroll
+    for (int i = 0; i < MAXG; ++i) {
+        const int e = tid + 512 * i;
+        off[i] = -1;
+        if (e < CO * nwin) {
+            const int c2 = e / nwin, w = e - c2 * nwin, r = w / g.PW, px = w - r * g.PW, py = py0 + r;
+            if (py < g.PH) off[i] = c2 * chan + py * g.PW + px;
+        }
+    }
+    const int plane = g.PH * g.PW;
+    for (int b = blockIdx.z; b < P.B; b += gridDim.z) {
+        const int64_t srow = P.rows ? P.rows[b] : b;
+        const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
+        const uint8_t* amb = P.am + (int64_t)b * CO * chan;
+        const float* dpb = P.dP + (int64_t)b * CO * chan;
+        float gv[MAXG];
+        int jv[MAXG];
+        auto load_row = [&](int k) {
+#pragma unroll
+            for (int i = 0; i < MAXG; ++i) {
+                const int o = off[i] + k * plane;
+                const int byte = off[i] >= 0 ? amb[o] : 0;
+                gv[i] = off[i] >= 0 ? dpb[o] : 0.0f;
+                jv[i] = byte;
+            }
+        };
+        auto store_row = [&](int buf) {
+#pragma unroll
+            for (int i = 0; i < MAXG; ++i) {
+                const int e = tid + 512 * i;
+                if (e < CO * nwin) {
+                    gbuf[buf * CO * nwin + e] = (jv[i] & 8) ? gv[i] : 0.0f;  // inactive window (max <= 0): no gradient
+                    jbuf[buf * CO * nwin + e] = (uint8_t)(jv[i] & 7);
+                }
+            }
+        };
+        __syncthreads();  // the previous sample's ring and row reads are done
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ld.load(xb, P.rg, xs, i, i, wave, lane);
+        load_row(0);
+        store_row(0);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+        int sb = 0;
+        for (int k = 0; k < g.PD; ++k) {
+            const bool more = k + 1 < g.PD;
+            if (more) {
+                ld.load(xb, P.rg, xs, 2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4, wave, lane);
+                ld.load(xb, P.rg, xs, 2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5, wave, lane);
+                load_row(k + 1);
+            }
+            const float* grow = gbuf + (k & 1) * CO * nwin + co * nwin;
+            const uint8_t* jrow = jbuf + (k & 1) * CO * nwin + co * nwin;
+            int r = 0, px = sidx;
+            while (px >= g.PW) {
+                px -= g.PW;
+                ++r;
+            }
+            for (int w = sidx; w < nwin; w += NS) {
+                if (py0 + r >= g.PH) break;  // uniform: the band's rows past the volume
+                const float gw = grow[w];
+                const int j = jrow[w];
+                const int dz = j >> 2, dy = (j >> 1) & 1, dx = j & 1;
+                const int inplane = ci * g.CS + (2 * r + dy) * g.YS + 2 * px + dx;
+#pragma unroll
+                for (int tz = 0; tz < 3; ++tz) {
+                    int sl = sb + dz + tz;
+                    sl = sl >= kRing ? sl - kRing : sl;
+                    const float* pp = xs + sl * SLOT + inplane;
+#pragma unroll
+                    for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+                        for (int tx = 0; tx < 3; ++tx)
+                            acc[tz * 9 + ty * 3 + tx] = fmaf(gw, pp[ty * g.YS + tx], acc[tz * 9 + ty * 3 + tx]);
+                }
+                dbacc += gw;
+                px += NS;
+                while (px >= g.PW) {
+                    px -= g.PW;
+                    ++r;
+                }
+            }
+            if (more) store_row((k + 1) & 1);
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            __syncthreads();
+            sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+        }
+    }
+    // the NS streams' partial sums through LDS (fixed order), one partial row per block
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    constexpr int NCOL = CIN * 27 + 1;
+    float* out = P.part + (size_t)blk * (CO * NCOL);
+    __syncthreads();
+    float* R = xs;
+#pragma unroll
+    for (int q = 0; q < 27; ++q) R[(sidx * L + li) * 28 + q] = acc[q];
+    R[(sidx * L + li) * 28 + 27] = dbacc;
+    __syncthreads();
+    for (int i = tid; i < L * 28; i += 512) {
+        const int l2 = i / 28, q = i - l2 * 28;
+        float v = R[i];
+#pragma unroll
+        for (int k = 1; k < NS; ++k) v += R[k * L * 28 + i];
+        const int co2 = l2 / CPG, cig2 = l2 - co2 * CPG, ci2 = (co2 / (CO / G)) * CPG + cig2;
+        if (q < 27)
+            out[co2 * NCOL + ci2 * 27 + q] = v;
+        else if (cig2 == 0)
+            out[co2 * NCOL + CIN * 27] = v;
+    }
+}
+
 // sum of the block partials -> dW [16][cin/G][27] (in-group columns) and db [16].
 // A 1024-thread block owns 64 consecutive outputs (lane = output): wave w sums
 // the partial rows k = w, w + 16, ... (4 chains, coalesced 64-float rows), the
@@ -2304,6 +2465,43 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
     return RT_OK;
 }
 
+// the sparse weight gradient: two-row bands (one-row for wide 16-channel
+// planes), one partial row per block, k_wgrad_reduce over ncol = cin*27 + 1
+template <int CIN, int G, int PYB>
+int launch_wgrad_sparse_k(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
+                          const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
+    const RingGeom rg = make_ring_geom<CIN, PYB, 1, 2>(L, B, 512);
+    const int nwin = PYB * rg.g.PW;
+    const size_t lds = std::max((size_t)kRing * rg.SLOT * 4 + (size_t)2 * CO * nwin * 5, (size_t)512 * 28 * 4);
+    if (lds > 160 * 1024 || CO * nwin > 512 * kWgSparseMaxG || (rg.npiece + 7) / 8 > ring_max_pieces<CIN, 1>())
+        return RT_ELIMIT;
+    const int gz = std::max(1, std::min<int>(B, kWgradRingBlocks / std::max(1, rg.nyb)));
+    const int nblk = rg.nyb * gz;
+    constexpr int NCOL = CIN * 27 + 1;
+    if ((int64_t)nblk * CO * NCOL > ws_floats) return rt_internal_fail(RT_EINVAL, "rt_conv_wgrad: workspace too small");
+    static bool attr = false;
+    if (!attr) {
+        if (const int rc_lds = allow_big_lds(&k_conv_wgrad_sparse<CIN, G, PYB>)) return rc_lds;
+        attr = true;
+    }
+    WgradRingParams P{x, rows, dP, am, ws, B, rg};
+    hipLaunchKernelGGL((k_conv_wgrad_sparse<CIN, G, PYB>), dim3(rg.nyb, 1, gz), dim3(512), lds, st, P);
+    const int nout = CO * (CIN / G) * 27 + CO;
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((nout + 63) / 64), dim3(64 * kRedWaves), 0, st, (const float*)ws, nblk,
+                       CIN, G, NCOL, dw, db);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+template <int CIN, int G>
+int launch_wgrad_sparse(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
+                        const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
+    int rc = launch_wgrad_sparse_k<CIN, G, 2>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+    if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 1>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+    return rc;
+}
+
 bool bad_layer(const rt_conv_layer* L) {
     if (!L) return true;
     if (!((L->cin == 4 && L->groups == 1) || (L->cin == 16 && (L->groups == 1 || L->groups == 2 || L->groups == 4))))
@@ -2391,6 +2589,23 @@ extern "C" int rt_conv_relu_pool_wgrad(const rt_conv_layer* L, int32_t batch, co
     if (bad_layer(L) || batch < 1 || !x_d || !dy_d || !argmax_d || !dw_d || !db_d || !ws_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_wgrad: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // the gather through the pooling argmax (RT_C3D_WGSPARSE=0: the dense MFMA ring kernels, A/B runs)
+    static const bool sparse = [] {
+        const char* e = std::getenv("RT_C3D_WGSPARSE");
+        return !(e && e[0] == '0');
+    }();
+    if (sparse && RT_C3D_EXP != 3) {
+        int rc = RT_ELIMIT;
+        if (L->cin == 4)
+            rc = launch_wgrad_sparse<4, 1>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+        else if (L->groups == 1)
+            rc = launch_wgrad_sparse<16, 1>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+        else if (L->groups == 2)
+            rc = launch_wgrad_sparse<16, 2>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+        else
+            rc = launch_wgrad_sparse<16, 4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+        if (rc != RT_ELIMIT) return rc;
+    }
     if (RT_C3D_EXP != 3) {
         const int rc = L->cin == 4
                            ? launch_wgrad_ring<4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st)
