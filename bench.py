@@ -435,14 +435,24 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
         train_ms += t_trn + t_wg + t_dg
     f_fwd = sum(flops)
     f_train = 2 * sum(flops) + sum(flops[1:])
+    # executed: the weight gradients gather one argmax patch per (channel,
+    # pooled window) -- 1/8 of the dense conv backward's multiply-adds, on the
+    # VALU (k_conv_wgrad_sparse); forward and data gradients are dense MFMA
+    f_exec = sum(flops) + sum(flops[1:]) + sum(flops) // 8
     return {"bound": "mfma", "workload": f"C3D extractor stages, {batch} observations at {grid[0]}^3 "
                                          "(BASELINE configs[3] rollout step), f32 MFMA",
             "peak": F32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
             "forward": {"ms": fwd_ms, "flop": f_fwd, "achieved": f_fwd / fwd_ms / 1e9,
                         "frac": f_fwd / (fwd_ms * 1e-3) / F32_MFMA_PEAK},
             "train_pass": {"ms": train_ms, "flop": f_train, "achieved": f_train / train_ms / 1e9,
-                           "frac": f_train / (train_ms * 1e-3) / F32_MFMA_PEAK},
-            "stages": stages, "timing": "HIP events on the kernels' stream, mean of 5 back-to-back launches"}
+                           "frac": f_train / (train_ms * 1e-3) / F32_MFMA_PEAK,
+                           "flop_model": "dense conv forward + weight gradient + data gradient (stages 2, 3): the "
+                                         "reference's cuDNN work",
+                           "executed_flop": f_exec, "executed_achieved": f_exec / train_ms / 1e9,
+                           "executed_frac": f_exec / (train_ms * 1e-3) / F32_MFMA_PEAK,
+                           "wgrad_form": "argmax gather, 1/8 of the dense MACs (VALU FMA, k_conv_wgrad_sparse)"},
+            "stages": stages, "stage_tflops": "dense-equivalent conv FLOPs / stage kernel time",
+            "timing": "HIP events on the kernels' stream, mean of 5 back-to-back launches"}
 
 
 def main():
