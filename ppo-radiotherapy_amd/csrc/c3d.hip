@@ -1627,9 +1627,26 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring_zs(WgradRingParams
 // the blocks by k_wgrad_reduce (deterministic).  A row's (gradient, argmax)
 // pairs of the band are loaded into registers beside the next planes' DMA and
 // written to a double-buffered LDS row after the row's gathers, so the
-// row's one wait + barrier covers both.  LDS strides: YS = 4, CS = 8, SLOT =
-// 2 (mod 32 dwords) put conv1's 4 channels x 8 argmax offsets of a half-wave
-// (8 output channels) on 32 distinct banks, ring wrap included.
+// row's one wait + barrier covers both.  The patch rows are read as two 8-B
+// pairs from the even x at or below the patch start (4 LDS cycles per 3 taps
+// instead of 6 for a dword pair + dword), strides from make_sparse_geom.
+// ring geometry of the sparse weight gradient: 8-B pair reads (ds_read_b64)
+// of even-aligned x pairs; stride residues (mod 32 dwords) from a bank model
+// of a half-wave's pair reads (4 / 8 input channels x the argmax (dz, dy)
+// variants of its output channels, the ring wrap included): conflict-free
+// with (YS, CS, SLOT) = (4, 16, 8) for conv1 and (2, 8, 4) for the
+// 16-channel stages
+template <int CIN, int PYB>
+RingGeom make_sparse_geom(const rt_conv_layer* L, int B) {
+    RingGeom r = make_ring_geom<CIN, PYB, 1>(L, B, 512);
+    Geom& g = r.g;
+    g.YS = round_mod(g.XL + 2, CIN == 4 ? 4 : 2);  // + 2: the second pair of a row may read one past XL
+    g.CS = round_mod(g.YL * g.YS, CIN == 4 ? 16 : 8);
+    r.SLOT = round_mod(CIN * g.CS, CIN == 4 ? 8 : 4);
+    r.npiece = (r.SLOT + 63) / 64;
+    return r;
+}
+
 constexpr int kWgSparseMaxG = 4;  // a band row holds <= 512 * 4 (channel, window) entries
 
 template <int CIN, int G, int PYB>
@@ -1725,18 +1742,28 @@ __global__ __launch_bounds__(512) void k_conv_wgrad_sparse(WgradRingParams P) {
                 if (py0 + r >= g.PH) break;  // uniform: the band's rows past the volume
                 const float gw = grow[w];
                 const int j = jrow[w];
-                const int dz = j >> 2, dy = (j >> 1) & 1, dx = j & 1;
-                const int inplane = ci * g.CS + (2 * r + dy) * g.YS + 2 * px + dx;
+                const int dz = j >> 2, dy = (j >> 1) & 1;
+                const bool odd = j & 1;  // dx: the patch starts at x 2px + dx, inside the pair at 2px
+                const int inplane = ci * g.CS + (2 * r + dy) * g.YS + 2 * px;
 #pragma unroll
                 for (int tz = 0; tz < 3; ++tz) {
                     int sl = sb + dz + tz;
                     sl = sl >= kRing ? sl - kRing : sl;
                     const float* pp = xs + sl * SLOT + inplane;
+                    // the second pair's address is laundered so the two 8-B reads stay two
+                    // ds_read_b64 (2 LDS cycles each): merged into one ds_read2_b64 they cost 8
+                    int o2 = sl * SLOT + inplane + 2;
+                    asm volatile("" : "+v"(o2));
+                    const float* pq = xs + o2;
 #pragma unroll
-                    for (int ty = 0; ty < 3; ++ty)
-#pragma unroll
-                        for (int tx = 0; tx < 3; ++tx)
-                            acc[tz * 9 + ty * 3 + tx] = fmaf(gw, pp[ty * g.YS + tx], acc[tz * 9 + ty * 3 + tx]);
+                    for (int ty = 0; ty < 3; ++ty) {
+                        const float2 u = *reinterpret_cast<const float2*>(pp + ty * g.YS);
+                        const float2 v = *reinterpret_cast<const float2*>(pq + ty * g.YS);
+                        const int q = tz * 9 + ty * 3;
+                        acc[q] = fmaf(gw, odd ? u.y : u.x, acc[q]);
+                        acc[q + 1] = fmaf(gw, odd ? v.x : u.y, acc[q + 1]);
+                        acc[q + 2] = fmaf(gw, odd ? v.y : v.x, acc[q + 2]);
+                    }
                 }
                 dbacc += gw;
                 px += NS;
@@ -2470,7 +2497,7 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
 template <int CIN, int G, int PYB>
 int launch_wgrad_sparse_k(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                           const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
-    const RingGeom rg = make_ring_geom<CIN, PYB, 1, 2>(L, B, 512);
+    const RingGeom rg = make_sparse_geom<CIN, PYB>(L, B);
     const int nwin = PYB * rg.g.PW;
     const size_t lds = std::max((size_t)kRing * rg.SLOT * 4 + (size_t)2 * CO * nwin * 5, (size_t)512 * 28 * 4);
     if (lds > 160 * 1024 || CO * nwin > 512 * kWgSparseMaxG || (rg.npiece + 7) / 8 > ring_max_pieces<CIN, 1>())
