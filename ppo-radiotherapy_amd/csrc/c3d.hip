@@ -473,9 +473,9 @@ RingGeom make_ring_geom(const rt_conv_layer* L, int B, int nthreads) {
 // of the block's y band, [ci][yl][xl]; lane l of wave w fills VEC floats of
 // piece w + NW*i.  Sources are clamped into the volume (out-of-volume values
 // feed masked positions only, and stay finite for the backward).
-template <int CIN, int VEC, int NW>
+template <int CIN, int VEC, int NW, int MPX = 0>
 struct RingLoader {
-    static constexpr int MP = ring_max_pieces<CIN, VEC>();
+    static constexpr int MP = MPX ? MPX : ring_max_pieces<CIN, VEC>();
     int goff[MP];              // per piece: offset within a plane of channel 0
     int npw;                   // pieces of this wave
 
@@ -1627,35 +1627,22 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring_zs(WgradRingParams
 // the blocks by k_wgrad_reduce (deterministic).  A row's (gradient, argmax)
 // pairs of the band are loaded into registers beside the next planes' DMA and
 // written to a double-buffered LDS row after the row's gathers, so the
-// row's one wait + barrier covers both.  The patch rows are read as two 8-B
-// pairs from the even x at or below the patch start (4 LDS cycles per 3 taps
-// instead of 6 for a dword pair + dword), strides from make_sparse_geom.
-// ring geometry of the sparse weight gradient: 8-B pair reads (ds_read_b64)
-// of even-aligned x pairs; stride residues (mod 32 dwords) from a bank model
-// of a half-wave's pair reads (4 / 8 input channels x the argmax (dz, dy)
-// variants of its output channels, the ring wrap included): conflict-free
-// with (YS, CS, SLOT) = (4, 16, 8) for conv1 and (2, 8, 4) for the
-// 16-channel stages
-template <int CIN, int PYB>
-RingGeom make_sparse_geom(const rt_conv_layer* L, int B) {
-    RingGeom r = make_ring_geom<CIN, PYB, 1>(L, B, 512);
-    Geom& g = r.g;
-    g.YS = round_mod(g.XL + 2, CIN == 4 ? 4 : 2);  // + 2: the second pair of a row may read one past XL
-    g.CS = round_mod(g.YL * g.YS, CIN == 4 ? 16 : 8);
-    r.SLOT = round_mod(CIN * g.CS, CIN == 4 ? 8 : 4);
-    r.npiece = (r.SLOT + 63) / 64;
-    return r;
-}
+// row's one wait + barrier covers both.  LDS strides: YS = 4, CS = 8, SLOT =
+// 2 (mod 32 dwords) put conv1's 4 channels x 8 argmax offsets of a half-wave
+// (8 output channels) on 32 distinct banks, ring wrap included.  (Reading the
+// patch rows as 8-B pairs from the even x below the patch start -- 2/3 of the
+// LDS cycles, but 27 selects and no packed FMAs -- measured slower: conv1
+// 2.45 -> 2.94 ms)
+constexpr int kWgSparseMaxG = 4;  // a band row holds <= NT * 4 (channel, window) entries
 
-constexpr int kWgSparseMaxG = 4;  // a band row holds <= 512 * 4 (channel, window) entries
-
-template <int CIN, int G, int PYB>
-__global__ __launch_bounds__(512) void k_conv_wgrad_sparse(WgradRingParams P) {
+template <int CIN, int G, int PYB, int NT>
+__global__ __launch_bounds__(NT) void k_conv_wgrad_sparse(WgradRingParams P) {
     extern __shared__ float xs[];
     constexpr int CPG = CIN / G;   // input channels per group
     constexpr int L = CO * CPG;    // threads per window
-    constexpr int NS = 512 / L;    // window streams per block
-    constexpr int NW = 8;
+    constexpr int NS = NT / L;     // window streams per block
+    constexpr int NW = NT / 64;
+    static_assert(NS >= 1, "block too small for one window");
     const Geom& g = P.rg.g;
     const int SLOT = P.rg.SLOT;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1669,7 +1656,7 @@ __global__ __launch_bounds__(512) void k_conv_wgrad_sparse(WgradRingParams P) {
     const int chan = g.PD * g.PH * g.PW;
     float* gbuf = xs + kRing * SLOT;                                   // [2][CO][nwin] gradient (0: inactive)
     uint8_t* jbuf = reinterpret_cast<uint8_t*>(gbuf + 2 * CO * nwin);  // [2][CO][nwin] argmax index
-    RingLoader<CIN, 1, NW> ld;
+    RingLoader<CIN, 1, NW, NT == 256 ? 16 : 0> ld;
     ld.init(P.rg, y0, x0, wave, lane);
     float acc[27];
 #pragma unroll
@@ -1682,7 +1669,7 @@ __global__ __launch_bounds__(512) void k_conv_wgrad_sparse(WgradRingParams P) {
     int off[MAXG];
 #pragma unroll
     for (int i = 0; i < MAXG; ++i) {
-        const int e = tid + 512 * i;
+        const int e = tid + NT * i;
         off[i] = -1;
         if (e < CO * nwin) {
             const int c2 = e / nwin, w = e - c2 * nwin, r = w / g.PW, px = w - r * g.PW, py = py0 + r;
@@ -1709,7 +1696,7 @@ __global__ __launch_bounds__(512) void k_conv_wgrad_sparse(WgradRingParams P) {
         auto store_row = [&](int buf) {
 #pragma unroll
             for (int i = 0; i < MAXG; ++i) {
-                const int e = tid + 512 * i;
+                const int e = tid + NT * i;
                 if (e < CO * nwin) {
                     gbuf[buf * CO * nwin + e] = (jv[i] & 8) ? gv[i] : 0.0f;  // inactive window (max <= 0): no gradient
                     jbuf[buf * CO * nwin + e] = (uint8_t)(jv[i] & 7);
@@ -1742,28 +1729,18 @@ __global__ __launch_bounds__(512) void k_conv_wgrad_sparse(WgradRingParams P) {
                 if (py0 + r >= g.PH) break;  // uniform: the band's rows past the volume
                 const float gw = grow[w];
                 const int j = jrow[w];
-                const int dz = j >> 2, dy = (j >> 1) & 1;
-                const bool odd = j & 1;  // dx: the patch starts at x 2px + dx, inside the pair at 2px
-                const int inplane = ci * g.CS + (2 * r + dy) * g.YS + 2 * px;
+                const int dz = j >> 2, dy = (j >> 1) & 1, dx = j & 1;
+                const int inplane = ci * g.CS + (2 * r + dy) * g.YS + 2 * px + dx;
 #pragma unroll
                 for (int tz = 0; tz < 3; ++tz) {
                     int sl = sb + dz + tz;
                     sl = sl >= kRing ? sl - kRing : sl;
                     const float* pp = xs + sl * SLOT + inplane;
-                    // the second pair's address is laundered so the two 8-B reads stay two
-                    // ds_read_b64 (2 LDS cycles each): merged into one ds_read2_b64 they cost 8
-                    int o2 = sl * SLOT + inplane + 2;
-                    asm volatile("" : "+v"(o2));
-                    const float* pq = xs + o2;
 #pragma unroll
-                    for (int ty = 0; ty < 3; ++ty) {
-                        const float2 u = *reinterpret_cast<const float2*>(pp + ty * g.YS);
-                        const float2 v = *reinterpret_cast<const float2*>(pq + ty * g.YS);
-                        const int q = tz * 9 + ty * 3;
-                        acc[q] = fmaf(gw, odd ? u.y : u.x, acc[q]);
-                        acc[q + 1] = fmaf(gw, odd ? v.x : u.y, acc[q + 1]);
-                        acc[q + 2] = fmaf(gw, odd ? v.y : v.x, acc[q + 2]);
-                    }
+                    for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+                        for (int tx = 0; tx < 3; ++tx)
+                            acc[tz * 9 + ty * 3 + tx] = fmaf(gw, pp[ty * g.YS + tx], acc[tz * 9 + ty * 3 + tx]);
                 }
                 dbacc += gw;
                 px += NS;
@@ -1788,7 +1765,7 @@ __global__ __launch_bounds__(512) void k_conv_wgrad_sparse(WgradRingParams P) {
     for (int q = 0; q < 27; ++q) R[(sidx * L + li) * 28 + q] = acc[q];
     R[(sidx * L + li) * 28 + 27] = dbacc;
     __syncthreads();
-    for (int i = tid; i < L * 28; i += 512) {
+    for (int i = tid; i < L * 28; i += NT) {
         const int l2 = i / 28, q = i - l2 * 28;
         float v = R[i];
 #pragma unroll
@@ -2494,25 +2471,26 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
 
 // the sparse weight gradient: two-row bands (one-row for wide 16-channel
 // planes), one partial row per block, k_wgrad_reduce over ncol = cin*27 + 1
-template <int CIN, int G, int PYB>
+template <int CIN, int G, int PYB, int NT>
 int launch_wgrad_sparse_k(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                           const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
-    const RingGeom rg = make_sparse_geom<CIN, PYB>(L, B);
+    const RingGeom rg = make_ring_geom<CIN, PYB, 1, 2>(L, B, NT);
     const int nwin = PYB * rg.g.PW;
-    const size_t lds = std::max((size_t)kRing * rg.SLOT * 4 + (size_t)2 * CO * nwin * 5, (size_t)512 * 28 * 4);
-    if (lds > 160 * 1024 || CO * nwin > 512 * kWgSparseMaxG || (rg.npiece + 7) / 8 > ring_max_pieces<CIN, 1>())
+    const size_t lds = std::max((size_t)kRing * rg.SLOT * 4 + (size_t)2 * CO * nwin * 5, (size_t)NT * 28 * 4);
+    if (lds > 160 * 1024 || CO * nwin > NT * kWgSparseMaxG ||
+        (rg.npiece + NT / 64 - 1) / (NT / 64) > (NT == 256 ? 16 : ring_max_pieces<CIN, 1>()))
         return RT_ELIMIT;
-    const int gz = std::max(1, std::min<int>(B, kWgradRingBlocks / std::max(1, rg.nyb)));
+    const int gz = std::max(1, std::min<int>(B, kWgradRingBlocks * (512 / NT) / std::max(1, rg.nyb)));
     const int nblk = rg.nyb * gz;
     constexpr int NCOL = CIN * 27 + 1;
     if ((int64_t)nblk * CO * NCOL > ws_floats) return rt_internal_fail(RT_EINVAL, "rt_conv_wgrad: workspace too small");
     static bool attr = false;
     if (!attr) {
-        if (const int rc_lds = allow_big_lds(&k_conv_wgrad_sparse<CIN, G, PYB>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_wgrad_sparse<CIN, G, PYB, NT>)) return rc_lds;
         attr = true;
     }
     WgradRingParams P{x, rows, dP, am, ws, B, rg};
-    hipLaunchKernelGGL((k_conv_wgrad_sparse<CIN, G, PYB>), dim3(rg.nyb, 1, gz), dim3(512), lds, st, P);
+    hipLaunchKernelGGL((k_conv_wgrad_sparse<CIN, G, PYB, NT>), dim3(rg.nyb, 1, gz), dim3(NT), lds, st, P);
     const int nout = CO * (CIN / G) * 27 + CO;
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((nout + 63) / 64), dim3(64 * kRedWaves), 0, st, (const float*)ws, nblk,
                        CIN, G, NCOL, dw, db);
@@ -2521,11 +2499,25 @@ int launch_wgrad_sparse_k(const rt_conv_layer* L, int32_t B, const float* x, con
     return RT_OK;
 }
 
+// RT_WGS_NT (A/B runs): 512- or 256-thread blocks of the sparse weight gradient
 template <int CIN, int G>
 int launch_wgrad_sparse(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                         const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
-    int rc = launch_wgrad_sparse_k<CIN, G, 2>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
-    if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 1>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+    static const int nt = [] {
+        const char* e = std::getenv("RT_WGS_NT");
+        return e && std::atoi(e) == 512 ? 512 : 256;
+    }();
+    static const int pyb1 = [] {  // RT_WGS_PYB=1 (A/B runs): one-row bands first
+        const char* e = std::getenv("RT_WGS_PYB");
+        return e && e[0] == '1';
+    }();
+    int rc = RT_ELIMIT;
+    if (nt == 256) {
+        if (!pyb1) rc = launch_wgrad_sparse_k<CIN, G, 2, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+        if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 1, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+    }
+    if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 2, 512>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+    if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 1, 512>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
     return rc;
 }
 
@@ -2607,7 +2599,8 @@ extern "C" int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* L, int32_
     // ring: at most kWgradRingBlocks partial rows (one per block); the tile
     // kernel (fallback for planes too wide for the ring) may need more
     const int64_t ring = (int64_t)kWgradRingBlocks * CO * (L->cin == 4 ? wg_nct<4>() : wg_nct<16>()) * 16;
-    return std::max(ring, wgrad_tile_ws(L, batch));
+    const int64_t sparse = (int64_t)2 * kWgradRingBlocks * CO * (L->cin * 27 + 1);  // 256-thread blocks: 2x the rows
+    return std::max(std::max(ring, sparse), wgrad_tile_ws(L, batch));
 }
 
 extern "C" int rt_conv_relu_pool_wgrad(const rt_conv_layer* L, int32_t batch, const float* x_d, const int64_t* rows_d,
