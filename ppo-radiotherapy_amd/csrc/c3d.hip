@@ -1634,6 +1634,9 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring_zs(WgradRingParams
 // LDS cycles, but 27 selects and no packed FMAs -- measured slower: conv1
 // 2.45 -> 2.94 ms)
 constexpr int kWgSparseMaxG = 4;  // a band row holds <= NT * 4 (channel, window) entries
+#ifndef RT_WGS_U
+#define RT_WGS_U 1  // windows per loop iteration of k_conv_wgrad_sparse (2: A/B builds)
+#endif
 
 template <int CIN, int G, int PYB, int NT>
 __global__ __launch_bounds__(NT) void k_conv_wgrad_sparse(WgradRingParams P) {
@@ -1720,34 +1723,68 @@ __global__ __launch_bounds__(NT) void k_conv_wgrad_sparse(WgradRingParams P) {
             }
             const float* grow = gbuf + (k & 1) * CO * nwin + co * nwin;
             const uint8_t* jrow = jbuf + (k & 1) * CO * nwin + co * nwin;
-            int r = 0, px = sidx;
-            while (px >= g.PW) {
-                px -= g.PW;
-                ++r;
+            // ring slots of the row's planes 2k + 0..3 (the patch of argmax dz uses dz .. dz + 2)
+            int so[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int sl = sb + t;
+                so[t] = (sl >= kRing ? sl - kRing : sl) * SLOT + ci * g.CS;
             }
-            for (int w = sidx; w < nwin; w += NS) {
-                if (py0 + r >= g.PH) break;  // uniform: the band's rows past the volume
+            // one window: its 27 patch values (registers) and its gradient
+            auto gather = [&](int w, int r, int px, float (&v)[27]) {
                 const float gw = grow[w];
                 const int j = jrow[w];
                 const int dz = j >> 2, dy = (j >> 1) & 1, dx = j & 1;
-                const int inplane = ci * g.CS + (2 * r + dy) * g.YS + 2 * px + dx;
+                const int inrow = (2 * r + dy) * g.YS + 2 * px + dx;
+                const int zb[3] = {(dz ? so[1] : so[0]) + inrow, (dz ? so[2] : so[1]) + inrow,
+                                   (dz ? so[3] : so[2]) + inrow};
 #pragma unroll
-                for (int tz = 0; tz < 3; ++tz) {
-                    int sl = sb + dz + tz;
-                    sl = sl >= kRing ? sl - kRing : sl;
-                    const float* pp = xs + sl * SLOT + inplane;
+                for (int tz = 0; tz < 3; ++tz)
 #pragma unroll
                     for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-                        for (int tx = 0; tx < 3; ++tx)
-                            acc[tz * 9 + ty * 3 + tx] = fmaf(gw, pp[ty * g.YS + tx], acc[tz * 9 + ty * 3 + tx]);
-                }
+                        for (int tx = 0; tx < 3; ++tx) v[tz * 9 + ty * 3 + tx] = xs[zb[tz] + ty * g.YS + tx];
+                return gw;
+            };
+            auto accumulate = [&](float gw, const float (&v)[27]) {
+#pragma unroll
+                for (int q = 0; q < 27; ++q) acc[q] = fmaf(gw, v[q], acc[q]);
                 dbacc += gw;
+            };
+            auto advance = [&](int& r, int& px) {
                 px += NS;
                 while (px >= g.PW) {
                     px -= g.PW;
                     ++r;
                 }
+            };
+            int r = 0, px = sidx, w = sidx;
+            while (px >= g.PW) {
+                px -= g.PW;
+                ++r;
+            }
+#if RT_WGS_U == 2
+            // two windows per iteration: both gathers in flight before the FMAs
+            for (; w + NS < nwin && py0 + r < g.PH; w += 2 * NS) {
+                int r2 = r, px2 = px;
+                advance(r2, px2);
+                float va[27], vb[27];
+                const float ga = gather(w, r, px, va);
+                const bool second = py0 + r2 < g.PH;  // uniform
+                const float gb = second ? gather(w + NS, r2, px2, vb) : 0.0f;
+                accumulate(ga, va);
+                if (second) accumulate(gb, vb);
+                r = r2;
+                px = px2;
+                advance(r, px);
+            }
+#endif
+            for (; w < nwin; w += NS) {
+                if (py0 + r >= g.PH) break;  // uniform: the band's rows past the volume
+                float v[27];
+                const float gw = gather(w, r, px, v);
+                accumulate(gw, v);
+                advance(r, px);
             }
             if (more) store_row((k + 1) & 1);
             __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -2507,14 +2544,15 @@ int launch_wgrad_sparse(const rt_conv_layer* L, int32_t B, const float* x, const
         const char* e = std::getenv("RT_WGS_NT");
         return e && std::atoi(e) == 512 ? 512 : 256;
     }();
-    static const int pyb1 = [] {  // RT_WGS_PYB=1 (A/B runs): one-row bands first
+    static const int pyb2 = [] {  // RT_WGS_PYB=2 (A/B runs): two-row bands first (measured slower at 256 threads)
         const char* e = std::getenv("RT_WGS_PYB");
-        return e && e[0] == '1';
+        return e && e[0] == '2';
     }();
     int rc = RT_ELIMIT;
     if (nt == 256) {
-        if (!pyb1) rc = launch_wgrad_sparse_k<CIN, G, 2, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+        if (pyb2) rc = launch_wgrad_sparse_k<CIN, G, 2, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
         if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 1, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+        if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 2, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
     }
     if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 2, 512>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
     if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 1, 512>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
