@@ -1001,6 +1001,18 @@ int launch_fwd_ring(const rt_conv_layer* L, int32_t B, const float* x, const int
                rg.g.W >= vec;
     };
     constexpr int PY_BIG = CIN == 4 ? 4 : 2;
+    if constexpr (CIN == 4) {
+        // RT_C3D_FWD_NTH=256 (A/B runs): 4-wave blocks on 2-row bands (4 blocks per CU)
+        static const bool small = [] {
+            const char* e = std::getenv("RT_C3D_FWD_NTH");
+            return e && std::atoi(e) == 256;
+        }();
+        if (small && vec4) {
+            const RingGeom rg = make_ring_geom<CIN, 2, 4>(L, B, 256);
+            if ((size_t)kRing * rg.SLOT * sizeof(float) <= 40 * 1024 && (rg.npiece + 3) / 4 <= ring_max_pieces<CIN, 4>())
+                return launch_ring<CIN, G, 2, 4, 256>(rg, B, x, rows, w, bias, y, amax, st);
+        }
+    }
     for (const size_t budget : {(size_t)(CIN == 4 ? 80 : 160) * 1024, (size_t)160 * 1024}) {
         if constexpr (CIN == 4) {
             if (vec4) {
@@ -1633,6 +1645,24 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring_zs(WgradRingParams
 // patch rows as 8-B pairs from the even x below the patch start -- 2/3 of the
 // LDS cycles, but 27 selects and no packed FMAs -- measured slower: conv1
 // 2.45 -> 2.94 ms)
+// ring geometry of the sparse weight gradient: conv1 keeps the ring's (YS,
+// CS, SLOT) = (4, 8, 2) residues (mod 32 dwords; conflict-free for its lane
+// map), the 16-channel stages take (2, 4, 0) -- a bank model of their
+// half-waves (4 output channels x 8 input channels for groups = 2) over random
+// argmax variants: 1.54 vs 2.0 mean multiplicity (PMC: 48 % conflict cycles)
+template <int CIN, int PYB, int NT>
+RingGeom make_sparse_geom(const rt_conv_layer* L, int B) {
+    RingGeom r = make_ring_geom<CIN, PYB, 1, 2>(L, B, NT);
+    if constexpr (CIN == 16) {
+        Geom& g = r.g;
+        g.YS = round_mod(g.XL, 2);
+        g.CS = round_mod(g.YL * g.YS, 4);
+        r.SLOT = round_mod(CIN * g.CS, 0);
+        r.npiece = (r.SLOT + 63) / 64;
+    }
+    return r;
+}
+
 constexpr int kWgSparseMaxG = 4;  // a band row holds <= NT * 4 (channel, window) entries
 #ifndef RT_WGS_U
 #define RT_WGS_U 1  // windows per loop iteration of k_conv_wgrad_sparse (2: A/B builds)
@@ -2511,7 +2541,7 @@ int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const i
 template <int CIN, int G, int PYB, int NT>
 int launch_wgrad_sparse_k(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                           const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
-    const RingGeom rg = make_ring_geom<CIN, PYB, 1, 2>(L, B, NT);
+    const RingGeom rg = make_sparse_geom<CIN, PYB, NT>(L, B);
     const int nwin = PYB * rg.g.PW;
     const size_t lds = std::max((size_t)kRing * rg.SLOT * 4 + (size_t)2 * CO * nwin * 5, (size_t)NT * 28 * 4);
     if (lds > 160 * 1024 || CO * nwin > NT * kWgSparseMaxG ||

@@ -35,17 +35,24 @@ for k, cs in vals.items():
     row["kernel_ms"] = t * 1e3 if t else None
     if t and "GRBM_GUI_ACTIVE" in m:
         row["clock_GHz"] = m["GRBM_GUI_ACTIVE"] / 8 / t / 1e9
-    if "SQ_INSTS_MFMA" in m:
+    if "SQ_INSTS_MFMA" in m and m["SQ_INSTS_MFMA"] > 0:
         mf = m["SQ_INSTS_MFMA"]
         row["valu_per_mfma"] = (m["SQ_INSTS_VALU"] - mf) / mf
         row["salu_per_mfma"] = m["SQ_INSTS_SALU"] / mf
         if t and "clock_GHz" in row:
             row["mfma_busy_frac"] = 32 * mf / (1024 * t * row["clock_GHz"] * 1e9)
+    if t and "clock_GHz" in row and "SQ_LDS_IDX_ACTIVE" in m:
+        # LDS-array cycles over the CU-cycles of the kernel (256 CUs)
+        row["lds_active_frac"] = m["SQ_LDS_IDX_ACTIVE"] / (256 * t * row["clock_GHz"] * 1e9)
+        if "SQ_LDS_BANK_CONFLICT" in m:
+            row["lds_conflict_frac"] = m["SQ_LDS_BANK_CONFLICT"] / max(m["SQ_LDS_IDX_ACTIVE"], 1)
+    if t and "clock_GHz" in row and "SQ_INSTS_VALU" in m:
+        row["valu_insts_per_cu_cycle"] = m["SQ_INSTS_VALU"] / (256 * t * row["clock_GHz"] * 1e9)
     out[k] = row
     print(f"{k[:60]:60s} ms {row['kernel_ms'] or 0:7.3f} clk {row.get('clock_GHz', 0):5.2f} "
           f"mfma_busy {row.get('mfma_busy_frac', 0):5.3f} valu/mfma {row.get('valu_per_mfma', 0):5.2f} "
           f"salu/mfma {row.get('salu_per_mfma', 0):5.2f} wait_inst {m.get('SQ_WAIT_INST_ANY', 0) / max(m.get('SQ_WAVE_CYCLES', 1), 1):5.2f} "
           f"wait_any {m.get('SQ_WAIT_ANY', 0) / max(m.get('SQ_WAVE_CYCLES', 1), 1):5.2f}")
 if len(sys.argv) > 2:
-    json.dump({"source": "tools/archive/gpu_c3d_pmc.sh over tools/c3d_pmc_driver.py (batch 64, 64^3 stage shapes)",
+    json.dump({"source": "tools/gpu_r03_s9.sh (or tools/archive/gpu_c3d_pmc.sh) over tools/c3d_pmc_driver.py (batch C3D_PMC_B, 64^3 stage shapes)",
                "kernels": out}, open(sys.argv[2], "w"), indent=1)
