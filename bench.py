@@ -115,6 +115,8 @@ def parse():
                          "0 = one persistent launch with a per-env dense pass)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
+    ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="f32",
+                    help="the fused update's 64x64 layer products (ppo_update_ms); the other is timed beside it")
     ap.add_argument("--rehearse-same-device", action="store_true",
                     help="multi-rank rehearsal on one GPU: every rank on cuda:0, gloo instead of RCCL")
     a = ap.parse_args()
@@ -136,7 +138,7 @@ def trainer_cfg(a):
     return SimpleNamespace(num_steps=a.num_steps, num_minibatches=a.num_minibatches, update_epochs=a.update_epochs,
                            learning_rate=3e-4, anneal_lr=False, gamma=0.99, gae_lambda=0.95, norm_adv=True,
                            clip_coef=0.1, clip_vloss=True, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
-                           micro_batch=a.micro_batch)
+                           micro_batch=a.micro_batch, update_precision=a.update_precision)
 
 
 def cpu_baseline(seconds: float):
@@ -469,7 +471,7 @@ def main():
     import torch.distributed as dist
 
     import _rtpkg  # noqa: F401
-    from ppo_radiotherapy_amd import assets
+    from ppo_radiotherapy_amd import _lib, assets
     from ppo_radiotherapy_amd.networks import PPO, PPO_3DCNN
     from ppo_radiotherapy_amd.ppo import PPOTrainer, broadcast_parameters
     from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
@@ -628,9 +630,25 @@ def main():
             # MLP forward + backward of both heads: 28,224 MACs per sample
             # (DESIGN.md §3); whole minibatch step (grad + reduce + clip/Adam + epoch overheads)
             fl = 2 * UPDATE_MACS_PER_SAMPLE * tr.minibatch_size
+            upd["update_precision"] = a.update_precision
             upd["update_mfma"] = {"bound": "mfma", "flop_per_minibatch": fl,
                                   "achieved": fl / (du / n_upd) / 1e12, "peak": F32_MFMA_PEAK / 1e12,
-                                  "unit": "TFLOP/s", "frac": fl / (du / n_upd) / F32_MFMA_PEAK}
+                                  "unit": "TFLOP/s", "frac": fl / (du / n_upd) / F32_MFMA_PEAK,
+                                  "peak_note": "f32 MFMA peak (the f32-equivalent rate, also for bf16x3)"}
+            # the other precision of the 64x64 layer products, same update (parameters move on)
+            other = "bf16x3" if a.update_precision == "f32" else "f32"
+            keep = tr._update_prec
+            tr._update_prec = _lib.PPO_PREC[other]
+            tr.update()  # warm (first launch of the other kernel instantiation)
+            torch.cuda.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            n2 = tr.update()
+            torch.cuda.synchronize()
+            barrier()
+            d2 = max_over_ranks(time.perf_counter() - t0)
+            tr._update_prec = keep
+            upd[f"ppo_update_ms_{other}"] = 1000 * d2 / n2
 
     # ---------------- roofline of the dominant kernel, k_dense
     V = int(np.prod(grid))

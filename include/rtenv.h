@@ -331,6 +331,19 @@ int64_t rt_ppo_workspace_floats(int32_t minibatch_size);
 /* Parameters of the fused agent (10,061). */
 int32_t rt_ppo_num_params(void);
 
+/* Arithmetic of the two 64x64 layer products in rt_ppo_grad / rt_ppo_update
+ * (forward and data gradient; process-wide, initially RT_PPO_PREC=f32|bf16x3
+ * from the environment, else f32).  F32: exact f32 MFMA, the reference's
+ * arithmetic (torch f32 Linear, TF32 off: train.py:200-238 via networks.py).
+ * BF16X3: each f32 operand split into bf16 hi + lo, products hi*hi + hi*lo +
+ * lo*hi accumulated in f32 (relative error <= ~2^-15 per product); the same
+ * f64-autograd gates hold (tests/test_gpu_trainer.py).  RT_EINVAL on another
+ * value. */
+#define RT_PPO_PREC_F32 0
+#define RT_PPO_PREC_BF16X3 1
+int rt_ppo_set_precision(int32_t prec);
+int32_t rt_ppo_get_precision(void);
+
 /* Gradient of the minibatch PPO loss (train.py:200-238: clipped surrogate,
  * [clipped] value loss * vf_coef, - ent_coef * entropy; advantages normalised
  * with adv_stats_d when norm_adv) w.r.t. the 13 parameter tensors (order of

@@ -401,8 +401,19 @@ constexpr int SCR = 136;  // scratch rows per wave: A 0..63, B 64..127, GM^T 128
 constexpr int IN_OBS = 0, IN_ACT = 144, IN_LOGP = 240, IN_ADV = 256, IN_RET = 144, IN_VAL = 160, IN_FLOATS = 272;
 constexpr int kMaxGradBlocks = 256;
 
+// bf16x3 mode (kPrecBf16x3): each W2 as two bf16 images, hi = the upper 16
+// bits of the f32 value and lo = bf16(value - hi), rows = output unit j,
+// columns = input unit i at wpos(i) (the k order of the 16x16x32 operand
+// fragments, below).  80-element rows (128 B + 32 B pad): the ds_read_b128
+// row reads are conflict-free, the ds_read_b64_tr_b16 column reads 2-way.
+constexpr int WBP = 80;
+constexpr int kPrecF32 = 0, kPrecBf16x3 = 1;
+
 struct MfmaLds {
-    float w2[2][H * WP];
+    union {
+        float w2[2][H * WP];           // kPrecF32
+        uint16_t w2b[2][2][H * WBP];   // kPrecBf16x3: [head][hi, lo]
+    };
     float w1[2][H * W1P];
     float b2[2][H];
     float w3[7 * H];  // rows 0..5 actor_mean.4, row 6 critic.4
@@ -429,6 +440,73 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// ---- bf16x3 operands --------------------------------------------------------
+// x = hi + lo + e with hi the truncated upper half of x, lo = bf16(x - hi)
+// (x - hi is exact), |e| <= 2^-17 |x|; a product is hi*hi + hi*lo + lo*hi in
+// three v_mfma_f32_16x16x32_bf16 (f32 accumulate), dropping lo*lo: relative
+// error <= ~2^-15 per product against exact f32's 2^-24, at 3/16 of the f32
+// MFMA's cycles per flop (MI355X_MICROARCH.md cycle constants: 16 cycles per
+// 16x16x32 bf16, 32 per 16x16x4 f32).
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf_trunc(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
+// (hi(a), hi(b)) packed, a in the low half
+__device__ __forceinline__ uint32_t bf_hi2(float a, float b) {
+    return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+__device__ __forceinline__ uint32_t bf_lo2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a - bf_trunc(a), b - bf_trunc(b)}, b2v));
+}
+
+// The k order of a 64-long contraction in two 16x16x32 steps s: element e of
+// lane group g is unit u(s,g,e) = 16(2s + e/4) + 4g + e%4, so that a
+// transposed tile in MFMA accumulator layout (lane (c,g) holds rows 4g+r of
+// 16-row tile J) is the B operand with no lane movement: elements 0..3 =
+// tile 2s, rows 4g..4g+3; 4..7 = tile 2s+1.  wpos(u) = 32s + 8g + e puts a
+// lane's 8 elements of a W2 row next to each other.
+__device__ __forceinline__ int wpos(int u) {
+    return (u & 32) | (((u >> 2) & 3) << 3) | (((u >> 4) & 1) << 2) | (u & 3);
+}
+
+__device__ __forceinline__ void split_frag(const f4 v[4], int s, bf8& hi, bf8& lo) {
+    u4v h, l;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int J = 2 * s + (d >> 1), r = 2 * (d & 1);
+        h[d] = bf_hi2(v[J][r], v[J][r + 1]);
+        l[d] = bf_lo2(v[J][r], v[J][r + 1]);
+    }
+    hi = __builtin_bit_cast(bf8, h);
+    lo = __builtin_bit_cast(bf8, l);
+}
+
+__device__ __forceinline__ f4 mfma3(bf8 ah, bf8 al, bf8 bh, bf8 bl, f4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+
+// A operand W2[16J + c][u(s,g,.)] of image img: one 16-B row read
+__device__ __forceinline__ bf8 w2_row_frag(const uint16_t* img, int J, int s, int c, int g) {
+    return *reinterpret_cast<const bf8*>(img + (16 * J + c) * WBP + 32 * s + 8 * g);
+}
+
+// A operand W2^T[16I + c][u(s,g,.)] = W2[u(s,g,e)][16I + c]: two transposed
+// reads (ds_read_b64_tr_b16, 4 rows x 16 columns per 16-lane group; lane
+// 4q+p of the group addresses row q, columns 16I+4p..+3).  EXEC must be full.
+typedef __attribute__((address_space(3))) s4v* lds_s4_t;
+__device__ __forceinline__ bf8 w2_col_frag(const uint16_t* img, int I, int s, int c, int g) {
+    const int q = c >> 2, p = c & 3;
+    const uint16_t* a = img + (32 * s + 4 * g + q) * WBP + 32 * (I >> 1) + 8 * p + 4 * (I & 1);
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(a));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(a + 16 * WBP));
+    return __builtin_bit_cast(bf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
 __device__ __forceinline__ float el(const float4& v, int r) { return r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w; }
 
 // tanh(x) = 1 - 2 / (exp(2x) + 1) on v_exp_f32 + v_rcp_f32 (1 ulp each; the
@@ -487,13 +565,50 @@ __device__ __forceinline__ void mf_prefetch(const GradParams& P, float* in, int 
     }
 }
 
+// ---- bf16x3 dW2: the sum over the tile's 16 samples in v_mfma_f32_16x16x16_bf16
+// (lane l: A[l&15][k = 4(l>>4) + j], B[k][l&15]).  G2^T and H1^T go through
+// [sample][unit] bf16 images (hi at img, lo at img + IMG_FL; rows of IMG_RS
+// elements = 136 B: the lanes' 8-B stores conflict-free, the transposed reads
+// 2-way) and come back as 4-sample fragments by ds_read_b64_tr_b16.
+constexpr int IMG_RS = 68, IMG_FL = 16 * IMG_RS;
+static_assert(2 * IMG_FL * 2 <= 64 * SP * 4, "an image pair fits a 64-row scratch region");
+
+// lane (c,g) stores units 4g..4g+3 of tiles 2s, 2s+1 of sample c: the packed
+// dwords split_frag made (dwords 0,1: tile 2s; 2,3: tile 2s+1)
+__device__ __forceinline__ void put_img(uint16_t* img, const bf8 hi[2], const bf8 lo[2], int c, int g) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const u4v h = __builtin_bit_cast(u4v, hi[s]), l = __builtin_bit_cast(u4v, lo[s]);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            uint16_t* a = img + c * IMG_RS + 16 * (2 * s + half) + 4 * g;
+            *reinterpret_cast<uint2*>(a) = make_uint2(h[2 * half], h[2 * half + 1]);
+            *reinterpret_cast<uint2*>(a + IMG_FL) = make_uint2(l[2 * half], l[2 * half + 1]);
+        }
+    }
+}
+
+// X^T[16J + c][samples 4g..4g+3] from X's [sample][unit] image (16-lane group
+// g: lane 4q+p addresses sample 4g+q, units 16J+4p..+3; lane i receives unit 16J+i)
+__device__ __forceinline__ s4v img_frag(const uint16_t* img, int J, int c, int g) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(img + (4 * g + (c >> 2)) * IMG_RS + 16 * J + 4 * (c & 3)));
+}
+
+__device__ __forceinline__ f4 mfma3k16(s4v ah, s4v al, s4v bh, s4v bl, f4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, c, 0, 0, 0);
+}
+
 // X^T of the augmented first layer (row NOBS = the bias input 1, rows above 0)
 __device__ __forceinline__ float xin(const float* in, int row, int smp) {
     return row < NOBS ? in[IN_OBS + row * 16 + smp] : (row == NOBS ? 1.0f : 0.0f);
 }
 
 // forward of this wave's trunk for its tile: h1, h2 = tanh layers, transposed tiles
-__device__ __forceinline__ void mf_fwd(const MfmaLds& S, int h, const float* in, int c, int g, f4 h1[4], f4 h2[4]) {
+template <int PREC>
+__device__ __forceinline__ void mf_fwd(const MfmaLds& S, int h, const float* in, int c, int g, f4 h1[4], f4 h2[4],
+                                       uint16_t* img_h1) {
 #pragma clang fp contract(fast)
     float xb[3];
 #pragma unroll
@@ -505,6 +620,24 @@ __device__ __forceinline__ void mf_fwd(const MfmaLds& S, int h, const float* in,
         for (int q = 0; q < 3; ++q) z = mfma4(S.w1[h][(16 * J + c) * W1P + 4 * q + g], xb[q], z);
 #pragma unroll
         for (int r = 0; r < 4; ++r) h1[J][r] = tanh_fast(z[r]);
+    }
+    if constexpr (PREC == kPrecBf16x3) {
+        bf8 bh[2], bl[2];
+        split_frag(h1, 0, bh[0], bl[0]);
+        split_frag(h1, 1, bh[1], bl[1]);
+        put_img(img_h1, bh, bl, c, g);  // dW2's H1 operand (read after later wave_syncs)
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {
+            f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                z = mfma3(w2_row_frag(S.w2b[h][0], J, s, c, g), w2_row_frag(S.w2b[h][1], J, s, c, g), bh[s], bl[s],
+                          z);
+            const float4 b = ld4(&S.b2[h][16 * J + 4 * g]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h2[J][r] = tanh_fast(z[r] + el(b, r));
+        }
+        return;
     }
 #pragma unroll
     for (int J = 0; J < 4; ++J) {
@@ -726,6 +859,40 @@ __device__ __forceinline__ void ph_g1(const MfmaLds& S, const f4 g2[4], const f4
     }
 }
 
+// bf16x3 G1: the B operand G2^T split once (gh, gl; also the dW2 image)
+template <int HEAD>
+__device__ __forceinline__ void ph_g1_b(const MfmaLds& S, const bf8 gh[2], const bf8 gl[2], const f4 h1[4], int c,
+                                        int g, f4 g1[4]) {
+    RT_FP_FAST
+#pragma unroll
+    for (int I = 0; I < 4; ++I) {
+        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            z = mfma3(w2_col_frag(S.w2b[HEAD][0], I, s, c, g), w2_col_frag(S.w2b[HEAD][1], I, s, c, g), gh[s], gl[s],
+                      z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g1[I][r] = z[r] * (1.0f - h1[I][r] * h1[I][r]);
+    }
+}
+
+// dW2 += G2^T . H1 over the tile's samples; acc.d2[J][T] as in ph_dw2
+template <int HEAD>
+__device__ __forceinline__ void ph_dw2_b(const uint16_t* ig, const uint16_t* ih, int c, int g, Acc<HEAD>& acc) {
+    s4v ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+        ah[J] = img_frag(ig, J, c, g);
+        al[J] = img_frag(ig + IMG_FL, J, c, g);
+        bh[J] = img_frag(ih, J, c, g);
+        bl[J] = img_frag(ih + IMG_FL, J, c, g);
+    }
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+        for (int T = 0; T < 4; ++T) acc.d2[J][T] = mfma3k16(ah[J], al[J], bh[T], bl[T], acc.d2[J][T]);
+}
+
 // [dW1 | db1] += G1^T . [X | 1]   (G1^T in A)
 template <int HEAD>
 __device__ __forceinline__ void ph_dw1(const float* A, const float xd[4], int c, int g, Acc<HEAD>& acc) {
@@ -745,7 +912,7 @@ __device__ __forceinline__ void load_xd(const float* in, int c, int g, float xd[
     for (int k = 0; k < 4; ++k) xd[k] = xin(in, c, 4 * g + k);
 }
 
-template <int HEAD>
+template <int HEAD, int PREC>
 __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, float* A, float* Bs, float* in,
                                         float* GMs, int c, int g, int t, int t_next, float inv_n, Acc<HEAD>& acc) {
     constexpr int NOUT = HEAD == 0 ? NACT : 1;
@@ -753,7 +920,10 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
     __builtin_amdgcn_s_waitcnt(0);  // this tile's inputs (LDS DMA issued during the previous tile) have landed
     wave_sync();  // ... and the previous tile's reads of the scratch are done
     f4 h1[4], h2[4];
-    mf_fwd(S, HEAD, in, c, g, h1, h2);
+    // bf16x3: the H1 images over B, the G2 images over A once dW3 is done with it
+    uint16_t* const img_h1 = reinterpret_cast<uint16_t*>(Bs);
+    uint16_t* const img_g2 = reinterpret_cast<uint16_t*>(A);
+    mf_fwd<PREC>(S, HEAD, in, c, g, h1, h2, img_h1);
     float xd[4];  // read now: `in` is refilled below
     load_xd(in, c, g, xd);
     float go[NOUT];
@@ -770,20 +940,31 @@ __device__ __forceinline__ void mf_tile(const MfmaLds& S, const GradParams& P, f
     ph_dw3<HEAD>(A, GMs, h2, go, c, g, acc);
     f4 g2[4];
     ph_g2<HEAD>(S, go, h2, g, acc, g2);
-    wave_sync();
-    ph_put(A, g2, c, g);
-    ph_put(Bs, h1, c, g);
-    wave_sync();
-    ph_dw2<HEAD>(A, Bs, c, g, acc);
     f4 g1[4];
-    ph_g1<HEAD>(S, g2, h1, c, g, g1);
+    if constexpr (PREC == kPrecBf16x3) {
+        bf8 gh[2], gl[2];
+        split_frag(g2, 0, gh[0], gl[0]);
+        split_frag(g2, 1, gh[1], gl[1]);
+        if constexpr (HEAD == 0) wave_sync();  // dW3's reads of A are done
+        put_img(img_g2, gh, gl, c, g);
+        wave_sync();
+        ph_dw2_b<HEAD>(img_g2, img_h1, c, g, acc);
+        ph_g1_b<HEAD>(S, gh, gl, h1, c, g, g1);
+    } else {
+        wave_sync();
+        ph_put(A, g2, c, g);
+        ph_put(Bs, h1, c, g);
+        wave_sync();
+        ph_dw2<HEAD>(A, Bs, c, g, acc);
+        ph_g1<HEAD>(S, g2, h1, c, g, g1);
+    }
     wave_sync();
     ph_put(A, g1, c, g);
     wave_sync();
     ph_dw1<HEAD>(A, xd, c, g, acc);
 }
 
-template <int HEAD>
+template <int HEAD, int PREC>
 __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pair, int lane) {
     const int c = lane & 15, g = lane >> 4;
     float* A = S.scr[2 * pair + HEAD];
@@ -809,7 +990,7 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
     int nt_done = 0;
     const int tstep = gridDim.x * NPAIR;
     for (int t = blockIdx.x * NPAIR + pair; t < ntiles; t += tstep) {
-        mf_tile<HEAD>(S, P, A, Bs, in, GMs, c, g, t, t + tstep < ntiles ? t + tstep : -1, inv_n, acc);
+        mf_tile<HEAD, PREC>(S, P, A, Bs, in, GMs, c, g, t, t + tstep < ntiles ? t + tstep : -1, inv_n, acc);
         if (lane == 0 && nt_done++ == 0) RT_STAMP(tw, 6);
     }
     if (lane == 0) RT_STAMP(tw, 2);
@@ -898,6 +1079,7 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
     if (lane == 0) RT_STAMP(tw, 5);
 }
 
+template <int PREC>
 __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
     __shared__ __attribute__((aligned(16))) MfmaLds S;
     const int tid = threadIdx.x;
@@ -907,10 +1089,12 @@ __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
     // ~10 times: 4.8 us per launch)
     constexpr int NW2 = H * H / MT, NW1 = (H * W1P + MT - 1) / MT;
     float w2v[2][NW2], w1v[2][NW1];
+    // f32: element tid + MT u; bf16x3: the pair 2 (tid + MT u'), u' < NW2 / 2
 #pragma unroll
     for (int u = 0; u < NW2; ++u) {
-        w2v[0][u] = P.w.p[2][tid + MT * u];
-        w2v[1][u] = P.w.p[9][tid + MT * u];
+        const int f = PREC == kPrecF32 ? tid + MT * u : 2 * (tid + MT * (u >> 1)) + (u & 1);
+        w2v[0][u] = P.w.p[2][f];
+        w2v[1][u] = P.w.p[9][f];
     }
 #pragma unroll
     for (int u = 0; u < NW1; ++u) {
@@ -943,11 +1127,23 @@ __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
                 mf_prefetch<0>(P, S.in[2 * pair], t0, tid & 63);
         }
     }
+    if constexpr (PREC == kPrecF32) {
 #pragma unroll
-    for (int u = 0; u < NW2; ++u) {
-        const int i = tid + MT * u;
-        S.w2[0][(i >> 6) * WP + (i & 63)] = w2v[0][u];
-        S.w2[1][(i >> 6) * WP + (i & 63)] = w2v[1][u];
+        for (int u = 0; u < NW2; ++u) {
+            const int i = tid + MT * u;
+            S.w2[0][(i >> 6) * WP + (i & 63)] = w2v[0][u];
+            S.w2[1][(i >> 6) * WP + (i & 63)] = w2v[1][u];
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < NW2; u += 2) {
+            const int f = 2 * (tid + MT * (u >> 1)), o = (f >> 6) * WBP + wpos(f & 63);  // wpos(i + 1) = wpos(i) + 1
+#pragma unroll
+            for (int hd = 0; hd < 2; ++hd) {
+                *reinterpret_cast<uint32_t*>(&S.w2b[hd][0][o]) = bf_hi2(w2v[hd][u], w2v[hd][u + 1]);
+                *reinterpret_cast<uint32_t*>(&S.w2b[hd][1][o]) = bf_lo2(w2v[hd][u], w2v[hd][u + 1]);
+            }
+        }
     }
 #pragma unroll
     for (int u = 0; u < NW1; ++u) {
@@ -981,9 +1177,9 @@ __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
     // older wave, which wins VALU arbitration (MI355X_MICROARCH.md, two waves
     // per SIMD).  (wave & 1 as the role put both actors of two pairs on one SIMD.)
     if (wave >= 4)
-        mf_wave<1>(S, P, wave & 3, lane);
+        mf_wave<1, PREC>(S, P, wave & 3, lane);
     else
-        mf_wave<0>(S, P, wave & 3, lane);
+        mf_wave<0, PREC>(S, P, wave & 3, lane);
 }
 
 int grad_blocks(int mb) {
@@ -1387,6 +1583,13 @@ bool rt_ppo_use_mfma() {
     return v != 0;
 }
 
+// Arithmetic of k_ppo_grad_mfma's two 64x64 products (rt_ppo_set_precision;
+// the initial value from RT_PPO_PREC=f32|bf16x3, default f32)
+int g_ppo_prec = [] {
+    const char* e = std::getenv("RT_PPO_PREC");
+    return (e && std::strcmp(e, "bf16x3") == 0) ? kPrecBf16x3 : kPrecF32;
+}();
+
 // RT_PPO_FUSED_ADAM=1: rt_ppo_update launches k_ppo_reduce_adam instead of
 // k_ppo_reduce + k_adam -- bitwise the same update, measured slower (13.1 us
 // vs 5.1 + 5.6: the last block's Adam over all 10,061 parameters is
@@ -1439,8 +1642,10 @@ int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const r
     G.clip_vloss = hp->clip_vloss;
     G.vf_coef = hp->vf_coef;
     G.ws = ws_d;
-    if (use_mfma)
-        hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblk), dim3(MT), 0, st, G);
+    if (use_mfma && g_ppo_prec == kPrecBf16x3)
+        hipLaunchKernelGGL(k_ppo_grad_mfma<kPrecBf16x3>, dim3(nblk), dim3(MT), 0, st, G);
+    else if (use_mfma)
+        hipLaunchKernelGGL(k_ppo_grad_mfma<kPrecF32>, dim3(nblk), dim3(MT), 0, st, G);
     else
         hipLaunchKernelGGL(k_ppo_grad, dim3(nblk), dim3(kThreads), 0, st, G);
     R = reduce_params(grads_d, mb, hp, ws_d, ws_floats, stats_d, accum_d);
@@ -1508,6 +1713,17 @@ extern "C" int64_t rt_ppo_workspace_floats(int32_t minibatch_size) {
 }
 
 extern "C" int32_t rt_ppo_num_params(void) { return NP; }
+
+extern "C" int rt_ppo_set_precision(int32_t prec) {
+    if (prec != RT_PPO_PREC_F32 && prec != RT_PPO_PREC_BF16X3)
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_set_precision: unknown precision");
+    g_ppo_prec = prec == RT_PPO_PREC_BF16X3 ? kPrecBf16x3 : kPrecF32;
+    return RT_OK;
+}
+
+extern "C" int32_t rt_ppo_get_precision(void) {
+    return g_ppo_prec == kPrecBf16x3 ? RT_PPO_PREC_BF16X3 : RT_PPO_PREC_F32;
+}
 
 extern "C" int rt_ppo_grad(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
                            const int64_t* mb_idx_d, int32_t mb_size, const float* adv_stats_d,

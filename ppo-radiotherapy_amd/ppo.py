@@ -131,6 +131,12 @@ class PPOTrainer:
             self._adam_step = 0
             self._ppo_stats = torch.zeros(6, **kw)
             self._ppo_accum = torch.zeros(6, **kw)
+            # arithmetic of the fused grad kernel's 64x64 products: "f32" (the
+            # reference's) or "bf16x3" (rt_ppo_set_precision, include/rtenv.h)
+            prec = str(getattr(cfg, "update_precision", "f32"))
+            if prec not in _lib.PPO_PREC:
+                raise ValueError(f"update_precision {prec!r}: expected one of {sorted(_lib.PPO_PREC)}")
+            self._update_prec = _lib.PPO_PREC[prec]
         # one flat gradient bucket; every param.grad is a view of it
         self.flat_grad = torch.zeros(n, dtype=self.params[0].dtype, **kw)
         off = 0
@@ -497,6 +503,7 @@ class PPOTrainer:
         bucket between rt_ppo_grad and rt_adam_step)."""
         self._bind_batch()
         L = _lib.load()
+        _lib.check(L.rt_ppo_set_precision(self._update_prec), "rt_ppo_set_precision")  # process-wide: set per call
         stream = _lib.stream_handle()
         batch = self._batch_struct()
         hp = ctypes.byref(self._hp)

@@ -173,3 +173,19 @@ def test_fast_sincos_matches_plain_double_double(tmp_path):
                     os.path.join(REPO, "tools", "check_sincos.cpp"), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe), "1000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
+
+
+def test_ppo_precision_switch():
+    """rt_ppo_set_precision: the two RT_PPO_PREC_* values round-trip, anything
+    else is RT_EINVAL and leaves the setting alone (host-only, no launch)."""
+    L = _lib.load()
+    before = L.rt_ppo_get_precision()
+    try:
+        for name, v in _lib.PPO_PREC.items():
+            assert L.rt_ppo_set_precision(v) == 0, name
+            assert L.rt_ppo_get_precision() == v
+        assert L.rt_ppo_set_precision(7) == -1
+        assert b"precision" in L.rt_last_error()
+        assert L.rt_ppo_get_precision() == _lib.PPO_PREC["bf16x3"]
+    finally:
+        L.rt_ppo_set_precision(before)

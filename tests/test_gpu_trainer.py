@@ -19,7 +19,7 @@ def _cfg(**kw):
     return SimpleNamespace(**c)
 
 
-def _make(fused=False):
+def _make(fused=False, prec="f32"):
     from fake_env import FakeVecEnv, torch_gae
 
     from ppo_radiotherapy_amd.networks import PPO
@@ -31,23 +31,26 @@ def _make(fused=False):
     torch.manual_seed(0)
     agent = PPO((9,), (6,), 64).to(dev)
     gen = torch.Generator(device=dev).manual_seed(5)
-    tr = PPOTrainer(_cfg(fused_update=fused), FakeVecEnv(256), agent, dev, generator=gen, gae_fn=torch_gae)
+    tr = PPOTrainer(_cfg(fused_update=fused, update_precision=prec), FakeVecEnv(256), agent, dev, generator=gen,
+                    gae_fn=torch_gae)
     g = torch.Generator(device="cpu").manual_seed(1)
     for t in (tr.obs, tr.actions, tr.logprobs, tr.advantages, tr.returns, tr.values):
         t.copy_(torch.randn(t.shape, generator=g))
     return tr
 
 
-@pytest.mark.parametrize("fused", [False, True], ids=["torch", "fused"])
-def test_update_matches_float64_reference(fused):
-    """The eager torch update and the fused HIP update vs a CPU float64 run of
-    the same minibatches (2 iterations x 3 epochs x 4 minibatches)."""
+@pytest.mark.parametrize("fused,prec", [(False, "f32"), (True, "f32"), (True, "bf16x3")],
+                         ids=["torch", "fused", "fused-bf16x3"])
+def test_update_matches_float64_reference(fused, prec):
+    """The eager torch update and the fused HIP update (f32 and bf16x3 layer
+    products, same tolerances) vs a CPU float64 run of the same minibatches
+    (2 iterations x 3 epochs x 4 minibatches)."""
     from fake_env import FakeVecEnv, torch_gae
 
     from ppo_radiotherapy_amd.networks import PPO
     from ppo_radiotherapy_amd.ppo import PPOTrainer
 
-    e = _make(fused)
+    e = _make(fused, prec)
     assert e.fused_update == fused
     rec = []
     orig = torch.randperm
@@ -95,10 +98,12 @@ def _policy_ptrs(agent, grads=False):
     return (ctypes.c_void_p * 13)(*[t.data_ptr() for t in ts]), ts
 
 
+@pytest.mark.parametrize("prec", ["f32", "bf16x3"])
 @pytest.mark.parametrize("mb,clip_vloss,norm_adv,ent", [(4096, 1, 1, 0.0), (3001, 1, 0, 0.01), (77, 0, 1, 0.0)])
-def test_fused_grad_matches_autograd(mb, clip_vloss, norm_adv, ent):
+def test_fused_grad_matches_autograd(mb, clip_vloss, norm_adv, ent, prec):
     """rt_ppo_grad vs float64 autograd of train.py:200-238 on one minibatch
-    (ragged sizes: partial last tile; ratios spread across both clip edges)."""
+    (ragged sizes: partial last tile; ratios spread across both clip edges),
+    with the 64x64 layer products in f32 and in bf16x3 (same 2e-4 gate)."""
     import ctypes
 
     from ppo_radiotherapy_amd import _lib
@@ -136,9 +141,15 @@ def test_fused_grad_matches_autograd(mb, clip_vloss, norm_adv, ent):
     ws = torch.empty(int(L.rt_ppo_workspace_floats(mb)), device=dev)
     st = torch.zeros(6, device=dev)
     acc = torch.ones(6, device=dev)
-    _lib.check(L.rt_ppo_grad(pp, gp, ctypes.byref(batch), idx.data_ptr(), mb, stats2.data_ptr(), ctypes.byref(hp),
-                             ws.data_ptr(), ws.numel(), st.data_ptr(), acc.data_ptr(), None), "rt_ppo_grad")
-    torch.cuda.synchronize()
+    _lib.check(L.rt_ppo_set_precision(_lib.PPO_PREC[prec]), "rt_ppo_set_precision")
+    assert L.rt_ppo_get_precision() == _lib.PPO_PREC[prec]
+    try:
+        _lib.check(L.rt_ppo_grad(pp, gp, ctypes.byref(batch), idx.data_ptr(), mb, stats2.data_ptr(),
+                                 ctypes.byref(hp), ws.data_ptr(), ws.numel(), st.data_ptr(), acc.data_ptr(), None),
+                   "rt_ppo_grad")
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(L.rt_ppo_set_precision(_lib.PPO_PREC["f32"]), "rt_ppo_set_precision")
     # float64 autograd reference (ppo.PPOTrainer._loss_backward, the reference's formulas)
     ref = PPO((9,), (6,), 64).double()
     ref.load_state_dict({k: v.double().cpu() for k, v in agent.state_dict().items()})
