@@ -22,6 +22,11 @@ Also reported:
   train_env_steps_per_s  env steps/s of a full PPO iteration
                          (64 rollout steps + GAE + 80 updates)
   update_mfma            the fused update (rt_ppo_update) vs the f32 MFMA peak
+  update_precision       the 64x64 layer products of that update: bf16x3
+                         (--update-precision, default; split-operand bf16 MFMA,
+                         the f64 gates of tests/test_gpu_trainer.py hold) or
+                         f32 (the reference's arithmetic); ppo_update_ms_<other>
+                         times the other one on the same update
   other_step_mode        the same rollout + iteration with the other env step
                          formulation (incremental, SURVEY §8 f-2: bitwise-equal
                          rewards/termination, touches only the beam's voxels)
@@ -115,7 +120,7 @@ def parse():
                          "0 = one persistent launch with a per-env dense pass)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
-    ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="f32",
+    ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="bf16x3",
                     help="the fused update's 64x64 layer products (ppo_update_ms); the other is timed beside it")
     ap.add_argument("--rehearse-same-device", action="store_true",
                     help="multi-rank rehearsal on one GPU: every rank on cuda:0, gloo instead of RCCL")

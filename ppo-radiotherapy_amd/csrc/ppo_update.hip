@@ -401,8 +401,8 @@ constexpr int SCR = 136;  // scratch rows per wave: A 0..63, B 64..127, GM^T 128
 constexpr int IN_OBS = 0, IN_ACT = 144, IN_LOGP = 240, IN_ADV = 256, IN_RET = 144, IN_VAL = 160, IN_FLOATS = 272;
 constexpr int kMaxGradBlocks = 256;
 
-// bf16x3 mode (kPrecBf16x3): each W2 as two bf16 images, hi = the upper 16
-// bits of the f32 value and lo = bf16(value - hi), rows = output unit j,
+// bf16x3 mode (kPrecBf16x3): each W2 as two bf16 images, hi = bf16(value)
+// and lo = bf16(value - hi), rows = output unit j,
 // columns = input unit i at wpos(i) (the k order of the 16x16x32 operand
 // fragments, below).  80-element rows (128 B + 32 B pad): the ds_read_b128
 // row reads are conflict-free, the ds_read_b64_tr_b16 column reads 2-way.
@@ -442,25 +442,23 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // ---- bf16x3 operands --------------------------------------------------------
-// x = hi + lo + e with hi the truncated upper half of x, lo = bf16(x - hi)
-// (x - hi is exact), |e| <= 2^-17 |x|; a product is hi*hi + hi*lo + lo*hi in
-// three v_mfma_f32_16x16x32_bf16 (f32 accumulate), dropping lo*lo: relative
-// error <= ~2^-15 per product against exact f32's 2^-24, at 3/16 of the f32
-// MFMA's cycles per flop (MI355X_MICROARCH.md cycle constants: 16 cycles per
-// 16x16x32 bf16, 32 per 16x16x4 f32).
+// x = hi + lo + e with hi = bf16(x), lo = bf16(x - hi) (both round to nearest
+// even; x - hi is exact), |lo| <= 2^-8 |x|, |e| <= 2^-17 |x|; a product is
+// hi*hi + hi*lo + lo*hi in three bf16 MFMAs (f32 accumulate), dropping lo*lo:
+// relative error <= ~2^-15 per product against exact f32's 2^-24, at 3/16 of
+// the f32 MFMA's cycles per flop (MI355X_MICROARCH.md cycle constants: 16
+// cycles per 16x16x32 bf16, 32 per 16x16x4 f32).
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef __bf16 b2v __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ float bf_trunc(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
-// (hi(a), hi(b)) packed, a in the low half
-__device__ __forceinline__ uint32_t bf_hi2(float a, float b) {
-    return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
-}
-__device__ __forceinline__ uint32_t bf_lo2(float a, float b) {
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a - bf_trunc(a), b - bf_trunc(b)}, b2v));
+// (hi(a), hi(b)) and (lo(a), lo(b)) packed, a in the low halves
+__device__ __forceinline__ void bf_split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
+    const float ha = __uint_as_float(hi << 16), hb = __uint_as_float(hi & 0xFFFF0000u);
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a - ha, b - hb}, b2v));
 }
 
 // The k order of a 64-long contraction in two 16x16x32 steps s: element e of
@@ -478,8 +476,10 @@ __device__ __forceinline__ void split_frag(const f4 v[4], int s, bf8& hi, bf8& l
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int J = 2 * s + (d >> 1), r = 2 * (d & 1);
-        h[d] = bf_hi2(v[J][r], v[J][r + 1]);
-        l[d] = bf_lo2(v[J][r], v[J][r + 1]);
+        uint32_t hh, ll;
+        bf_split2(v[J][r], v[J][r + 1], hh, ll);
+        h[d] = hh;
+        l[d] = ll;
     }
     hi = __builtin_bit_cast(bf8, h);
     lo = __builtin_bit_cast(bf8, l);
@@ -1140,8 +1140,10 @@ __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
             const int f = 2 * (tid + MT * (u >> 1)), o = (f >> 6) * WBP + wpos(f & 63);  // wpos(i + 1) = wpos(i) + 1
 #pragma unroll
             for (int hd = 0; hd < 2; ++hd) {
-                *reinterpret_cast<uint32_t*>(&S.w2b[hd][0][o]) = bf_hi2(w2v[hd][u], w2v[hd][u + 1]);
-                *reinterpret_cast<uint32_t*>(&S.w2b[hd][1][o]) = bf_lo2(w2v[hd][u], w2v[hd][u + 1]);
+                uint32_t hh, ll;
+                bf_split2(w2v[hd][u], w2v[hd][u + 1], hh, ll);
+                *reinterpret_cast<uint32_t*>(&S.w2b[hd][0][o]) = hh;
+                *reinterpret_cast<uint32_t*>(&S.w2b[hd][1][o]) = ll;
             }
         }
     }
