@@ -118,6 +118,9 @@ def parse():
     ap.add_argument("--rollout-groups", type=int, default=2, choices=[0, 1, 2, 3, 4],
                     help="dense mode: env groups of the rollout call (2 = two pipelined streams, "
                          "0 = one persistent launch with a per-env dense pass)")
+    ap.add_argument("--dense-handoff", type=int, default=0, choices=[0, 1],
+                    help="dense pipelined rollout: 0 = a k_dense launch per group turn (events), "
+                         "1 = one k_dense_rollout launch per call gated by device hand-off words")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
     ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="bf16x3",
@@ -508,6 +511,8 @@ def main():
                              env_id_base=rank * a.envs, step_mode=a.step_mode)
     if not a.vision and a.step_mode == "dense":
         env.set_rollout_groups(a.rollout_groups)
+        if a.rollout_groups > 1:
+            env.set_dense_handoff(a.dense_handoff)
     torch.manual_seed(a.seed)
     if a.vision:
         agent = PPO_3DCNN((4, *grid), (6,), 64).to(dev)
@@ -667,8 +672,17 @@ def main():
         bytes_model = ("20 B x V x envs (k_dense_vis: dose read, the four observation channels written -- "
                        "lungs and dose, tumour and beam-view zeroed for k_finish's scatter)")
     persistent_dense = (not a.vision and not a.env_only and a.step_mode == "dense" and a.rollout_groups == 0)
+    dev_handoff = (not a.vision and not a.env_only and a.step_mode == "dense" and a.rollout_groups > 1
+                   and a.dense_handoff == 1)
     launches = max(kcalls, 1) / K  # launches per step (2: pipelined env groups; 1/K: one persistent launch)
-    if persistent_dense:
+    if dev_handoff:
+        # one k_dense_rollout launch per rollout call streams every group's
+        # turn of every step: its whole duration (hand-off waits included)
+        # against the lung segments of all envs and steps of the call
+        dense_ms = kms["k_dense"]
+        kernel_name = "k_dense_rollout"
+        traffic = load_pmc(grid, a.envs, "k_dense_rollout")
+    elif persistent_dense:
         # one k_rollout_policy<dense> launch per rollout call: each wave streams
         # its env's lung segment every step (dense_env); its whole duration is
         # in the first interval, and its bytes are the dense stream's
@@ -800,6 +814,8 @@ def main():
         out["steady_state"] = steady
     out["step_mode"] = a.step_mode
     out["rollout_groups"] = a.rollout_groups if a.step_mode == "dense" and not a.vision else 1
+    out["dense_handoff"] = "device" if (a.step_mode == "dense" and not a.vision and a.rollout_groups > 1
+                                        and a.dense_handoff == 1) else "events"
     if other is not None:
         out["other_step_mode"] = other
     out["roofline"] = roof

@@ -295,6 +295,20 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* 
  * returns RT_ELIMIT only when the per-wave LDS region cannot hold even the
  * policy's activations. */
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
+/* How the pipelined dense rollout (groups >= 2) hands the dose stream from
+ * one env group's turn to the next: 0 (default) = one persistent k_dense launch
+ * per group and step, turns ordered by events; 1 = device hand-off: ONE
+ * k_dense_rollout launch per rt_env_rollout_policy call streams every group's
+ * turn of every step on a library dose stream, gated by hand-off words that
+ * the group streams write after each policy/march kernel
+ * (hipStreamWriteValue64) and publishing per-turn completion counts the
+ * groups' k_finish launches wait on (hipStreamWaitValue64).  Same bits as
+ * mode 0.  A hand-off wait that exceeds 0.2 s (a stream operation that never
+ * arrived) makes the launch drain and the next rollout call return
+ * RT_EDEVICE.  RT_EINVAL for a handle without the pipelined rollout (vision,
+ * incremental or C-order dose rows).  The first call with 1 creates the dose
+ * stream -- a setup call, not graph-capturable. */
+int rt_env_set_dense_handoff(rt_env* env, int32_t mode);
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */

@@ -692,9 +692,14 @@ __device__ __forceinline__ float4 load_nt(const float4* p) {
 }
 
 // RESET envs' rows are zeroed by zero_reset_share, not by their slices.
+// XFER (k_dense_rollout): the env's mode is read with an L1-bypassing
+// non-temporal load (the same block re-reads it every phase, after another
+// kernel rewrote it) and the partials are stored `sc1` (write-through), so the
+// hand-off needs no acquire or release fence (MI355X_MICROARCH.md valid forms).
+template <bool XFER = false>
 __device__ __forceinline__ void dense_item(const DenseParams& P, int sl, int e) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int mode = P.st.setup[e].mode;
+    const int mode = XFER ? __builtin_nontemporal_load(&P.st.setup[e].mode) : P.st.setup[e].mode;
     if (mode != MODE_STEP) return;
     const float4* d4 = reinterpret_cast<const float4*>(P.st.dose + (size_t)e * P.G.Vpad);
     const int n = P.lung_n;
@@ -742,8 +747,13 @@ __device__ __forceinline__ void dense_item(const DenseParams& P, int sl, int e) 
             c += s_cnt[w];
             t += s_sum[w];
         }
-        P.part_cnt[(size_t)e * P.slices + sl] = c;
-        P.part_sum[(size_t)e * P.slices + sl] = t;
+        if (XFER) {
+            __hip_atomic_store(P.part_cnt + (size_t)e * P.slices + sl, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(P.part_sum + (size_t)e * P.slices + sl, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            P.part_cnt[(size_t)e * P.slices + sl] = c;
+            P.part_sum[(size_t)e * P.slices + sl] = t;
+        }
     }
     __syncthreads();  // s_cnt / s_sum are reused by the next item of a persistent block
 }
@@ -779,15 +789,17 @@ constexpr int kZeroBlocks = 256;  // grid k_dense: blocks that zero RESET rows (
 
 // zero_reset_share: part `part` of n_parts of the zeroing of the RESET rows
 // among envs [e_begin, e_begin + n_env) (reset_dose, environment.py:104).
-__device__ void zero_reset_share(const DenseParams& P, int n_env, int part, int n_parts) {
+// XFER: modes by non-temporal loads, zeros by `sc1` 16-B stores (see dense_item)
+template <bool XFER = false>
+__device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, int part, int n_parts) {
     __shared__ int s_w[kStepThreads / 64];
     __shared__ int s_env;
     const int tid = threadIdx.x;
     const int per = (n_env + kStepThreads - 1) / kStepThreads;
     const int a0 = min(tid * per, n_env), a1 = min(a0 + per, n_env);
-    const uint8_t* mb = P.st.mode_b + P.e_begin;
+    const uint8_t* mb = P.st.mode_b + e_begin;
     int c = 0;
-    for (int e = a0; e < a1; ++e) c += mb[e] == MODE_RESET;
+    for (int e = a0; e < a1; ++e) c += (XFER ? __builtin_nontemporal_load(mb + e) : mb[e]) == MODE_RESET;
     int R;
     const int pre = block_excl_scan(c, s_w, &R);
     if (R == 0) return;  // block-uniform
@@ -800,8 +812,8 @@ __device__ void zero_reset_share(const DenseParams& P, int n_env, int part, int 
         if (r >= pre && r < pre + c) {  // this thread's env range holds reset rank r
             int k = (int)(r - pre);
             for (int e = a0; e < a1; ++e) {
-                if (mb[e] == MODE_RESET && k-- == 0) {
-                    s_env = P.e_begin + e;
+                if ((XFER ? __builtin_nontemporal_load(mb + e) : mb[e]) == MODE_RESET && k-- == 0) {
+                    s_env = e_begin + e;
                     break;
                 }
             }
@@ -813,7 +825,12 @@ __device__ void zero_reset_share(const DenseParams& P, int n_env, int part, int 
         typedef float nf4 __attribute__((ext_vector_type(4)));
         nf4* d4 = reinterpret_cast<nf4*>(P.st.dose + (size_t)e * P.G.Vpad);
         const nf4 z = {0.f, 0.f, 0.f, 0.f};
-        for (int64_t q = q0 + tid; q < q1; q += kStepThreads) __builtin_nontemporal_store(z, d4 + q);
+        if (XFER) {
+            for (int64_t q = q0 + tid; q < q1; q += kStepThreads)
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(d4 + q), "v"(z) : "memory");
+        } else {
+            for (int64_t q = q0 + tid; q < q1; q += kStepThreads) __builtin_nontemporal_store(z, d4 + q);
+        }
     }
 }
 
@@ -823,7 +840,7 @@ __device__ void zero_reset_share(const DenseParams& P, int n_env, int part, int 
 // a block dispatched near the end of the grid set the launch's tail.)
 __global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env, int zero_rows) {
     if ((int)blockIdx.y < zero_rows) {
-        zero_reset_share(P, n_env, blockIdx.y * gridDim.x + blockIdx.x, zero_rows * gridDim.x);
+        zero_reset_share(P, P.e_begin, n_env, blockIdx.y * gridDim.x + blockIdx.x, zero_rows * gridDim.x);
         return;
     }
     dense_item(P, blockIdx.x, P.e_begin + blockIdx.y - zero_rows);
@@ -838,7 +855,89 @@ __global__ __launch_bounds__(256) void k_dense_persist(DenseParams P, int n_env)
     const int n_items = n_env * P.slices;
     for (int it = blockIdx.x; it < n_items; it += gridDim.x)
         dense_item(P, it % P.slices, P.e_begin + it / P.slices);
-    zero_reset_share(P, n_env, blockIdx.x, gridDim.x);
+    zero_reset_share(P, P.e_begin, n_env, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------
+// Device hand-off of the pipelined dense rollout (rt_env_set_dense_handoff 1):
+// ONE launch streams every group's lung segments for every step of the
+// rollout call, phase (t, g) after phase (t, g - 1), so the dose stream has no
+// kernel boundary, ramp or tail between the groups' turns.  Group g's
+// policy/march kernel of step t is followed on its stream by a stream write
+// beam_seq[g] = beam_base[g] + t + 1; a block polls that word (one lane, `sc1`
+// loads, s_sleep) before its share of the phase, streams its items and zeroes
+// its share of the RESET rows, then publishes: every wave vmcnt(0) -> barrier
+// -> one agent atomic add on done_cnt[g].  No fences: everything the block
+// reads that another kernel wrote since its last phase bypasses L1 (the
+// mode bytes and the dose rows by non-temporal loads), and everything the
+// finish kernel reads is stored `sc1` (write-through), the first valid form
+// of MI355X_MICROARCH.md's hand-off table.  (With an acquire and a release
+// fence per block and phase -- 1536 L2 write-backs per phase -- the step took
+// 0.45 ms instead of 0.28.)  Group g's k_finish of step t waits on its stream
+// for done_cnt[g] >= done_base[g] + grid * (t + 1) (hipStreamWaitValue64).
+// No block ever waits on another block, only on host-stream work ordered
+// before it; a wait longer than timeout_ticks (a stream op that never came)
+// sets *err and the block stops waiting, so the launch always drains.
+// ---------------------------------------------------------------------------
+constexpr int kMaxRolloutGroups = 4;
+
+struct DenseRolloutParams {
+    DenseParams P;                       // e_begin set per phase
+    int32_t bounds[kMaxRolloutGroups + 1];
+    int32_t G, n_steps;
+    uint64_t* beam_seq;                  // [G], 128-B apart (stride 16 words)
+    uint64_t* done_cnt;                  // [G], 128-B apart
+    uint64_t beam_base[kMaxRolloutGroups];
+    uint32_t* err;                       // host-visible, sticky
+    uint64_t timeout_ticks;              // s_memrealtime ticks (100 MHz)
+};
+
+constexpr int kSeqStride = 16;  // uint64 words between two groups' hand-off words (one 128-B line each)
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(56))) void k_dense_rollout(DenseRolloutParams R0) {
+    bool waiting = true;  // lane 0 of the block: false after a timeout
+    const int n_phases = R0.n_steps * R0.G;
+    for (int p = 0; p < n_phases; ++p) {
+            // the parameters through a laundered kernarg pointer, per phase:
+            // kept live across the loops they took 106 SGPRs, and 6 blocks per
+            // CU at 128 SGPRs a wave left no SGPRs for the policy kernel's
+            // waves, which the blocks wait on (MI355X_MICROARCH.md residency:
+            // 800 SGPRs per SIMD)
+            typedef const __attribute__((address_space(4))) DenseRolloutParams* KPtr;
+            KPtr ap = (KPtr)(__builtin_amdgcn_kernarg_segment_ptr());
+            asm volatile("" : "+s"(ap));
+            const DenseRolloutParams& R = *(const DenseRolloutParams*)ap;
+            const int t = p / R.G, g = p - t * R.G;
+            if (threadIdx.x == 0) {
+                const uint64_t want = R.beam_base[g] + (uint64_t)t + 1;
+                uint64_t* w = R.beam_seq + g * kSeqStride;
+                if (waiting && __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                        __builtin_amdgcn_s_sleep(4);
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > R.timeout_ticks) {
+                            __hip_atomic_store(R.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            waiting = false;
+                            break;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            const int e_begin = R.bounds[g];
+            const int n_env = R.bounds[g + 1] - e_begin;
+            const int slices = R.P.slices;
+            const int n_items = n_env * slices;
+            for (int it = blockIdx.x; it < n_items; it += gridDim.x)
+                dense_item<true>(R.P, it % slices, e_begin + it / slices);
+            zero_reset_share<true>(R.P, e_begin, n_env, blockIdx.x, gridDim.x);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __hip_atomic_fetch_add(R.done_cnt + g * kSeqStride, (uint64_t)1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
 }
 
 // Store 4 consecutive voxels [v0, v0+4) of one obs channel row.
@@ -1738,8 +1837,6 @@ struct PlanBuilder {
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
-constexpr int kMaxRolloutGroups = 4;
-
 struct rt_env {
     int device = 0;
     int N = 0;
@@ -1786,6 +1883,17 @@ struct rt_env {
     int rollout_groups = 2;  // DESIGN.md §3 "Pipelined dense rollout"
     hipStream_t pipe[kMaxRolloutGroups] = {};
     hipEvent_t pev[1 + 2 * kMaxRolloutGroups] = {};  // fork, dense[G], join[G]
+    // device hand-off (rt_env_set_dense_handoff 1): the dose stream (own
+    // hardware queue: a CU-masked stream is never pooled), the hand-off words
+    // (beam_seq[g], done_cnt[g], monotonic across calls) and the host's next
+    // bases, the sticky timeout flag (host pinned)
+    int dense_handoff = 0;
+    hipStream_t dstream = nullptr;
+    hipEvent_t dev_ev[2] = {};           // dose stream's join, spare
+    uint64_t* seq_d = nullptr;           // beam_seq at [g * kSeqStride], done_cnt at [(kMaxRolloutGroups + g) * kSeqStride]
+    uint64_t beam_next[kMaxRolloutGroups] = {};
+    uint64_t done_next[kMaxRolloutGroups] = {};
+    uint32_t* err_h = nullptr;
     std::vector<void*> allocs;
 };
 
@@ -1819,6 +1927,10 @@ void free_env(rt_env* env) {
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t q : env->pipe)
         if (q) (void)hipStreamDestroy(q);
+    for (hipEvent_t e : env->dev_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (env->dstream) (void)hipStreamDestroy(env->dstream);
+    if (env->err_h) (void)hipHostFree(env->err_h);
     for (void* p : env->allocs) (void)hipFree(p);
     (void)hipSetDevice(cur);
     delete env;
@@ -2269,6 +2381,20 @@ int allow_lds(const void* kernel, bool& raised) {
     return RT_OK;
 }
 
+// k_finish of envs [e0, e1)
+int launch_finish(rt_env* env, float* obs, float* reward, uint8_t* term, float* info, hipStream_t stream, int e0,
+                  int e1) {
+    FinishParams fp = finish_params(env, obs, reward, term, info);
+    fp.e_begin = e0;
+    fp.N = e1;
+    static bool big_lds = false;
+    if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_finish), big_lds)) return rc_lds;
+    hipLaunchKernelGGL(k_finish, dim3((e1 - e0 + fp.wpb - 1) / fp.wpb), dim3(64 * fp.wpb), env->finish_smem, stream,
+                       fp);
+    RT_LAUNCH_CHECK("k_finish");
+    return RT_OK;
+}
+
 // k_dense / k_dense_vis (skipped in incremental mode) then k_finish
 // envs [e0, e1) (e1 < 0: all).  wait_ev: k_dense starts after it (the other
 // env group's k_dense of the pipelined rollout); done_ev: recorded after k_dense.
@@ -2308,13 +2434,7 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
     }
     if (done_ev) RT_HIP(hipEventRecord(done_ev, stream));
     if (ev) (void)hipEventRecord(ev[2], stream);
-    FinishParams fp = finish_params(env, obs, reward, term, info);
-    fp.e_begin = e0;
-    fp.N = e1;
-    static bool big_lds = false;
-    if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_finish), big_lds)) return rc_lds;
-    hipLaunchKernelGGL(k_finish, dim3((n + fp.wpb - 1) / fp.wpb), dim3(64 * fp.wpb), env->finish_smem, stream, fp);
-    RT_LAUNCH_CHECK("k_finish");
+    if (const int rc = launch_finish(env, obs, reward, term, info, stream, e0, e1)) return rc;
     if (ev) (void)hipEventRecord(ev[3], stream);
     return RT_OK;
 }
@@ -2443,6 +2563,40 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
         return !(v && v[0] == '0');
     }();
     const size_t Nn = (size_t)N;
+    const bool dev = piped && env->dense_handoff;
+    DenseRolloutParams R{};
+    if (dev) {
+        // the whole call's dose stream: one k_dense_rollout launch on the
+        // dose stream, before any group's work is queued (it only waits on
+        // words the group streams write later)
+        if (*(volatile uint32_t*)env->err_h)
+            return fail(RT_EDEVICE, "rt_env_rollout_policy: a device hand-off wait timed out in an earlier call");
+        R.P.G = env->G;
+        R.P.lung_thr = env->C.lung_thr;
+        R.P.st = env->st;
+        R.P.lung_bits = env->lib.lung_bits;
+        R.P.part_cnt = env->part_cnt;
+        R.P.part_sum = env->part_sum;
+        R.P.slices = env->slices;
+        R.P.vec_per_slice = env->vec_per_slice;
+        R.P.lung_n = env->lung_n;
+        for (int g = 0; g <= G; ++g) R.bounds[g] = bounds[g];
+        R.G = G;
+        R.n_steps = r->n_steps;
+        R.beam_seq = env->seq_d;
+        R.done_cnt = env->seq_d + kMaxRolloutGroups * kSeqStride;
+        for (int g = 0; g < G; ++g) R.beam_base[g] = env->beam_next[g];
+        R.err = env->err_h;
+        R.timeout_ticks = 20000000;  // 0.2 s at 100 MHz
+        RT_HIP(hipStreamWaitEvent(env->dstream, env->pev[0], 0));
+        hipEvent_t* ev = next_timing_slot(env);
+        if (ev) (void)hipEventRecord(ev[0], env->dstream), (void)hipEventRecord(ev[1], env->dstream);
+        hipLaunchKernelGGL(k_dense_rollout, dim3(env->pipe_dense_bpc * env->num_cu), dim3(kStepThreads), 0,
+                           env->dstream, R);
+        RT_LAUNCH_CHECK("k_dense_rollout");
+        if (ev) (void)hipEventRecord(ev[2], env->dstream), (void)hipEventRecord(ev[3], env->dstream);
+    }
+    const uint64_t grid_dense = (uint64_t)env->pipe_dense_bpc * env->num_cu;
     for (int t = 0; t < r->n_steps; ++t) {
         Q.obs_in = t == 0 ? ps->obs_in : obs_d;
         Q.done_in = t == 0 ? ps->done_in : terminated_d;
@@ -2456,7 +2610,7 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
         float* info = r->info_store ? r->info_store + (size_t)t * Nn * RT_INFO_W : nullptr;
         for (int g = 0; g < G; ++g) {
             const int e0 = bounds[g], e1 = bounds[g + 1];
-            hipEvent_t* ev = next_timing_slot(env);
+            hipEvent_t* ev = dev ? nullptr : next_timing_slot(env);
             if (ev) (void)hipEventRecord(ev[0], S[g]);
             BeamParams bp = beam_params(env, false, Q.act_store, nullptr, nullptr);
             FinishParams fp = finish_params(env, obs_d, rew, terminated_d, info);
@@ -2465,6 +2619,14 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
             hipLaunchKernelGGL(k_step_policy<false>, dim3((e1 - e0 + wpb - 1) / wpb), dim3(64 * wpb), smem,
                                S[g], bp, fp, Q);
             RT_LAUNCH_CHECK("k_step_policy");
+            if (dev) {
+                RT_HIP(hipStreamWriteValue64(S[g], env->seq_d + g * kSeqStride, env->beam_next[g] + t + 1, 0));
+                RT_HIP(hipStreamWaitValue64(S[g], env->seq_d + (kMaxRolloutGroups + g) * kSeqStride,
+                                            env->done_next[g] + grid_dense * (t + 1), hipStreamWaitValueGte,
+                                            ~0ull));
+                if (const int rc = launch_finish(env, obs_d, rew, terminated_d, info, S[g], e0, e1)) return rc;
+                continue;
+            }
             // k_dense turns in a ring: group g of step t after group g-1 of step t
             // (group 0 after group G-1 of step t-1)
             hipEvent_t wait = (piped && serial && (t > 0 || g > 0)) ? dense_ev[(g + G - 1) % G] : nullptr;
@@ -2479,6 +2641,48 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
             RT_HIP(hipStreamWaitEvent(s, join_ev[g], 0));
         }
     }
+    if (dev) {
+        RT_HIP(hipEventRecord(env->dev_ev[0], env->dstream));
+        RT_HIP(hipStreamWaitEvent(s, env->dev_ev[0], 0));
+        for (int g = 0; g < G; ++g) {
+            env->beam_next[g] += (uint64_t)r->n_steps;
+            env->done_next[g] += grid_dense * (uint64_t)r->n_steps;
+        }
+    }
+    return RT_OK;
+}
+
+// Device hand-off resources, made on first use: the dose stream on its own
+// hardware queue (a CU-masked stream gets a dedicated queue; a pooled one could
+// sit behind a group stream's wait and never start), its join event, the
+// hand-off words and the host-visible timeout flag.
+static int ensure_handoff(rt_env* env) {
+    if (env->dstream) return RT_OK;
+    if (!env->pipe[0]) return fail(RT_EINVAL, "dense hand-off: dense visionless handles only");
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    RT_HIP(hipSetDevice(env->device));
+    std::vector<uint32_t> mask((env->num_cu + 31) / 32, 0u);
+    for (int c = 0; c < env->num_cu; ++c) mask[c / 32] |= 1u << (c % 32);
+    hipError_t e = hipExtStreamCreateWithCUMask(&env->dstream, (uint32_t)mask.size(), mask.data());
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&env->dev_ev[0], hipEventDisableTiming | kEventNoSysFence);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&env->dev_ev[1], hipEventDisableTiming | kEventNoSysFence);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&env->err_h), 64, hipHostMallocCoherent);
+    if (e == hipSuccess) *env->err_h = 0;
+    int rc = e == hipSuccess ? RT_OK : fail(RT_EDEVICE, std::string("dense hand-off setup: ") + hipGetErrorString(e));
+    if (!rc) rc = dev_alloc(env, &env->seq_d, (size_t)2 * kMaxRolloutGroups * kSeqStride);
+    if (!rc && hipMemset(env->seq_d, 0, (size_t)2 * kMaxRolloutGroups * kSeqStride * 8) != hipSuccess)
+        rc = fail(RT_EDEVICE, "dense hand-off: hipMemset failed");
+    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = fail(RT_EDEVICE, "dense hand-off: sync failed");
+    (void)hipSetDevice(cur);
+    return rc;
+}
+
+int rt_env_set_dense_handoff(rt_env* env, int32_t mode) {
+    if (!env || mode < 0 || mode > 1) return fail(RT_EINVAL, "rt_env_set_dense_handoff: mode must be 0 (events) or 1 (device)");
+    if (mode == 1)
+        if (const int rc = ensure_handoff(env)) return rc;
+    env->dense_handoff = mode;
     return RT_OK;
 }
 

@@ -177,6 +177,12 @@ class RadiotherapyVecEnv:
         """Env groups of the dense-mode rollout_policy: 2..4 (pipelined streams; default 2), 1 or 0 (persistent)."""
         _lib.check(self._L.rt_env_set_rollout_groups(self._h, int(groups)), "rt_env_set_rollout_groups")
 
+    def set_dense_handoff(self, mode: int):
+        """How the pipelined dense rollout hands the dose stream between env
+        groups: 0 = a k_dense launch per turn ordered by events, 1 = one
+        k_dense_rollout launch per call gated by device hand-off words."""
+        _lib.check(self._L.rt_env_set_dense_handoff(self._h, int(mode)), "rt_env_set_dense_handoff")
+
     def set_next_tumours(self, ids):
         t = torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
         _lib.check(self._L.rt_env_set_next_tumours(self._h, _lib.ptr(t), _lib.stream_handle()),
