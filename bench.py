@@ -123,6 +123,8 @@ def parse():
                          "1 = one k_dense_rollout launch per call gated by device hand-off words")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
+    ap.add_argument("--conv-precision", choices=["f32", "bf16x3"], default="f32",
+                    help="vision: conv1's forward products (rt_conv_set_precision) in the rollout and the update")
     ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="bf16x3",
                     help="the fused update's 64x64 layer products (ppo_update_ms); the other is timed beside it")
     ap.add_argument("--rehearse-same-device", action="store_true",
@@ -146,7 +148,8 @@ def trainer_cfg(a):
     return SimpleNamespace(num_steps=a.num_steps, num_minibatches=a.num_minibatches, update_epochs=a.update_epochs,
                            learning_rate=3e-4, anneal_lr=False, gamma=0.99, gae_lambda=0.95, norm_adv=True,
                            clip_coef=0.1, clip_vloss=True, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
-                           micro_batch=a.micro_batch, update_precision=a.update_precision)
+                           micro_batch=a.micro_batch, update_precision=a.update_precision,
+                           **({"conv_precision": a.conv_precision} if a.vision else {}))
 
 
 def cpu_baseline(seconds: float):
@@ -443,8 +446,39 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
         stages[names[k]] = row
         fwd_ms += t_inf
         train_ms += t_trn + t_wg + t_dg
+    # conv1's forward with bf16x3 products (rt_conv_set_precision), the
+    # extractor's dominant kernel; max |y - y_f32| on the same observations
+    prev = int(L.rt_conv_get_precision())
+    layer1 = plan[0][0]
+    w1, b1 = convs[0].weight.detach().contiguous(), convs[0].bias.detach().contiguous()
+    y32 = acts[1].clone()
+
+    def fwd1(am):
+        return lambda: _lib.check(L.rt_conv_relu_pool_fwd(ctypes.byref(layer1), batch, acts[0].data_ptr(), None,
+                                                          w1.data_ptr(), b1.data_ptr(), acts[1].data_ptr(),
+                                                          _lib.ptr(am), st), "fwd")
+    fwd1(None)()
+    y32 = acts[1].clone()
+    _lib.check(L.rt_conv_set_precision(_lib.CONV_PREC["bf16x3"]), "rt_conv_set_precision")
+    try:
+        t1_inf = timed(fwd1(None))
+        t1_trn = timed(fwd1(ams[0]))
+        fwd1(None)()
+        torch.cuda.synchronize()
+        dmax = float((acts[1] - y32).abs().max())
+    finally:
+        L.rt_conv_set_precision(prev)
+    s1 = stages["conv1"]
+    bf = {"conv1_forward_ms": t1_inf, "conv1_forward_tflops": flops[0] / t1_inf / 1e9,
+          "conv1_train_forward_ms": t1_trn, "conv1_max_abs_diff_vs_f32": dmax,
+          "forward_ms": fwd_ms - s1["forward_ms"] + t1_inf,
+          "train_pass_ms": train_ms - s1["train_forward_ms"] + t1_trn,
+          "note": "conv1 forward products in bf16x3 (hi*hi + hi*lo + lo*hi, f32 accumulate); stages 2-3 and "
+                  "every backward kernel f32; FLOP rates counted as f32-equivalent"}
     f_fwd = sum(flops)
     f_train = 2 * sum(flops) + sum(flops[1:])
+    bf["forward_tflops"] = f_fwd / bf["forward_ms"] / 1e9
+    bf["train_pass_tflops"] = f_train / bf["train_pass_ms"] / 1e9
     # executed: the weight gradients gather one argmax patch per (channel,
     # pooled window) -- 1/8 of the dense conv backward's multiply-adds, on the
     # VALU (k_conv_wgrad_sparse); forward and data gradients are dense MFMA
@@ -461,7 +495,8 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
                            "executed_flop": f_exec, "executed_achieved": f_exec / train_ms / 1e9,
                            "executed_frac": f_exec / (train_ms * 1e-3) / F32_MFMA_PEAK,
                            "wgrad_form": "argmax gather, 1/8 of the dense MACs (VALU FMA, k_conv_wgrad_sparse)"},
-            "stages": stages, "stage_tflops": "dense-equivalent conv FLOPs / stage kernel time",
+            "stages": stages, "bf16x3_conv1": bf,
+            "stage_tflops": "dense-equivalent conv FLOPs / stage kernel time",
             "timing": "HIP events on the kernels' stream, mean of 5 back-to-back launches"}
 
 
@@ -514,7 +549,7 @@ def main():
         if a.rollout_groups > 1:
             env.set_dense_handoff(a.dense_handoff)
     torch.manual_seed(a.seed)
-    if a.vision:
+    if a.vision:  # conv1's arithmetic: the trainer sets it from cfg.conv_precision
         agent = PPO_3DCNN((4, *grid), (6,), 64).to(dev)
     else:
         agent = PPO((9,), (6,), 64).to(dev)
@@ -813,6 +848,10 @@ def main():
     if steady is not None:
         out["steady_state"] = steady
     out["step_mode"] = a.step_mode
+    if a.vision:
+        out["conv_precision"] = a.conv_precision
+        if a.conv_precision != "f32":
+            out["dtype"] = "f32 (conv1 forward bf16x3)"
     out["rollout_groups"] = a.rollout_groups if a.step_mode == "dense" and not a.vision else 1
     out["dense_handoff"] = "device" if (a.step_mode == "dense" and not a.vision and a.rollout_groups > 1
                                         and a.dense_handoff == 1) else "events"

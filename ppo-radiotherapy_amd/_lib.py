@@ -24,6 +24,7 @@ INFO_NAMES = {
 INFO_W = 20
 STEP_DENSE, STEP_INCREMENTAL = 0, 1
 PPO_PREC = {"f32": 0, "bf16x3": 1}  # RT_PPO_PREC_* (rt_ppo_set_precision)
+CONV_PREC = {"f32": 0, "bf16x3": 1}  # RT_CONV_PREC_* (rt_conv_set_precision)
 
 RT_ELIMIT = -5
 RT_ERRORS = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EDEVICE", -4: "RT_ELAUNCH", -5: "RT_ELIMIT"}
@@ -38,7 +39,7 @@ EXPORTS = [
     "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups", "rt_env_set_dense_handoff",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_set_precision", "rt_ppo_get_precision", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
     "rt_ppo_shuffle", "rt_ppo_shuffle_epochs", "rt_ppo_adv_stats", "rt_ppo_adv_sums", "rt_ppo_adv_finalize",
-    "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
+    "rt_conv_set_precision", "rt_conv_get_precision", "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
     "rt_conv_relu_pool_dgrad",
     "rt_last_error", "rt_abi_version",
 ]
@@ -187,6 +188,8 @@ def load(build_if_missing: bool = True):
         "rt_ppo_adv_stats": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
         "rt_ppo_adv_sums": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
         "rt_ppo_adv_finalize": ([vp, i64, i32, vp, vp], ctypes.c_int),
+        "rt_conv_set_precision": ([i32], ctypes.c_int),
+        "rt_conv_get_precision": ([], i32),
         "rt_conv_out_dims": ([ctypes.POINTER(RtConvLayer), ctypes.POINTER(i32)], ctypes.c_int),
         "rt_conv_relu_pool_fwd": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_conv_wgrad_workspace_floats": ([ctypes.POINTER(RtConvLayer), i32], i64),

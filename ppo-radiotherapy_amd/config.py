@@ -34,6 +34,10 @@ DEFAULTS = {
     # resume_from: such a file -> the run continues at its iteration + 1
     "save_checkpoint": True,
     "resume_from": None,
+    # arithmetic (include/rtenv.h): the fused visionless update's 64x64 layer
+    # products and the C3D conv1 forward, "f32" (the reference's) or "bf16x3"
+    "update_precision": "f32",
+    "conv_precision": "f32",
 }
 
 

@@ -30,6 +30,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstdint>
+#include <cstring>
 #include <algorithm>
 #include <type_traits>
 #include <utility>
@@ -101,6 +102,40 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// bf16x3 products (rt_conv_set_precision(RT_CONV_PREC_BF16X3), conv1 forward):
+// x = hi + lo + e, hi = bf16(x), lo = bf16(x - hi), both round to nearest even
+// (|e| <= 2^-17 |x|); a product is hi*hi + hi*lo + lo*hi in three
+// v_mfma_f32_16x16x32_bf16 (16 cycles each, f32 accumulate) against one
+// 16x16x4 f32 MFMA (32 cycles) per 4 k: 3/16 of the f32 MFMA cycles per flop.
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t bf16_bits(float x) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)x);
+}
+// one element as a packed word: hi(x) << 16 | lo(x)
+__device__ __forceinline__ uint32_t bf_pack(float x) {
+    const uint32_t h = bf16_bits(x);
+    return (h << 16) | bf16_bits(x - __uint_as_float(h << 16));
+}
+__device__ __forceinline__ f4 mfma3(const bf8& ah, const bf8& al, const bf8& bh, const bf8& bl, f4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+// 8 packed words -> the hi and lo bf16x8 operands (element e = word e): one
+// v_perm_b32 per element pair and half
+__device__ __forceinline__ void bf_unpack8(const uint32_t (&p)[8], bf8& hi, bf8& lo) {
+    u4v h, l;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        h[d] = __builtin_amdgcn_perm(p[2 * d + 1], p[2 * d], 0x07060302u);
+        l[d] = __builtin_amdgcn_perm(p[2 * d + 1], p[2 * d], 0x05040100u);
+    }
+    hi = __builtin_bit_cast(bf8, h);
+    lo = __builtin_bit_cast(bf8, l);
 }
 
 int round_mod(int v, int m) {  // smallest x >= v with x % 32 == m
@@ -599,6 +634,89 @@ __device__ __forceinline__ void ring_row(const float* xs, const float (&af)[nste
     }
 }
 
+// ring_row in bf16x3 (conv1 only): the ring slots hold packed words (hi << 16
+// | lo, converted in place once per plane, ring_pack_bf); lane (c, g) supplies
+// B = 8 taps 8b..8b+7 of input channel g at position c (taps 27..31 zero) and
+// A = the same taps of W[c][g] as bf16 hi / lo images in registers, so a
+// 2-tile item is 2 x 4 x 3 MFMAs of 16x16x32 in place of 2 x 27 of 16x16x4.
+// The accumulator layout is the f32 kernel's: the epilogue is shared.
+template <int PYB, int NW, class Epi>
+__device__ __forceinline__ void ring_row_bf(const uint32_t* xs, const bf8 (&ah)[4], const bf8 (&al)[4], const Geom& g,
+                                            int SLOT, int sb, int k, int wave, int lane, RingPrev& pv, Epi&& epi) {
+    const int c = lane & 15, gq = lane >> 4, zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
+    const int lane_xy = gq * g.CS + yc * g.YS + xc;
+    const int nxp = (g.XT + 1) / 2;
+    const int NI = (PYB * nxp + NW - 1) / NW;
+    int zoff[3];
+#pragma unroll
+    for (int dz = 0; dz < 3; ++dz) {
+        int sl = sb + zc + dz;
+        sl = sl >= kRing ? sl - kRing : sl;
+        zoff[dz] = sl * SLOT + lane_xy;
+    }
+    int r = 0, xp = wave;
+    while (xp >= nxp) {
+        xp -= nxp;
+        ++r;
+    }
+    for (int it = 0; it < NI; ++it) {
+        const bool ok = r < PYB;
+        const int rr = ok ? r : PYB - 1;
+        const int tb = 2 * rr * g.YS + 8 * xp;
+        uint32_t pw[2][2][8];
+        auto fetch = [&](uint32_t (&dst)[2][8], int b) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int tap = 8 * b + j;
+                if (tap < 27) {
+                    const int base = zoff[tap / 9] + tb + ((tap / 3) % 3) * g.YS + tap % 3;
+                    dst[0][j] = xs[base];
+                    dst[1][j] = xs[base + 4];
+                } else {
+                    dst[0][j] = 0u;
+                    dst[1][j] = 0u;
+                }
+            }
+        };
+        fetch(pw[0], 0);
+        epi(pv.acc, pv.r, pv.xp, pv.k, pv.ok);  // the previous item's epilogue, between this item's MFMAs
+        f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            if (b + 1 < 4) fetch(pw[(b + 1) & 1], b + 1);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                bf8 bh, bl;
+                bf_unpack8(pw[b & 1][u], bh, bl);
+                acc[u] = mfma3(ah[b], al[b], bh, bl, acc[u]);
+            }
+        }
+        pv.acc[0] = acc[0];
+        pv.acc[1] = acc[1];
+        pv.r = r;
+        pv.xp = xp;
+        pv.k = k;
+        pv.ok = ok;
+        xp += NW;
+        while (xp >= nxp) {
+            xp -= nxp;
+            ++r;
+        }
+    }
+}
+
+// in-place f32 -> packed bf16x3 words of n ring slots from `slot` (after their
+// DMA landed and a barrier; a barrier before they are read)
+__device__ __forceinline__ void ring_pack_bf(float* xs, int slot, int n, int SLOT) {
+    for (int s = 0; s < n; ++s) {
+        int sl = slot + s;
+        sl = sl >= kRing ? sl - kRing : sl;
+        float* p = xs + sl * SLOT;
+        uint32_t* q = reinterpret_cast<uint32_t*>(p);
+        for (int i = threadIdx.x; i < SLOT; i += blockDim.x) q[i] = bf_pack(p[i]);
+    }
+}
+
 struct RingParams {
     const float* x;
     const int64_t* rows;  // sample b reads x row rows[b] (null: b)
@@ -609,8 +727,9 @@ struct RingParams {
     RingGeom rg;
 };
 
-template <int CIN, int G, int PYB, int VEC, int NTH, bool TRAIN>
+template <int CIN, int G, int PYB, int VEC, int NTH, bool TRAIN, bool BF = false>
 __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
+    static_assert(!BF || (CIN == 4 && G == 1), "bf16x3: conv1 only");
     extern __shared__ float xs[];
     constexpr int NS = nsteps<CIN>();
     constexpr int NW = NTH / 64;
@@ -630,9 +749,20 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
     auto load_plane = [&](int t, int slot) { ld.load(xb, P.rg, xs, t, slot, wave, lane); };
 
     // ---- weights (A fragments), bias, epilogue constants
-    float af[NS];
+    float af[BF ? 1 : NS];
+    bf8 ah[BF ? 4 : 1], al[BF ? 4 : 1];
+    if constexpr (BF) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) af[s] = a_frag<CIN, G>(P.w, s, c, gq);
+        for (int b = 0; b < 4; ++b) {
+            uint32_t pw[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pw[j] = 8 * b + j < 27 ? bf_pack(P.w[(c * 4 + gq) * 27 + 8 * b + j]) : 0u;
+            bf_unpack8(pw, ah[b], al[b]);
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) af[s] = a_frag<CIN, G>(P.w, s, c, gq);
+    }
     float bias[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[r] = P.bias[4 * gq + r];
@@ -691,6 +821,10 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
     for (int i = 0; i < 4; ++i) load_plane(2 * k0 + i, i);
     __builtin_amdgcn_s_waitcnt(0x0F70);
     __syncthreads();
+    if constexpr (BF) {
+        ring_pack_bf(xs, 0, 4, SLOT);
+        __syncthreads();
+    }
 
     RingPrev pv{{{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}}, 0, 0, k0, false};
     int sb = 0;  // ring slot of plane 2k
@@ -699,30 +833,39 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
             load_plane(2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4);
             load_plane(2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5);
         }
-        ring_row<CIN, PYB, NW>(xs, af, g, SLOT, sb, k, wave, lane, pv, epi);
+        if constexpr (BF)
+            ring_row_bf<PYB, NW>(reinterpret_cast<const uint32_t*>(xs), ah, al, g, SLOT, sb, k, wave, lane, pv, epi);
+        else
+            ring_row<CIN, PYB, NW>(xs, af, g, SLOT, sb, k, wave, lane, pv, epi);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next row has landed
         __syncthreads();                     // ... every wave's; and nobody still reads the slots reloaded next
         sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+        if constexpr (BF) {
+            if (k + 1 < k1) {  // the two planes that just landed, before row k + 1 reads them
+                ring_pack_bf(xs, sb + 2 >= kRing ? sb + 2 - kRing : sb + 2, 2, SLOT);
+                __syncthreads();
+            }
+        }
     }
     epi(pv.acc, pv.r, pv.xp, pv.k, pv.ok);
 }
 
-template <int CIN, int G, int PYB, int VEC, int NTH>
+template <int CIN, int G, int PYB, int VEC, int NTH, bool BF = false>
 int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
                 const float* bias, float* y, uint8_t* amax, hipStream_t st) {
     RingParams P{x, rows, w, bias, y, amax, rg};
     const size_t lds = (size_t)kRing * rg.SLOT * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (const int rc_lds = allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, true>)) return rc_lds;
-        if (const int rc_lds = allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, false>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, true, BF>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_ring<CIN, G, PYB, VEC, NTH, false, BF>)) return rc_lds;
         attr = true;
     }
     dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, B);
     if (amax)
-        hipLaunchKernelGGL((k_conv_ring<CIN, G, PYB, VEC, NTH, true>), grid, dim3(NTH), lds, st, P);
+        hipLaunchKernelGGL((k_conv_ring<CIN, G, PYB, VEC, NTH, true, BF>), grid, dim3(NTH), lds, st, P);
     else
-        hipLaunchKernelGGL((k_conv_ring<CIN, G, PYB, VEC, NTH, false>), grid, dim3(NTH), lds, st, P);
+        hipLaunchKernelGGL((k_conv_ring<CIN, G, PYB, VEC, NTH, false, BF>), grid, dim3(NTH), lds, st, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
@@ -983,6 +1126,21 @@ int launch_ring_zs(const rt_conv_layer* L, int32_t B, const float* x, const int6
     return RT_ELIMIT;
 }
 
+// Arithmetic of conv1's forward (rt_conv_set_precision; initial value from
+// RT_CONV_PREC=f32|bf16x3, default f32)
+int g_conv_prec = [] {
+    const char* e = std::getenv("RT_CONV_PREC");
+    return (e && std::strcmp(e, "bf16x3") == 0) ? 1 : 0;
+}();
+
+template <int CIN, int G, int PYB, int VEC, int NTH>
+int launch_ring_p(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
+                  const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+    if constexpr (CIN == 4 && G == 1)
+        if (g_conv_prec == 1) return launch_ring<CIN, G, PYB, VEC, NTH, true>(rg, B, x, rows, w, bias, y, amax, st);
+    return launch_ring<CIN, G, PYB, VEC, NTH, false>(rg, B, x, rows, w, bias, y, amax, st);
+}
+
 // the forward: the widest y band whose ring fits the LDS budget (80 KiB: two
 // 8-wave blocks per CU for conv1; the 16-channel stages hold 2 waves per SIMD
 // by registers, one 8-wave block per CU, 160 KiB).  Wider planes: conv1 takes
@@ -1010,27 +1168,27 @@ int launch_fwd_ring(const rt_conv_layer* L, int32_t B, const float* x, const int
         if (small && vec4) {
             const RingGeom rg = make_ring_geom<CIN, 2, 4>(L, B, 256);
             if ((size_t)kRing * rg.SLOT * sizeof(float) <= 40 * 1024 && (rg.npiece + 3) / 4 <= ring_max_pieces<CIN, 4>())
-                return launch_ring<CIN, G, 2, 4, 256>(rg, B, x, rows, w, bias, y, amax, st);
+                return launch_ring_p<CIN, G, 2, 4, 256>(rg, B, x, rows, w, bias, y, amax, st);
         }
     }
     for (const size_t budget : {(size_t)(CIN == 4 ? 80 : 160) * 1024, (size_t)160 * 1024}) {
         if constexpr (CIN == 4) {
             if (vec4) {
                 RingGeom rg = make_ring_geom<CIN, PY_BIG, 4>(L, B, NTH);
-                if (fits(rg, 4, budget)) return launch_ring<CIN, G, PY_BIG, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+                if (fits(rg, 4, budget)) return launch_ring_p<CIN, G, PY_BIG, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
                 rg = make_ring_geom<CIN, PY_BIG / 2, 4>(L, B, NTH);
                 if (fits(rg, 4, budget))
-                    return launch_ring<CIN, G, PY_BIG / 2, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+                    return launch_ring_p<CIN, G, PY_BIG / 2, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
             }
         }
         RingGeom rg = make_ring_geom<CIN, PY_BIG, 1>(L, B, NTH);
-        if (fits(rg, 1, budget)) return launch_ring<CIN, G, PY_BIG, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+        if (fits(rg, 1, budget)) return launch_ring_p<CIN, G, PY_BIG, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
         rg = make_ring_geom<CIN, PY_BIG / 2, 1>(L, B, NTH);
-        if (fits(rg, 1, budget)) return launch_ring<CIN, G, PY_BIG / 2, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+        if (fits(rg, 1, budget)) return launch_ring_p<CIN, G, PY_BIG / 2, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
         if constexpr (PY_BIG / 4 >= 1) {
             rg = make_ring_geom<CIN, PY_BIG / 4, 1>(L, B, NTH);
             if (fits(rg, 1, budget))
-                return launch_ring<CIN, G, PY_BIG / 4, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+                return launch_ring_p<CIN, G, PY_BIG / 4, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
         }
         if (CIN != 4) break;  // the 16-channel stages already tried the whole 160 KiB
     }
@@ -2629,6 +2787,15 @@ extern "C" int rt_conv_out_dims(const rt_conv_layer* L, int32_t* out_dims) {
     out_dims[2] = g.PW;
     return RT_OK;
 }
+
+extern "C" int rt_conv_set_precision(int32_t prec) {
+    if (prec != RT_CONV_PREC_F32 && prec != RT_CONV_PREC_BF16X3)
+        return rt_internal_fail(RT_EINVAL, "rt_conv_set_precision: unknown precision");
+    g_conv_prec = prec == RT_CONV_PREC_BF16X3 ? 1 : 0;
+    return RT_OK;
+}
+
+extern "C" int32_t rt_conv_get_precision(void) { return g_conv_prec ? RT_CONV_PREC_BF16X3 : RT_CONV_PREC_F32; }
 
 extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, const float* x_d, const int64_t* rows_d,
                                      const float* w_d, const float* b_d, float* y_d, uint8_t* argmax_d,

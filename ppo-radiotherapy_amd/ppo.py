@@ -137,6 +137,14 @@ class PPOTrainer:
             if prec not in _lib.PPO_PREC:
                 raise ValueError(f"update_precision {prec!r}: expected one of {sorted(_lib.PPO_PREC)}")
             self._update_prec = _lib.PPO_PREC[prec]
+        # arithmetic of the C3D conv1 forward (vision agent): "f32" (the
+        # reference's) or "bf16x3" (rt_conv_set_precision, process-wide; set
+        # only when the config names it)
+        if hasattr(cfg, "conv_precision"):
+            cprec = str(cfg.conv_precision)
+            if cprec not in _lib.CONV_PREC:
+                raise ValueError(f"conv_precision {cprec!r}: expected one of {sorted(_lib.CONV_PREC)}")
+            _lib.check(_lib.load().rt_conv_set_precision(_lib.CONV_PREC[cprec]), "rt_conv_set_precision")
         # one flat gradient bucket; every param.grad is a view of it
         self.flat_grad = torch.zeros(n, dtype=self.params[0].dtype, **kw)
         off = 0

@@ -42,6 +42,51 @@ def _ref(x, w, b, groups, pad):
 
 @pytest.mark.parametrize("cin,groups,dims,pad,B", STAGES)
 def test_conv_relu_pool_forward(cin, groups, dims, pad, B):
+    _check_forward(cin, groups, dims, pad, B)
+
+
+class _conv_precision:
+    """rt_conv_set_precision for the duration of a block (process-wide setting)."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        from ppo_radiotherapy_amd import _lib
+
+        self.L = _lib.load()
+        self.prev = int(self.L.rt_conv_get_precision())
+        _lib.check(self.L.rt_conv_set_precision(_lib.CONV_PREC[self.name]), "rt_conv_set_precision")
+
+    def __exit__(self, *exc):
+        self.L.rt_conv_set_precision(self.prev)
+
+
+@pytest.mark.parametrize("cin,groups,dims,pad,B", [s for s in STAGES if s[0] == 4])
+def test_conv1_forward_bf16x3(cin, groups, dims, pad, B):
+    """conv1 with bf16x3 products (rt_conv_set_precision): the f32 forward's
+    value and activity gates at unchanged tolerances (within 2e-5 of float64
+    torch), and torch's argmax on every window whose top-2 gap exceeds the
+    arithmetic's error bound: 1e-6 + 2 x 2^-15 x max over the window of
+    sum |x||w| (bf16x3 keeps ~2^-15 of each product; with the f32 test's bare
+    1e-6, windows whose f64 gap is below the bf16x3 rounding pick the other
+    maximum)."""
+    from ppo_radiotherapy_amd import _lib
+
+    with _conv_precision("bf16x3"):
+        assert int(_lib.load().rt_conv_get_precision()) == _lib.CONV_PREC["bf16x3"]
+        _check_forward(cin, groups, dims, pad, B, prod_err=2.0 ** -15)
+
+
+def test_conv_precision_rejects_unknown():
+    from ppo_radiotherapy_amd import _lib
+
+    L = _lib.load()
+    assert L.rt_conv_set_precision(7) == -1  # RT_EINVAL
+    assert int(L.rt_conv_get_precision()) in _lib.CONV_PREC.values()
+
+
+def _check_forward(cin, groups, dims, pad, B, prod_err=0.0):
     from ppo_radiotherapy_amd import _lib
 
     dev = torch.device("cuda")
@@ -86,7 +131,13 @@ def test_conv_relu_pool_forward(cin, groups, dims, pad, B):
     ypad = F.pad(yfull, (pad[2], pad[2], pad[1], pad[1], pad[0], pad[0]), value=-1.0)
     win = ypad.unfold(2, 2, 2).unfold(3, 2, 2).unfold(4, 2, 2).reshape(*ref.shape, 8)
     top2 = win.topk(2, dim=-1).values
-    clear = (top2[..., 0] - top2[..., 1] > 1e-6) & (ref > 0)
+    margin = 1e-6
+    if prod_err:
+        absc = F.conv3d(x[rows].double().abs(), w.double().abs(), groups=groups) * prod_err
+        absc = F.pad(absc, (pad[2], pad[2], pad[1], pad[1], pad[0], pad[0]), value=0.0)
+        wb = absc.unfold(2, 2, 2).unfold(3, 2, 2).unfold(4, 2, 2).reshape(*ref.shape, 8).amax(-1)
+        margin = 1e-6 + 2 * wb
+    clear = (top2[..., 0] - top2[..., 1] > margin) & (ref > 0)
     assert clear.float().mean() > 0.5
     assert torch.equal(flat[clear], idx[clear])
 
@@ -197,11 +248,27 @@ def test_planes_too_wide_fail_cleanly():
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("shape,B", [((4, 34, 27, 40), 6), ((4, 22, 23, 160), 2)])
-def test_features_extractor_matches_torch_modules(shape, B):
+@pytest.mark.parametrize("shape,B,prec,gtol", [((4, 34, 27, 40), 6, "f32", 2e-3), ((4, 22, 23, 160), 2, "f32", 2e-3),
+                                               ((4, 64, 64, 64), 2, "f32", 2e-3),
+                                               ((4, 34, 27, 40), 6, "bf16x3", 2e-3),
+                                               ((4, 64, 64, 64), 2, "bf16x3", 5e-3)])
+def test_features_extractor_matches_torch_modules(shape, B, prec, gtol):
     """FeaturesExtractor3D on the GPU (fused kernels) vs its own torch modules
     on the CPU in float64: features and every parameter gradient (the second
-    shape: a grid 160 voxels wide, beyond the conv1 ring's 80 KiB band)."""
+    shape: a grid 160 voxels wide, beyond the conv1 ring's 80 KiB band).
+    bf16x3: conv1's forward products in bf16x3 -- features at the f32
+    tolerances (measured 5e-7 vs 5e-8 for f32).  Gradients: conv1's weight
+    gradient routes each window's gradient through the forward's argmax, and
+    a window whose float64 top-2 gap is below the bf16x3 rounding (~2^-15 of
+    each product) routes it to the other voxel: at 64^3 its max relative error
+    is 3.8e-3 (f32: <= 1e-6), so that case is gated at 5e-3; every other
+    parameter stays within 1e-5 (tools/c3d_prec_err.py,
+    profiles/r03/r03_s27_c3d_prec_err.json)."""
+    with _conv_precision(prec):
+        _check_extractor(shape, B, gtol)
+
+
+def _check_extractor(shape, B, gtol):
     from ppo_radiotherapy_amd.networks import FeaturesExtractor3D
 
     torch.manual_seed(0)
@@ -218,6 +285,6 @@ def test_features_extractor_matches_torch_modules(shape, B):
     fr.backward(gf)
     for (n, p), q in zip(fe.named_parameters(), ref.parameters()):
         err = float((p.grad.cpu().double() - q.grad).abs().max()) / (float(q.grad.abs().max()) + 1e-12)
-        assert err < 2e-3, (n, err)
+        assert err < gtol, (n, err)
     with torch.no_grad():
         torch.testing.assert_close(fe(x.cuda()), f.detach())  # inference path (no argmax) = training forward

@@ -205,23 +205,34 @@ def test_export_trajectory_format(tmp_path, golden):
     env.close()
 
 
-def test_train_cli_vision_reference_grid(tmp_path, capsys):
+@pytest.mark.parametrize("conv_precision", [None, "bf16x3"])
+def test_train_cli_vision_reference_grid(tmp_path, capsys, conv_precision):
     """The reference's vision entry point, `python train.py --config-file
     configs/vision.yaml` (train.py:102-106: PPO_3DCNN + agent.summary(),
     configs/vision.yaml.template keys), run through the CLI at the reference
     grid 67x43x70 -- odd dims, so the first pool pads (networks.py:18-20) --
-    on the C3D kernels, with the micro-batched update."""
+    on the C3D kernels, with the micro-batched update; and with the config key
+    conv_precision: bf16x3 (conv1's forward products, rt_conv_set_precision)."""
     import yaml
 
     import train as train_mod
+    from ppo_radiotherapy_amd import _lib
 
     cfg = yaml.safe_load(open(os.path.join(REPO, "configs", "vision.yaml")))
     cfg.update(dict(exp_name="vis", num_envs=4, num_steps=8, total_timesteps=64, num_minibatches=2,
                     update_epochs=2, num_saves=1, micro_batch=6))
+    if conv_precision:
+        cfg["conv_precision"] = conv_precision
+    L = _lib.load()
+    prev = int(L.rt_conv_get_precision())
     p = tmp_path / "vision.yaml"
     yaml.safe_dump(cfg, open(p, "w"))
     out = tmp_path / "out"
-    agent = train_mod.main(["--config-file", str(p), "--output-dir", str(out)])
+    try:
+        agent = train_mod.main(["--config-file", str(p), "--output-dir", str(out)])
+        assert int(L.rt_conv_get_precision()) == _lib.CONV_PREC[conv_precision or "f32"] if conv_precision else True
+    finally:
+        L.rt_conv_set_precision(prev)
     printed = capsys.readouterr().out
     assert "Observation shape:  (4, 67, 43, 70)" in printed  # agent.summary()
     from ppo_radiotherapy_amd.networks import PPO_3DCNN
