@@ -422,13 +422,13 @@ typedef struct rt_conv_layer {
     int32_t pool_pad[3];  /* 0 or 1 per axis */
 } rt_conv_layer;
 
-/* Arithmetic of conv1's forward (the 4-channel stage, the C3D's dominant
- * kernel; process-wide, initially RT_CONV_PREC=f32|bf16x3 from the
- * environment, else f32).  F32: exact f32 MFMA (the reference's torch Conv3d
- * in f32; its cuDNN default allowed TF32).  BF16X3: every input and weight
- * split into bf16 hi + lo (round to nearest even), products hi*hi + hi*lo +
- * lo*hi accumulated in f32 (relative error <= ~2^-15 per product).  The
- * 16-channel stages and every backward kernel stay f32.  RT_EINVAL on another
+/* Arithmetic of the C3D forward products (process-wide, initially
+ * RT_CONV_PREC=f32|bf16x3 from the environment, else f32).  F32: exact f32
+ * MFMA (the reference's torch Conv3d in f32; its cuDNN default allowed TF32).
+ * BF16X3: in conv1's kernel and the grouped stages' (groups 2 and 4) kernels,
+ * every input and weight split into bf16 hi + lo (round to nearest even),
+ * products hi*hi + hi*lo + lo*hi accumulated in f32 (relative error <= ~2^-15
+ * per product).  Every backward kernel stays f32.  RT_EINVAL on another
  * value. */
 #define RT_CONV_PREC_F32 0
 #define RT_CONV_PREC_BF16X3 1

@@ -707,10 +707,11 @@ __device__ __forceinline__ void ring_row_bf(const uint32_t* xs, const bf8 (&ah)[
 
 // in-place f32 -> packed bf16x3 words of n ring slots from `slot` (after their
 // DMA landed and a barrier; a barrier before they are read)
+template <int NRING = kRing>
 __device__ __forceinline__ void ring_pack_bf(float* xs, int slot, int n, int SLOT) {
     for (int s = 0; s < n; ++s) {
         int sl = slot + s;
-        sl = sl >= kRing ? sl - kRing : sl;
+        sl = sl >= NRING ? sl - NRING : sl;
         float* p = xs + sl * SLOT;
         uint32_t* q = reinterpret_cast<uint32_t*>(p);
         for (int i = threadIdx.x; i < SLOT; i += blockDim.x) q[i] = bf_pack(p[i]);
@@ -921,16 +922,30 @@ RingGeom make_ring_geom_zs(const rt_conv_layer* L, int B) {
     return r;
 }
 
+// Arithmetic of the C3D forward products (rt_conv_set_precision; initial
+// value from RT_CONV_PREC=f32|bf16x3, default f32): bf16x3 in conv1's ring
+// kernel and the grouped stages' z-shift kernels
+int g_conv_prec = [] {
+    const char* e = std::getenv("RT_CONV_PREC");
+    return (e && std::strcmp(e, "bf16x3") == 0) ? 1 : 0;
+}();
+
 // ring slots of the z-shift kernel: the G + 2 planes of a tile + the next G
 template <int G>
 constexpr int ring_zs_slots() {
     return 2 * G + 2;
 }
 
-template <int G, int PYB, bool TRAIN>
+// bf16x3 (BF): lane group g's k values are the list (tz', channel quad q,
+// tap) of its input channel 4q + g, 8 per 16x16x32 MFMA (NVB = ZX * QPB * 9 / 8
+// rounded up, zero-padded); A = the patch as packed ring words (ring_pack_bf),
+// B = Wext hi / lo images in registers; the accumulator layout and the
+// epilogue are the f32 kernel's.
+template <int G, int PYB, bool TRAIN, bool BF = false>
 __global__ __launch_bounds__(512) RT_ZS_FWD_ATTR void k_conv_ring_zs(RingParams P) {
     extern __shared__ float xs[];
     constexpr int CPG = CO / G, NW = 8, ZX = G + 2, KS = CPG * ZX * 9 / 4, NB = KS / 9, NR = ring_zs_slots<G>();
+    constexpr int NV = ZX * (CPG / 4) * 9, NVB = (NV + 7) / 8;  // bf16x3: k values per lane group, MFMAs
     constexpr int QPB = CPG / 4;  // channel quads per plane: batch bj = (tz' = bj / QPB, quad bj % QPB)
     static_assert(PYB % 2 == 0, "4-row y tiles");
     const Geom& g = P.rg.g;
@@ -950,11 +965,26 @@ __global__ __launch_bounds__(512) RT_ZS_FWD_ATTR void k_conv_ring_zs(RingParams 
 
     // B = Wext: k-step st = 9 bj + q, batch bj = (tz', channel quad), q = (ty, tx); lane group = ci in the quad
     const int co_l = c / G, sz = c % G;
-    float bw[KS];
+    float bw[BF ? 1 : KS];
+    bf8 bwh[BF ? NVB : 1], bwl[BF ? NVB : 1];
+    if constexpr (BF) {
 #pragma unroll
-    for (int st = 0; st < KS; ++st) {
-        const int bj = st / 9, q = st % 9, tz = bj / QPB, ci = 4 * (bj % QPB) + gq, dz = tz - sz;
-        bw[st] = (dz >= 0 && dz < 3) ? P.w[((grp * CPG + co_l) * CPG + ci) * 27 + dz * 9 + q] : 0.0f;
+        for (int v8 = 0; v8 < NVB; ++v8) {
+            uint32_t pw[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int e = 8 * v8 + j, tz = e / (9 * QPB), ci = 4 * ((e / 9) % QPB) + gq, q = e % 9, dz = tz - sz;
+                pw[j] = (e < NV && dz >= 0 && dz < 3) ? bf_pack(P.w[((grp * CPG + co_l) * CPG + ci) * 27 + dz * 9 + q])
+                                                      : 0u;
+            }
+            bf_unpack8(pw, bwh[v8], bwl[v8]);
+        }
+    } else {
+#pragma unroll
+        for (int st = 0; st < KS; ++st) {
+            const int bj = st / 9, q = st % 9, tz = bj / QPB, ci = 4 * (bj % QPB) + gq, dz = tz - sz;
+            bw[st] = (dz >= 0 && dz < 3) ? P.w[((grp * CPG + co_l) * CPG + ci) * 27 + dz * 9 + q] : 0.0f;
+        }
     }
     const int co = grp * CPG + co_l;
     const float bias = P.bias[co];
@@ -1012,6 +1042,10 @@ __global__ __launch_bounds__(512) RT_ZS_FWD_ATTR void k_conv_ring_zs(RingParams 
     for (int i = 0; i < ZX; ++i) load_plane(2 * k0 + i, i);
     __builtin_amdgcn_s_waitcnt(0x0F70);
     __syncthreads();
+    if constexpr (BF) {
+        ring_pack_bf<NR>(xs, 0, ZX, SLOT);
+        __syncthreads();
+    }
 
     f4 pacc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
     int pyt = 0, pxp = 0, ppz = k0;
@@ -1054,7 +1088,7 @@ __global__ __launch_bounds__(512) RT_ZS_FWD_ATTR void k_conv_ring_zs(RingParams 
                         if constexpr (decltype(two_t)::value) dst[1][ty * 3 + tx] = xs[base + ty * g.YS + tx + 4];
                     }
             };
-            fetch(bv[0], 0, std::true_type{});
+            if constexpr (!BF) fetch(bv[0], 0, std::true_type{});
             epi(pacc, pyt, pxp, ppz, pok);  // the previous item's epilogue, between this item's MFMAs
             f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
             auto mloop = [&](auto two_t) {
@@ -1068,7 +1102,38 @@ __global__ __launch_bounds__(512) RT_ZS_FWD_ATTR void k_conv_ring_zs(RingParams 
                     }
                 }
             };
-            if (live) {
+            if constexpr (BF) {
+                const uint32_t* xu = reinterpret_cast<const uint32_t*>(xs);
+                auto fetchb = [&](uint32_t (&dst)[2][8], int v8) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int e = 8 * v8 + j;
+                        if (e < NV) {
+                            const int q = e % 9;
+                            const int a = zoff[e / (9 * QPB)] + ((e / 9) % QPB) * 4 * g.CS + tb + (q / 3) * g.YS + q % 3;
+                            dst[0][j] = xu[a];
+                            dst[1][j] = xu[a + 4];
+                        } else {
+                            dst[0][j] = 0u;
+                            dst[1][j] = 0u;
+                        }
+                    }
+                };
+                if (live) {
+                    uint32_t pv[2][2][8];
+                    fetchb(pv[0], 0);
+#pragma unroll
+                    for (int v8 = 0; v8 < NVB; ++v8) {
+                        if (v8 + 1 < NVB) fetchb(pv[(v8 + 1) & 1], v8 + 1);
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            bf8 ah, al;
+                            bf_unpack8(pv[v8 & 1][u], ah, al);
+                            acc[u] = mfma3(ah, al, bwh[v8], bwl[v8], acc[u]);
+                        }
+                    }
+                }
+            } else if (live) {
                 if (two)
                     mloop(std::true_type{});
                 else
@@ -1084,29 +1149,42 @@ __global__ __launch_bounds__(512) RT_ZS_FWD_ATTR void k_conv_ring_zs(RingParams 
         __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next row has landed
         __syncthreads();                     // ... every wave's; and nobody still reads the slots reloaded next
         sb = sb + G >= NR ? sb + G - NR : sb + G;
+        if constexpr (BF) {
+            if (k + G / 2 < k1) {  // the G planes that just landed, before the next tile row reads them
+                ring_pack_bf<NR>(xs, sb + 2 >= NR ? sb + 2 - NR : sb + 2, G, SLOT);
+                __syncthreads();
+            }
+        }
     }
     epi(pacc, pyt, pxp, ppz, pok);
+}
+
+template <int G, int PYB, bool BF>
+int launch_ring_zs_kp(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
+                      const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+    RingParams P{x, rows, w, bias, y, amax, rg};
+    const size_t lds = (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        if (const int rc_lds = allow_big_lds(&k_conv_ring_zs<G, PYB, true, BF>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_ring_zs<G, PYB, false, BF>)) return rc_lds;
+        attr = true;
+    }
+    dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, G * B);
+    if (amax)
+        hipLaunchKernelGGL((k_conv_ring_zs<G, PYB, true, BF>), grid, dim3(512), lds, st, P);
+    else
+        hipLaunchKernelGGL((k_conv_ring_zs<G, PYB, false, BF>), grid, dim3(512), lds, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
 }
 
 template <int G, int PYB>
 int launch_ring_zs_k(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
                      const float* bias, float* y, uint8_t* amax, hipStream_t st) {
-    RingParams P{x, rows, w, bias, y, amax, rg};
-    const size_t lds = (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float);
-    static bool attr = false;
-    if (!attr) {
-        if (const int rc_lds = allow_big_lds(&k_conv_ring_zs<G, PYB, true>)) return rc_lds;
-        if (const int rc_lds = allow_big_lds(&k_conv_ring_zs<G, PYB, false>)) return rc_lds;
-        attr = true;
-    }
-    dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, G * B);
-    if (amax)
-        hipLaunchKernelGGL((k_conv_ring_zs<G, PYB, true>), grid, dim3(512), lds, st, P);
-    else
-        hipLaunchKernelGGL((k_conv_ring_zs<G, PYB, false>), grid, dim3(512), lds, st, P);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
-    return RT_OK;
+    if (g_conv_prec == 1) return launch_ring_zs_kp<G, PYB, true>(rg, B, x, rows, w, bias, y, amax, st);
+    return launch_ring_zs_kp<G, PYB, false>(rg, B, x, rows, w, bias, y, amax, st);
 }
 
 // the widest y band whose ring fits 160 KiB (one 8-wave block per CU)
@@ -1126,12 +1204,6 @@ int launch_ring_zs(const rt_conv_layer* L, int32_t B, const float* x, const int6
     return RT_ELIMIT;
 }
 
-// Arithmetic of conv1's forward (rt_conv_set_precision; initial value from
-// RT_CONV_PREC=f32|bf16x3, default f32)
-int g_conv_prec = [] {
-    const char* e = std::getenv("RT_CONV_PREC");
-    return (e && std::strcmp(e, "bf16x3") == 0) ? 1 : 0;
-}();
 
 template <int CIN, int G, int PYB, int VEC, int NTH>
 int launch_ring_p(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,

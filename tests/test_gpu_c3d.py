@@ -62,9 +62,10 @@ class _conv_precision:
         self.L.rt_conv_set_precision(self.prev)
 
 
-@pytest.mark.parametrize("cin,groups,dims,pad,B", [s for s in STAGES if s[0] == 4])
-def test_conv1_forward_bf16x3(cin, groups, dims, pad, B):
-    """conv1 with bf16x3 products (rt_conv_set_precision): the f32 forward's
+@pytest.mark.parametrize("cin,groups,dims,pad,B", STAGES)
+def test_forward_bf16x3(cin, groups, dims, pad, B):
+    """bf16x3 products (rt_conv_set_precision: conv1's ring kernel and the
+    grouped stages' z-shift kernels; other stage kernels stay f32): the f32 forward's
     value and activity gates at unchanged tolerances (within 2e-5 of float64
     torch), and torch's argmax on every window whose top-2 gap exceeds the
     arithmetic's error bound: 1e-6 + 2 x 2^-15 x max over the window of
@@ -131,12 +132,7 @@ def _check_forward(cin, groups, dims, pad, B, prod_err=0.0):
     ypad = F.pad(yfull, (pad[2], pad[2], pad[1], pad[1], pad[0], pad[0]), value=-1.0)
     win = ypad.unfold(2, 2, 2).unfold(3, 2, 2).unfold(4, 2, 2).reshape(*ref.shape, 8)
     top2 = win.topk(2, dim=-1).values
-    margin = 1e-6
-    if prod_err:
-        absc = F.conv3d(x[rows].double().abs(), w.double().abs(), groups=groups) * prod_err
-        absc = F.pad(absc, (pad[2], pad[2], pad[1], pad[1], pad[0], pad[0]), value=0.0)
-        wb = absc.unfold(2, 2, 2).unfold(3, 2, 2).unfold(4, 2, 2).reshape(*ref.shape, 8).amax(-1)
-        margin = 1e-6 + 2 * wb
+    margin = _argmax_margin(x[rows].double(), w.double(), groups, pad, ref.shape, prod_err)
     clear = (top2[..., 0] - top2[..., 1] > margin) & (ref > 0)
     assert clear.float().mean() > 0.5
     assert torch.equal(flat[clear], idx[clear])
@@ -154,7 +150,30 @@ def _fwd(lib, L, B, xd, rd, wd, bd, od):
 
 
 @pytest.mark.parametrize("cin,groups,dims,pad,B", STAGES)
+def test_conv_relu_pool_backward_bf16x3_forward(cin, groups, dims, pad, B):
+    """The backward gates (float64 autograd routed through the kernel's argmax
+    bytes) with the argmax bytes of a bf16x3 forward."""
+    with _conv_precision("bf16x3"):
+        _check_backward(cin, groups, dims, pad, B, prod_err=2.0 ** -15)
+
+
+def _argmax_margin(x64, w64, groups, pad, shape, prod_err):
+    """Top-2 gap above which a window's argmax must equal torch's: 1e-6, plus
+    for bf16x3 products twice the error bound prod_err x sum |x||w| of the
+    window's worst position."""
+    if not prod_err:
+        return 1e-6
+    absc = F.conv3d(x64.abs(), w64.abs(), groups=groups) * prod_err
+    absc = F.pad(absc, (pad[2], pad[2], pad[1], pad[1], pad[0], pad[0]), value=0.0)
+    return 1e-6 + 2 * absc.unfold(2, 2, 2).unfold(3, 2, 2).unfold(4, 2, 2).reshape(*shape, 8).amax(-1)
+
+
+@pytest.mark.parametrize("cin,groups,dims,pad,B", STAGES)
 def test_conv_relu_pool_backward(cin, groups, dims, pad, B):
+    _check_backward(cin, groups, dims, pad, B)
+
+
+def _check_backward(cin, groups, dims, pad, B, prod_err=0.0):
     """rt_conv_relu_pool_wgrad (dW, db) and, for 16-channel stages,
     rt_conv_relu_pool_dgrad (dX) vs float64 autograd of the same stage, the
     pooled gradients routed through the kernel's argmax bytes (equal to
@@ -208,7 +227,8 @@ def test_conv_relu_pool_backward(cin, groups, dims, pad, B):
     yfull = F.relu(F.conv3d(x64, w64, b64, groups=groups))
     ypad = F.pad(yfull, (pad[2], pad[2], pad[1], pad[1], pad[0], pad[0]), value=-1.0)
     top2 = ypad.unfold(2, 2, 2).unfold(3, 2, 2).unfold(4, 2, 2).reshape(*ref_pool.shape, 8).topk(2, dim=-1).values
-    clear = (top2[..., 0] - top2[..., 1] > 1e-6) & (ref_pool > 0)
+    margin = _argmax_margin(x64, w64, groups, pad, ref_pool.shape, prod_err)
+    clear = (top2[..., 0] - top2[..., 1] > margin) & (ref_pool > 0)
     assert torch.equal(flat[clear], idx[clear])
     dconv = torch.zeros((B, 16, cd * ch * cw), dtype=torch.float64)
     dconv.scatter_(2, flat.clamp(0, cd * ch * cw - 1).reshape(B, 16, -1),

@@ -1,16 +1,18 @@
 #!/bin/bash
-# r03 session 27: conv1 forward in bf16x3 (packed ring, 16x16x32 bf16 MFMA): C3D tests, stage timing, vision A/B
+# r03 session 29: bf16x3 in the grouped stages' z-shift forward too: C3D tests, timing, vision A/B
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/r03_s27
+O=gpurun_out/r03_s29
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_c3d.py > $O/pytest_c3d.log 2>&1 || { tail -60 $O/pytest_c3d.log; exit 1; }
+tail -2 $O/pytest_c3d.log
 timeout -k 10 200 python -u tools/c3d_prec_err.py $O/prec_err.json > $O/prec_err.log 2>&1 || { tail -30 $O/prec_err.log; exit 1; }
-cat $O/prec_err.log
+grep -v Warning $O/prec_err.log | grep "^(" 
 timeout -k 10 300 python -u bench.py --no-cpu --no-steady --no-update --steps 8 --warmup 4 > $O/bench_c3d.json 2> $O/bench_c3d.err || { tail -20 $O/bench_c3d.err; exit 1; }
 python -c "
 import json; d=json.load(open('$O/bench_c3d.json'))['c3d_mfma']
-print('conv1 f32 fwd', round(d['stages']['conv1']['forward_ms'],3), 'train', round(d['stages']['conv1']['train_forward_ms'],3))
+print('stages f32', {k: {kk: round(vv,3) for kk,vv in v.items() if kk.endswith('_ms')} for k,v in d['stages'].items()})
 print('bf16x3', {k: (round(v,4) if isinstance(v,float) else v) for k,v in d['bf16x3'].items() if k!='note'})
 print('train pass f32', round(d['train_pass']['ms'],3))"
 for p in f32 bf16x3; do
