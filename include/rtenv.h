@@ -425,11 +425,11 @@ typedef struct rt_conv_layer {
 /* Arithmetic of the C3D forward products (process-wide, initially
  * RT_CONV_PREC=f32|bf16x3 from the environment, else f32).  F32: exact f32
  * MFMA (the reference's torch Conv3d in f32; its cuDNN default allowed TF32).
- * BF16X3: in conv1's kernel and the grouped stages' (groups 2 and 4) kernels,
- * every input and weight split into bf16 hi + lo (round to nearest even),
- * products hi*hi + hi*lo + lo*hi accumulated in f32 (relative error <= ~2^-15
- * per product).  Every backward kernel stays f32.  RT_EINVAL on another
- * value. */
+ * BF16X3: in conv1's forward kernel and the grouped stages' (groups 2 and 4)
+ * forward and data-gradient kernels, every operand split into bf16 hi + lo
+ * (round to nearest even), products hi*hi + hi*lo + lo*hi accumulated in f32
+ * (relative error <= ~2^-15 per product).  The weight gradients stay f32.
+ * RT_EINVAL on another value. */
 #define RT_CONV_PREC_F32 0
 #define RT_CONV_PREC_BF16X3 1
 int rt_conv_set_precision(int32_t prec);

@@ -2392,11 +2392,12 @@ int launch_dgrad_ring(const rt_conv_layer* L, int32_t B, const float* w, const f
 // mapping with flipped, transposed weights (1.33x / 2x the useful work for
 // groups 2 / 4 instead of 2x / 4x).  Planes come from the pooling-window
 // scatter of k_conv_dgrad_ring, G/2 pooled rows per tile row.
-template <int G, int PYB>
+template <int G, int PYB, bool BF = false>
 __global__ __launch_bounds__(512) void k_conv_dgrad_ring_zs(DgradRingParams P) {
     extern __shared__ float xs[];
     constexpr int CPG = CO / G, NW = 8, NTH = 512, ZX = G + 2, KS = CPG * ZX * 9 / 4, NB = KS / 9;
     constexpr int NR = ring_zs_slots<G>(), QPB = CPG / 4, MW = kDgMaxWin, HP = G / 2;
+    constexpr int NV = ZX * QPB * 9, NVB = (NV + 7) / 8;  // bf16x3 (BF): k values per lane group, MFMAs
     static_assert(PYB % 2 == 0, "4-row y tiles");
     const Geom& g = P.rg.g;
     const int SLOT = P.rg.SLOT;
@@ -2442,19 +2443,39 @@ __global__ __launch_bounds__(512) void k_conv_dgrad_ring_zs(DgradRingParams P) {
 #pragma unroll
                 for (int ky = 0; ky < 2; ++ky) {
                     const int k2 = kz * 4 + ky * 2;
-                    *reinterpret_cast<float2*>(xs + (slot0 + kz) * SLOT + wlds[u] + ky * g.YS) =
-                        make_float2(kk == k2 ? v : 0.0f, kk == k2 + 1 ? v : 0.0f);
+                    if constexpr (BF)  // packed hi << 16 | lo words (the forward's ring_pack_bf form)
+                        *reinterpret_cast<uint2*>(xs + (slot0 + kz) * SLOT + wlds[u] + ky * g.YS) =
+                            make_uint2(kk == k2 ? bf_pack(v) : 0u, kk == k2 + 1 ? bf_pack(v) : 0u);
+                    else
+                        *reinterpret_cast<float2*>(xs + (slot0 + kz) * SLOT + wlds[u] + ky * g.YS) =
+                            make_float2(kk == k2 ? v : 0.0f, kk == k2 + 1 ? v : 0.0f);
                 }
         }
     };
 
     // B = Wext: k-step st = 9 bj + q, batch bj = (tz', dY channel quad), q = (ty, tx); lane group = dY channel
     const int ci_l = c / G, sz = c % G;
-    float bw[KS];
+    float bw[BF ? 1 : KS];
+    bf8 bwh[BF ? NVB : 1], bwl[BF ? NVB : 1];
+    if constexpr (BF) {  // k list of lane group gq: (tz', dY channel quad, tap) of dY channel 4 quad + gq
 #pragma unroll
-    for (int st = 0; st < KS; ++st) {
-        const int bj = st / 9, q = st % 9, tz = bj / QPB, co = 4 * (bj % QPB) + gq, dz = tz - sz;
-        bw[st] = (dz >= 0 && dz < 3) ? P.w[((grp * CPG + co) * CPG + ci_l) * 27 + (2 - dz) * 9 + 8 - q] : 0.0f;
+        for (int v8 = 0; v8 < NVB; ++v8) {
+            uint32_t pw[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int e = 8 * v8 + j, tz = e / (9 * QPB), co = 4 * ((e / 9) % QPB) + gq, q = e % 9, dz = tz - sz;
+                pw[j] = (e < NV && dz >= 0 && dz < 3)
+                            ? bf_pack(P.w[((grp * CPG + co) * CPG + ci_l) * 27 + (2 - dz) * 9 + 8 - q])
+                            : 0u;
+            }
+            bf_unpack8(pw, bwh[v8], bwl[v8]);
+        }
+    } else {
+#pragma unroll
+        for (int st = 0; st < KS; ++st) {
+            const int bj = st / 9, q = st % 9, tz = bj / QPB, co = 4 * (bj % QPB) + gq, dz = tz - sz;
+            bw[st] = (dz >= 0 && dz < 3) ? P.w[((grp * CPG + co) * CPG + ci_l) * 27 + (2 - dz) * 9 + 8 - q] : 0.0f;
+        }
     }
     const int cstride = g.D * g.H * g.W;
     float* dxb = P.dx + ((int64_t)b * CO + grp * CPG + ci_l) * cstride;
@@ -2525,16 +2546,47 @@ __global__ __launch_bounds__(512) void k_conv_dgrad_ring_zs(DgradRingParams P) {
                         dst[1][ty * 3 + tx] = xs[base + ty * g.YS + tx + 4];
                     }
             };
-            fetch(bv[0], 0);
+            if constexpr (!BF) fetch(bv[0], 0);
             epi(pacc, pyt, pxp, pk, pok);  // the previous item's epilogue, between this item's MFMAs
             f4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+            if constexpr (BF) {
+                const uint32_t* xu = reinterpret_cast<const uint32_t*>(xs);
+                auto fetchb = [&](uint32_t (&dst)[2][8], int v8) {
 #pragma unroll
-            for (int bj = 0; bj < NB; ++bj) {
-                if (bj + 1 < NB) fetch(bv[(bj + 1) & 1], bj + 1);
+                    for (int j = 0; j < 8; ++j) {
+                        const int e = 8 * v8 + j;
+                        if (e < NV) {
+                            const int q = e % 9;
+                            const int a = zoff[e / (9 * QPB)] + ((e / 9) % QPB) * 4 * g.CS + tb + (q / 3) * g.YS + q % 3;
+                            dst[0][j] = xu[a];
+                            dst[1][j] = xu[a + 4];
+                        } else {
+                            dst[0][j] = 0u;
+                            dst[1][j] = 0u;
+                        }
+                    }
+                };
+                uint32_t pv[2][2][8];
+                fetchb(pv[0], 0);
 #pragma unroll
-                for (int q = 0; q < 9; ++q) {
-                    acc[0] = mfma4(bv[bj & 1][0][q], bw[bj * 9 + q], acc[0]);
-                    acc[1] = mfma4(bv[bj & 1][1][q], bw[bj * 9 + q], acc[1]);
+                for (int v8 = 0; v8 < NVB; ++v8) {
+                    if (v8 + 1 < NVB) fetchb(pv[(v8 + 1) & 1], v8 + 1);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        bf8 ah, al;
+                        bf_unpack8(pv[v8 & 1][u], ah, al);
+                        acc[u] = mfma3(ah, al, bwh[v8], bwl[v8], acc[u]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int bj = 0; bj < NB; ++bj) {
+                    if (bj + 1 < NB) fetch(bv[(bj + 1) & 1], bj + 1);
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) {
+                        acc[0] = mfma4(bv[bj & 1][0][q], bw[bj * 9 + q], acc[0]);
+                        acc[1] = mfma4(bv[bj & 1][1][q], bw[bj * 9 + q], acc[1]);
+                    }
                 }
             }
             pacc[0] = acc[0];
@@ -2571,21 +2623,28 @@ RingGeom make_dgrad_ring_geom_zs(const rt_conv_layer* L, int B) {
     return r;
 }
 
-template <int G, int PYB>
-int launch_dgrad_ring_zs_k(const RingGeom& rg, int32_t B, const float* w, const float* dP, const uint8_t* am,
-                           float* dx, hipStream_t st) {
+template <int G, int PYB, bool BF>
+int launch_dgrad_ring_zs_kp(const RingGeom& rg, int32_t B, const float* w, const float* dP, const uint8_t* am,
+                            float* dx, hipStream_t st) {
     DgradRingParams P{w, dP, am, dx, rg};
     const size_t lds = (size_t)ring_zs_slots<G>() * rg.SLOT * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (const int rc_lds = allow_big_lds(&k_conv_dgrad_ring_zs<G, PYB>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_dgrad_ring_zs<G, PYB, BF>)) return rc_lds;
         attr = true;
     }
     dim3 grid(rg.nyb, ((rg.g.D + 1) / 2 + rg.ZC - 1) / rg.ZC, G * B);
-    hipLaunchKernelGGL((k_conv_dgrad_ring_zs<G, PYB>), grid, dim3(512), lds, st, P);
+    hipLaunchKernelGGL((k_conv_dgrad_ring_zs<G, PYB, BF>), grid, dim3(512), lds, st, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
+}
+
+template <int G, int PYB>
+int launch_dgrad_ring_zs_k(const RingGeom& rg, int32_t B, const float* w, const float* dP, const uint8_t* am,
+                           float* dx, hipStream_t st) {
+    if (g_conv_prec == 1) return launch_dgrad_ring_zs_kp<G, PYB, true>(rg, B, w, dP, am, dx, st);
+    return launch_dgrad_ring_zs_kp<G, PYB, false>(rg, B, w, dP, am, dx, st);
 }
 
 template <int G>
