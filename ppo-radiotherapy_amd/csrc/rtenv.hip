@@ -1188,6 +1188,13 @@ __device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const 
     return result >= 0 ? tv[result] : 0.0f;
 }
 
+// KG > 1 (k_finish): the tumour gather issues the loads of KG voxels per lane
+// (their row positions, then their doses) before using any of them, so a
+// 586-voxel tumour costs two dependent HBM round trips per 64 * KG voxels
+// instead of two per 64.  Beside the saturating dose stream of the pipelined
+// rollout a round trip is several microseconds; the fused step kernels (tight
+// register budgets) keep the one-voxel-per-iteration loop (KG = 1).
+template <int KG = 1>
 __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char* wave_lds) {
     float* tvals = reinterpret_cast<float*>(wave_lds);
     if (lane == 0) RT_STAMP(e, 5);
@@ -1235,20 +1242,43 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     int ctum = 0;
     double best = INFINITY;
     int bidx = 0x7fffffff;
-    for (int i = lane; i < nt; i += 64) {
-        const int v = tv[i];
-        const uint32_t c = tc[i];
-        const float x = dose[tp[i]];
+    auto voxel = [&](int i, int v, uint32_t c, float x, bool lung) {
         if (in_lds) tvals[i] = x;
         else tg[i] = x;
-        const bool lung = (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u;
         ctum += (lung && x > P.C.lung_thr) ? 1 : 0;
         const int ix = (int)(c >> 20), iy = (int)((c >> 10) & 1023u), iz = (int)(c & 1023u);
         const double d0 = (double)ix - px, d1 = (double)iy - py, d2 = (double)iz - pz;
         const double nn = sqrt((d0 * d0 + d1 * d1) + d2 * d2);  // np.linalg.norm(axis=1) order
-        if (nn < best) {
+        if (nn < best) {  // ascending i per lane: the first minimum
             best = nn;
             bidx = i;
+        }
+    };
+    if constexpr (KG == 1) {
+        for (int i = lane; i < nt; i += 64) {
+            const int v = tv[i];
+            voxel(i, v, tc[i], dose[tp[i]], (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u);
+        }
+    } else {
+        for (int i0 = lane; i0 < nt; i0 += 64 * KG) {
+            int pos[KG], vv[KG];
+            uint32_t cc[KG], lb[KG];
+            float xv[KG];
+#pragma unroll
+            for (int k = 0; k < KG; ++k) {
+                const int i = min(i0 + 64 * k, nt - 1);
+                pos[k] = tp[i];
+                vv[k] = tv[i];
+                cc[k] = tc[i];
+            }
+#pragma unroll
+            for (int k = 0; k < KG; ++k) {
+                xv[k] = dose[pos[k]];
+                lb[k] = P.lib.lung_bits[vv[k] >> 5];
+            }
+#pragma unroll
+            for (int k = 0; k < KG; ++k)
+                if (i0 + 64 * k < nt) voxel(i0 + 64 * k, vv[k], cc[k], xv[k], (lb[k] >> (vv[k] & 31)) & 1u);
         }
     }
     ctum = wave_sum_i(ctum);
@@ -1328,12 +1358,24 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     if (P.vision) vision_scatter(P, e, lane, pose, m, wave_lds);
 }
 
+// k_finish's tumour gather batch (voxels per lane in flight; finish_env).  1:
+// batching 4 or 8 voxels per lane (VGPRs 78 -> 106) made the pipelined dense
+// step slower, 0.2756 -> 0.2774 / 0.2812-0.2911 ms; A/B builds
+#ifndef RT_FINISH_KG
+#define RT_FINISH_KG 1
+#endif
+// RT_CHAIN_PRIO (A/B builds): wave issue priority (s_setprio) of the latency
+// chain's kernels (k_finish, k_step_policy) against the co-running dose stream
+#ifndef RT_CHAIN_PRIO
+#define RT_CHAIN_PRIO 0
+#endif
 __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
+    if (RT_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(RT_CHAIN_PRIO);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int e = P.e_begin + blockIdx.x * P.wpb + w;
     if (e >= P.N) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm_raw[];
-    finish_env(P, e, lane, fsm_raw + (size_t)w * P.wave_lds);
+    finish_env<RT_FINISH_KG>(P, e, lane, fsm_raw + (size_t)w * P.wave_lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1364,6 +1406,7 @@ struct PolicyStepParams {
 
 template <bool FINISH>
 __global__ __launch_bounds__(1024) void k_step_policy(BeamParams B, FinishParams F, PolicyStepParams Q) {
+    if (RT_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(RT_CHAIN_PRIO);
     extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
     rtpol::Lds& L = *reinterpret_cast<rtpol::Lds*>(psm);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
