@@ -47,6 +47,11 @@ namespace {
 #ifndef RT_C3D_EXP
 #define RT_C3D_EXP 0
 #endif
+// ring forward epilogue: transposed window reduction (1) or one reduction per
+// channel (0, the round-2 form; A/B builds)
+#ifndef RT_EPI_T
+#define RT_EPI_T 1
+#endif
 // blocks the z-shift forward / data-gradient grids aim for when they split z into
 // chunks (A/B builds): 2048 (no split at 512 samples) beat 4096 / 8192 -- a block
 // that sweeps the whole depth pays its weight load and ring prologue once
@@ -769,7 +774,9 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
     for (int r = 0; r < 4; ++r) bias[r] = P.bias[4 * gq + r];
     const int zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
     const int widx = zc * 4 + yc * 2 + (xc & 1);  // rank of the lane in its pooling window
-    const int myr = widx & 3;                      // after the window reduction: lane stores channel 4g + myr
+    // after the window reduction the lane stores channel 4g + myr: RT_EPI_T
+    // (transposed reduction, below) leaves channel 2 (xc & 1) + yc on it
+    const int myr = RT_EPI_T ? 2 * (xc & 1) + yc : widx & 3;
     const bool storer = widx < 4;
     const int chan = g.PD * g.PH * g.PW;
     const int cbase = (4 * gq + myr) * chan;       // element offset of this lane's channel in the sample
@@ -791,14 +798,59 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
             const int px = 2 * tx + (xc >> 1);
             float mine = 0.0f;
             int kmine = 0;
+            if constexpr (RT_EPI_T) {
+                // transposed window reduction: each DPP step halves the
+                // channels a lane keeps while it reduces over a window bit
+                // (bit 0: xor 1; bit 2: row_ror 4, the partner's bit 2 always
+                // differs; bit 3: row_ror 8, same channel) -- 3 / 6 DPP moves
+                // for the 4 channels instead of 12 / 24.  (value, index) pairs
+                // combine as max value, smallest window index among equals:
+                // torch's first maximum in (z, y, x) order.
+                int vi[4];
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const float v = valid ? fmaxf(acc[u][rr] + bias[rr], 0.0f) : -INFINITY;
-                const float m = win_max(v);
-                mine = rr == myr ? m : mine;
+                for (int rr = 0; rr < 4; ++rr)
+                    vi[rr] = __float_as_int(valid ? fmaxf(acc[u][rr] + bias[rr], 0.0f) : -INFINITY);
+                const bool b0 = (c & 1) != 0, b2 = ((c >> 2) & 1) != 0;
+                auto comb = [](int& v, int& k, int rv, int rk) {
+                    const int m = max(v, rv);
+                    k = min(v == m ? k : 8, rv == m ? rk : 8);
+                    v = m;
+                };
+                int va = b0 ? vi[2] : vi[0], vb = b0 ? vi[3] : vi[1];
+                const int ra = __builtin_amdgcn_mov_dpp(b0 ? vi[0] : vi[2], 0xB1, 0xF, 0xF, true);
+                const int rb = __builtin_amdgcn_mov_dpp(b0 ? vi[1] : vi[3], 0xB1, 0xF, 0xF, true);
+                int ka = widx, kb = widx;
                 if constexpr (TRAIN) {
-                    const int k = win_min(v == m ? widx : 8);  // torch: first maximum in (z, y, x) window order
-                    kmine = rr == myr ? k : kmine;
+                    comb(va, ka, ra, widx ^ 1);
+                    comb(vb, kb, rb, widx ^ 1);
+                } else {
+                    va = max(va, ra);
+                    vb = max(vb, rb);
+                }
+                int v = b2 ? vb : va, k = b2 ? kb : ka;
+                const int rv2 = __builtin_amdgcn_mov_dpp(b2 ? va : vb, 0x124, 0xF, 0xF, true);
+                if constexpr (TRAIN) {
+                    const int rk2 = __builtin_amdgcn_mov_dpp(b2 ? ka : kb, 0x124, 0xF, 0xF, true);
+                    comb(v, k, rv2, rk2);
+                    const int rv3 = __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, true);
+                    const int rk3 = __builtin_amdgcn_mov_dpp(k, 0x128, 0xF, 0xF, true);
+                    comb(v, k, rv3, rk3);
+                    kmine = k;
+                } else {
+                    v = max(v, rv2);
+                    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, true));
+                }
+                mine = __int_as_float(v);
+            } else {
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const float v = valid ? fmaxf(acc[u][rr] + bias[rr], 0.0f) : -INFINITY;
+                    const float m = win_max(v);
+                    mine = rr == myr ? m : mine;
+                    if constexpr (TRAIN) {
+                        const int k = win_min(v == m ? widx : 8);  // torch: first maximum in (z, y, x) window order
+                        kmine = rr == myr ? k : kmine;
+                    }
                 }
             }
             const bool st = ok && storer && tx < g.XT && py < g.PH && px < g.PW;
