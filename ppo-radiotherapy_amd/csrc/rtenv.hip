@@ -1194,7 +1194,11 @@ __device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const 
 // instead of two per 64.  Beside the saturating dose stream of the pipelined
 // rollout a round trip is several microseconds; the fused step kernels (tight
 // register budgets) keep the one-voxel-per-iteration loop (KG = 1).
-template <int KG = 1>
+// PF (k_finish): the step's independent scalars (the env's dense partial
+// sums, t, episode return / length) are loaded before the tumour gather and
+// the nearest tumour voxel's index travels with the distance argmin, so the
+// tail issues no dependent load (each one a few us beside the dose stream).
+template <int KG = 1, bool PF = false>
 __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char* wave_lds) {
     float* tvals = reinterpret_cast<float*>(wave_lds);
     if (lane == 0) RT_STAMP(e, 5);
@@ -1239,9 +1243,24 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
         if (lane < m.nlev)
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(lend + lane), (lds_ptr_t)lev_s, 4, 0, 0);
     }
+    // PF: independent loads of the tail, issued before the gather
+    int pf_cnt = 0, pf_t = 0, pf_len = 0;
+    double pf_dl = 0.0, pf_ret = 0.0;
+    if constexpr (PF) {
+        if (!P.incremental)
+            for (int j = lane; j < P.slices; j += 64) {
+                pf_cnt += P.part_cnt[(size_t)e * P.slices + j];
+                pf_dl += P.part_sum[(size_t)e * P.slices + j];
+            }
+        if (lane == 0) {
+            pf_t = P.st.t[e];
+            pf_ret = P.st.ep_return[e];
+            pf_len = P.st.ep_len[e];
+        }
+    }
     int ctum = 0;
     double best = INFINITY;
-    int bidx = 0x7fffffff;
+    int bidx = 0x7fffffff, bvox = 0;
     auto voxel = [&](int i, int v, uint32_t c, float x, bool lung) {
         if (in_lds) tvals[i] = x;
         else tg[i] = x;
@@ -1252,6 +1271,7 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
         if (nn < best) {  // ascending i per lane: the first minimum
             best = nn;
             bidx = i;
+            if constexpr (PF) bvox = v;
         }
     };
     if constexpr (KG == 1) {
@@ -1286,9 +1306,12 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     for (int off = 32; off > 0; off >>= 1) {
         const double ob = __shfl_xor(best, off, 64);
         const int oi = __shfl_xor(bidx, off, 64);
+        int ov = 0;
+        if constexpr (PF) ov = __shfl_xor(bvox, off, 64);
         if (ob < best || (ob == best && oi < bidx)) {
             best = ob;
             bidx = oi;
+            if constexpr (PF) bvox = ov;
         }
     }
     if (lane == 0) RT_STAMP(e, 6);
@@ -1307,9 +1330,14 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
         cnt = P.st.lung_cnt[e];
         dl = P.st.lung_sum[e];
     } else {
-        for (int j = lane; j < P.slices; j += 64) {
-            cnt += P.part_cnt[(size_t)e * P.slices + j];
-            dl += P.part_sum[(size_t)e * P.slices + j];
+        if constexpr (PF) {
+            cnt = pf_cnt;
+            dl = pf_dl;
+        } else {
+            for (int j = lane; j < P.slices; j += 64) {
+                cnt += P.part_cnt[(size_t)e * P.slices + j];
+                dl += P.part_sum[(size_t)e * P.slices + j];
+            }
         }
         cnt = wave_sum_i(cnt);
         dl = wave_sum_d(dl);
@@ -1319,18 +1347,18 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
         const float ratio = S / m.T;
         const float r_tum = ratio * P.C.tum_reward;
         const double r_lung = (double)c / m.lung_total * P.C.lung_reward;
-        const int v = tv[bidx];
+        const int v = PF ? bvox : tv[bidx];
         const int ix = v / HW, iy = (v / W) % H, iz = v % W;
         const double dn = ddot_norm3((double)ix - px, (double)iy - py, (double)iz - pz);
         const double r_dist = dn / P.G.normS * P.C.dist_reward;
         const double total = ((double)r_tum + r_lung) + r_dist;
-        const int t = P.st.t[e];
+        const int t = PF ? pf_t : P.st.t[e];
         const bool done = (ratio >= P.C.tum_thr) || (t >= P.C.max_t);
         if (!P.vision) write_obs9(P.obs, P.G, e, pose, m);
         P.reward[e] = (float)total;
         P.terminated[e] = done ? 1 : 0;
-        const double ret = P.st.ep_return[e] + total;
-        const int len = P.st.ep_len[e] + 1;
+        const double ret = (PF ? pf_ret : P.st.ep_return[e]) + total;
+        const int len = (PF ? pf_len : P.st.ep_len[e]) + 1;
         P.st.ep_return[e] = ret;
         P.st.ep_len[e] = len;
         if (done) P.st.flags[e] |= FLAG_NEEDS_RESET;
@@ -1364,6 +1392,10 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
 #ifndef RT_FINISH_KG
 #define RT_FINISH_KG 1
 #endif
+// k_finish's early loads of the tail's scalars (finish_env PF; A/B builds)
+#ifndef RT_FINISH_PF
+#define RT_FINISH_PF 1
+#endif
 // RT_CHAIN_PRIO (A/B builds): wave issue priority (s_setprio) of the latency
 // chain's kernels (k_finish, k_step_policy) against the co-running dose stream
 #ifndef RT_CHAIN_PRIO
@@ -1375,7 +1407,7 @@ __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
     const int e = P.e_begin + blockIdx.x * P.wpb + w;
     if (e >= P.N) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm_raw[];
-    finish_env<RT_FINISH_KG>(P, e, lane, fsm_raw + (size_t)w * P.wave_lds);
+    finish_env<RT_FINISH_KG, RT_FINISH_PF != 0>(P, e, lane, fsm_raw + (size_t)w * P.wave_lds);
 }
 
 // ---------------------------------------------------------------------------
