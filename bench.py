@@ -330,8 +330,8 @@ def stream_ceilings(dev, lib_obj, gib: float = 4.0, reps: int = 8) -> dict:
 
 
 PMC_FILE = os.path.join(REPO, "profiles", "r03", "r03_s2_k_dense_persist_pmc.json")
-# rocprofv3 --kernel-trace --stats of this bench's default command (tools/archive/r03/gpu_r03_s41.sh)
-ROCPROF_FILE = os.path.join(REPO, "profiles", "r03", "r03_s41_kernel_stats.csv")
+# rocprofv3 --kernel-trace --stats of this bench's default command (tools/archive/r03/gpu_r03_s43.sh)
+ROCPROF_FILE = os.path.join(REPO, "profiles", "r03", "r03_s43_kernel_stats.csv")
 
 
 def load_rocprof(kernel: str):
