@@ -303,7 +303,7 @@ int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
  * the group streams write after each policy/march kernel
  * (hipStreamWriteValue64) and publishing per-turn completion counts the
  * groups' k_finish launches wait on (hipStreamWaitValue64).  Same bits as
- * mode 0.  A hand-off wait that exceeds 0.2 s (a stream operation that never
+ * mode 0.  A hand-off wait that exceeds 2 s (a stream operation that never
  * arrived) makes the launch drain and the next rollout call return
  * RT_EDEVICE.  RT_EINVAL for a handle without the pipelined rollout (vision,
  * incremental or C-order dose rows).  The first call with 1 creates the dose

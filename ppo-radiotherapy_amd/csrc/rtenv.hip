@@ -2662,7 +2662,7 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
         R.done_cnt = env->seq_d + kMaxRolloutGroups * kSeqStride;
         for (int g = 0; g < G; ++g) R.beam_base[g] = env->beam_next[g];
         R.err = env->err_h;
-        R.timeout_ticks = 20000000;  // 0.2 s at 100 MHz
+        R.timeout_ticks = 200000000;  // 2 s at 100 MHz: only a stream op that never comes waits this long
         RT_HIP(hipStreamWaitEvent(env->dstream, env->pev[0], 0));
         hipEvent_t* ev = next_timing_slot(env);
         if (ev) (void)hipEventRecord(ev[0], env->dstream), (void)hipEventRecord(ev[1], env->dstream);
