@@ -118,14 +118,11 @@ def parse():
     ap.add_argument("--rollout-groups", type=int, default=2, choices=[0, 1, 2, 3, 4],
                     help="dense mode: env groups of the rollout call (2 = two pipelined streams, "
                          "0 = one persistent launch with a per-env dense pass)")
-    ap.add_argument("--dense-handoff", type=int, default=0, choices=[0, 1],
-                    help="dense pipelined rollout: 0 = a k_dense launch per group turn (events), "
-                         "1 = one k_dense_rollout launch per call gated by device hand-off words")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
     ap.add_argument("--conv-precision", choices=["f32", "bf16x3"], default="f32",
                     help="vision: conv1's forward products (rt_conv_set_precision) in the rollout and the update")
-    ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="bf16x3",
+    ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="f32",
                     help="the fused update's 64x64 layer products (ppo_update_ms); the other is timed beside it")
     ap.add_argument("--rehearse-same-device", action="store_true",
                     help="multi-rank rehearsal on one GPU: every rank on cuda:0, gloo instead of RCCL")
@@ -193,17 +190,31 @@ def run_steps(tr, k: int):
         i += c
 
 
+def stagger_phases(tr, env, dev):
+    """Spread the envs' episode clocks uniformly over the 100-step episode: a
+    100-step pre-roll resets the envs with e % 100 == k at pre-roll step k
+    (masked rt_env_reset), so from then on every rollout step carries ~1 % of
+    the envs through the t = 100 truncation autoreset (a RESET zeroes the
+    env's whole dose row) -- the steady state of a long run (train.py:138-161
+    with every env autoresetting inside the rollout), which a window started
+    right after reset() never reaches."""
+    import torch
+
+    N = env.num_envs
+    e_idx = torch.arange(N, device=dev)
+    for k in range(100):
+        env.reset(options={"mask": (e_idx % 100) == k})
+        tr.rollout_steps(k % tr.T, 1)
+
+
 def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int = 2):
-    """Env steps/s over a window of calls x T (>= 101) rollout steps with the
-    envs' episode clocks spread uniformly: a 100-step pre-roll resets the envs
-    with e % 100 == k at pre-roll step k (masked rt_env_reset), so every step
-    of the window carries ~1 % of the envs through the t = 100 truncation
-    autoreset (a RESET zeroes the env's whole dose row) -- the steady state of
-    a long run, which a window started right after reset() never reaches.
-    Nothing but the rollout calls runs inside the timed windows; the autoreset
-    count and the kernel times come from a fourth, instrumented window.  A
-    one-block rt_probe_stream launch before each window marks it in a
-    rocprofv3 kernel trace (tools/steady_trace.py)."""
+    """Env steps/s over three back-to-back windows of calls x T (>= 101)
+    rollout steps each, on the staggered episode phases stagger_phases set up
+    before the warmup (the phases stay staggered: every env autoresets on its
+    own clock).  Nothing but the rollout calls runs inside the timed windows;
+    the autoreset count and the kernel times come from a fourth, instrumented
+    window.  A one-block rt_probe_stream launch before each window marks it in
+    a rocprofv3 kernel trace (tools/window_kernels.py)."""
     import torch
 
     from ppo_radiotherapy_amd import _lib
@@ -215,11 +226,7 @@ def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int =
         _lib.check(L.rt_probe_stream(mark_buf.data_ptr(), mark_buf.data_ptr(), 4, 0, 1, _lib.stream_handle()),
                    "marker")
 
-    N, T = env.num_envs, tr.T
-    e_idx = torch.arange(N, device=dev)
-    for k in range(100):
-        env.reset(options={"mask": (e_idx % 100) == k})
-        tr.rollout_steps(k % T, 1)
+    T = tr.T
     K = calls * T
     # three back-to-back windows (the phases stay staggered); the median is reported
     dts = []
@@ -248,7 +255,27 @@ def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int =
             "windows_env_steps_per_s": [total_envs * K / d for d in dts],
             "kernel_ms_per_step": {k: v * kcalls / K for k, v in kms.items()},
             "autoresets_in_window": int(resets.item()),
-            "episode_phase": "staggered uniformly over the 100-step episode (masked resets in a 100-step pre-roll)"}
+            "episode_phase": "staggered uniformly over the 100-step episode (stagger_phases before the warmup)"}
+
+
+def march_lines(env):
+    """Distinct 128-B dose lines the march read-modify-writes per env-step
+    (draw_line.py:49-100 splats applied by environment.py:107-110), counted on
+    the beams the envs applied last (rt_env_beam_list), at the dose-row
+    positions the library stores them (lung-first rows: rt_env_dose_index).
+    Envs whose last call was a reset count 0 (they marched nothing)."""
+    import torch
+
+    idx, _, cnt = env.beam_list()
+    cap = idx.shape[1]
+    valid = torch.arange(cap, device=idx.device)[None, :] < cnt.clamp_min(0)[:, None]
+    pos = env.dose_index()
+    if pos is not None:
+        idx = pos.long()[idx.long().clamp(0, pos.numel() - 1)]
+    lines = torch.where(valid, idx.long() // 32, torch.full_like(idx.long(), -1))
+    lines, _ = lines.sort(dim=1)
+    distinct = ((lines[:, 1:] != lines[:, :-1]) & (lines[:, 1:] >= 0)).sum(1) + (lines[:, 0] >= 0).long()
+    return float(distinct.double().mean())
 
 
 def incremental_transactions(env, lib):
@@ -560,8 +587,6 @@ def main():
                              env_id_base=rank * a.envs, step_mode=a.step_mode)
     if not a.vision and a.step_mode == "dense":
         env.set_rollout_groups(a.rollout_groups)
-        if a.rollout_groups > 1:
-            env.set_dense_handoff(a.dense_handoff)
     torch.manual_seed(a.seed)
     if a.vision:  # conv1's arithmetic: the trainer sets it from cfg.conv_precision
         agent = PPO_3DCNN((4, *grid), (6,), 64).to(dev)
@@ -574,6 +599,10 @@ def main():
     tr = PPOTrainer(cfg, env, agent, dev, rank, world, gen)
     tr.reset()
     T = tr.T
+    if not a.vision and not a.env_only:
+        # every timed window below runs on staggered episode phases, as a long
+        # run does (autoresets and their dose-row zeroing inside the window)
+        stagger_phases(tr, env, dev)
 
     # ---------------- warmup: W untimed rollout steps around one untimed
     # update (its kernels warm too), so the timed pass follows rollout steps
@@ -721,17 +750,8 @@ def main():
         bytes_model = ("20 B x V x envs (k_dense_vis: dose read, the four observation channels written -- "
                        "lungs and dose, tumour and beam-view zeroed for k_finish's scatter)")
     persistent_dense = (not a.vision and not a.env_only and a.step_mode == "dense" and a.rollout_groups == 0)
-    dev_handoff = (not a.vision and not a.env_only and a.step_mode == "dense" and a.rollout_groups > 1
-                   and a.dense_handoff == 1)
     launches = max(kcalls, 1) / K  # launches per step (2: pipelined env groups; 1/K: one persistent launch)
-    if dev_handoff:
-        # one k_dense_rollout launch per rollout call streams every group's
-        # turn of every step: its whole duration (hand-off waits included)
-        # against the lung segments of all envs and steps of the call
-        dense_ms = kms["k_dense"]
-        kernel_name = "k_dense_rollout"
-        traffic = load_pmc(grid, a.envs, "k_dense_rollout")
-    elif persistent_dense:
+    if persistent_dense:
         # one k_rollout_policy<dense> launch per rollout call: each wave streams
         # its env's lung segment every step (dense_env); its whole duration is
         # in the first interval, and its bytes are the dense stream's
@@ -876,8 +896,6 @@ def main():
         if a.conv_precision != "f32":
             out["dtype"] = "f32 (conv1 forward bf16x3)"
     out["rollout_groups"] = a.rollout_groups if a.step_mode == "dense" and not a.vision else 1
-    out["dense_handoff"] = "device" if (a.step_mode == "dense" and not a.vision and a.rollout_groups > 1
-                                        and a.dense_handoff == 1) else "events"
     if other is not None:
         out["other_step_mode"] = other
     out["roofline"] = roof

@@ -41,7 +41,8 @@
 extern "C" {
 #endif
 
-#define RTENV_ABI_VERSION 2  /* 2: rt_env_config.struct_size (first member) */
+#define RTENV_ABI_VERSION 3  /* 2: rt_env_config.struct_size (first member); 3: rt_adam_step grad_div,
+                                rt_env_set_dense_handoff removed */
 
 enum {
     RT_OK = 0,
@@ -295,20 +296,6 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* 
  * returns RT_ELIMIT only when the per-wave LDS region cannot hold even the
  * policy's activations. */
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
-/* How the pipelined dense rollout (groups >= 2) hands the dose stream from
- * one env group's turn to the next: 0 (default) = one persistent k_dense launch
- * per group and step, turns ordered by events; 1 = device hand-off: ONE
- * k_dense_rollout launch per rt_env_rollout_policy call streams every group's
- * turn of every step on a library dose stream, gated by hand-off words that
- * the group streams write after each policy/march kernel
- * (hipStreamWriteValue64) and publishing per-turn completion counts the
- * groups' k_finish launches wait on (hipStreamWaitValue64).  Same bits as
- * mode 0.  A hand-off wait that exceeds 2 s (a stream operation that never
- * arrived) makes the launch drain and the next rollout call return
- * RT_EDEVICE.  RT_EINVAL for a handle without the pipelined rollout (vision,
- * incremental or C-order dose rows).  The first call with 1 creates the dose
- * stream -- a setup call, not graph-capturable. */
-int rt_env_set_dense_handoff(rt_env* env, int32_t mode);
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */
@@ -372,9 +359,14 @@ int rt_ppo_grad(const float* const* params_d, float* const* grads_d, const rt_pp
 
 /* nn.utils.clip_grad_norm_(max_grad_norm) + torch.optim.Adam step number
  * `step` (foreach op order) over flat parameter / gradient / state buffers.
- * workspace_d: >= 256 floats of device scratch (the norm partials). */
+ * grad_div >= 1: the gradient is first divided by it (IEEE division, as
+ * torch's grad.div_(grad_div)): the world size after a data-parallel SUM
+ * all-reduce, so the average needs no kernel of its own; 1 = as is.  grad_d
+ * holds the divided, clipped gradient afterwards.  workspace_d: >= 256 floats
+ * of device scratch (the norm partials). */
 int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp_avg_d, float* exp_avg_sq_d,
-                 int64_t step, double lr, const rt_ppo_hparams* hp, float* workspace_d, void* stream);
+                 int64_t step, double lr, const rt_ppo_hparams* hp, int32_t grad_div, float* workspace_d,
+                 void* stream);
 
 /* n_minibatches consecutive optimizer steps (rt_ppo_grad + rt_adam_step) on
  * the minibatches perm_d[i*mb_size, (i+1)*mb_size) -- of one epoch, or of
@@ -382,8 +374,7 @@ int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp_avg_d, flo
  * adv_stats_d then holding [n_minibatches][2] (single process; data-parallel
  * callers interleave rt_ppo_grad, the all-reduce and rt_adam_step themselves).
  * params_d / grads_d are views of flat_param_d / flat_grad_d; the first step
- * is numbered step0.  Uses the workspace's last float as scratch (the arrival
- * counter of the opt-in fused reduce + Adam launch, RT_PPO_FUSED_ADAM=1). */
+ * is numbered step0. */
 int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
                   const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches, const float* adv_stats_d,
                   const rt_ppo_hparams* hp, float* flat_param_d, float* flat_grad_d, float* exp_avg_d,

@@ -36,7 +36,7 @@ EXPORTS = [
     "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_env_beam_list", "rt_probe_random_rmw", "rt_probe_stream", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
-    "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups", "rt_env_set_dense_handoff",
+    "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_set_precision", "rt_ppo_get_precision", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
     "rt_ppo_shuffle", "rt_ppo_shuffle_epochs", "rt_ppo_adv_stats", "rt_ppo_adv_sums", "rt_ppo_adv_finalize",
     "rt_conv_set_precision", "rt_conv_get_precision", "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
@@ -49,7 +49,7 @@ class RtError(RuntimeError):
     pass
 
 
-ABI_VERSION = 2  # RTENV_ABI_VERSION of include/rtenv.h
+ABI_VERSION = 3  # RTENV_ABI_VERSION of include/rtenv.h
 
 
 class RtEnvConfig(ctypes.Structure):
@@ -172,14 +172,13 @@ def load(build_if_missing: bool = True):
         "rt_env_step_policy": ([vp, ctypes.POINTER(RtPolicyStep), vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_env_rollout_policy": ([vp, ctypes.POINTER(RtPolicyRollout), vp, vp, vp], ctypes.c_int),
         "rt_env_set_rollout_groups": ([vp, i32], ctypes.c_int),
-        "rt_env_set_dense_handoff": ([vp, i32], ctypes.c_int),
         "rt_ppo_workspace_floats": ([i32], i64),
         "rt_ppo_num_params": ([], i32),
         "rt_ppo_set_precision": ([i32], ctypes.c_int),
         "rt_ppo_get_precision": ([], i32),
         "rt_ppo_grad": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, vp,
                          ctypes.POINTER(RtPpoHparams), vp, i64, vp, vp, vp], ctypes.c_int),
-        "rt_adam_step": ([i64, vp, vp, vp, vp, i64, f64, ctypes.POINTER(RtPpoHparams), vp, vp], ctypes.c_int),
+        "rt_adam_step": ([i64, vp, vp, vp, vp, i64, f64, ctypes.POINTER(RtPpoHparams), i32, vp, vp], ctypes.c_int),
         "rt_ppo_update": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, i32, vp,
                            ctypes.POINTER(RtPpoHparams), vp, vp, vp, vp, i64, i64, f64, vp, i64, vp, vp, vp],
                           ctypes.c_int),

@@ -10,19 +10,15 @@
 // autograd backward, clip, foreach Adam); on a 64-wide MLP every one of them
 // is launch- and latency-bound.  Here it is three kernels:
 //
-//   k_ppo_grad    one 512-thread block per 64 samples: gathers the minibatch
-//                 rows, runs both MLPs forward, evaluates the PPO loss and its
-//                 derivative per sample in closed form, back-propagates
-//                 through both MLPs (all activations in LDS) and writes the
-//                 block's partial weight gradients + loss statistics;
-//   k_ppo_reduce  sums the block partials column-wise (fixed order:
-//                 deterministic) into the flat gradient bucket;
-//   k_clip_adam   one block: global grad norm, clip, Adam update over the flat
-//                 parameter / state buffers, in torch's foreach-Adam op order.
-//
-// GEMM shapes per block are 64 x 64 x 64; tiles are mapped so that one
-// wavefront shares an 8-sample group (broadcast LDS reads) and each lane owns a
-// hidden unit (bank-distinct reads of 68-float padded rows).
+//   k_ppo_grad_mfma  512-thread blocks of 4 (actor, critic) wave pairs over
+//                    16-sample tiles: gathers the minibatch rows, runs both MLPs
+//                    forward, the PPO loss derivative per sample in closed form
+//                    and the backward on MFMA, one partial gradient row per block;
+//   k_ppo_reduce     sums the block partials column-wise (fixed order:
+//                    deterministic) into the flat gradient bucket, plus the
+//                    ||g||^2 partials of the clip;
+//   k_adam           clip_grad_norm_ + Adam over the flat parameter / state
+//                    buffers, in torch's foreach-Adam op order.
 #include "rt_trace.h"
 #include <hip/hip_runtime.h>
 
@@ -41,14 +37,6 @@ namespace {
 constexpr int H = 64;
 constexpr int NOBS = 9;
 constexpr int NACT = 6;
-constexpr int TS = 64;          // samples per block
-constexpr int HP = H + 4;       // padded LDS row stride
-constexpr int kThreads = 512;             // 8 waves: 2 per SIMD (the LDS footprint allows 1 block per CU)
-constexpr int NW = kThreads / 64;          // wavefronts per block
-constexpr int SPW = TS / NW;               // samples per wavefront in the sample-major phases
-constexpr int LPS = kThreads / TS;         // lanes per sample in the per-sample phases
-constexpr int UPL = H / LPS;               // hidden units per lane there
-constexpr int CPW = H / NW;                // layer-2 weight-gradient columns per wavefront
 constexpr float kHalfLog2Pi = 0.91893853320467274f;
 
 // parameter offsets, policy order (include/rtenv.h RT_PPO_*)
@@ -85,286 +73,16 @@ struct GradParams {
     float* ws;  // [gridDim.x][PSTRIDE]
 };
 
-// ---- forward of one MLP trunk: H1 = tanh(X W1^T + b1), H2 = tanh(H1 W2^T + b2)
-// thread (j = tid % 64, sample group sg = tid / 64: one wavefront per SPW samples)
-__device__ __forceinline__ void trunk_fwd(const float* w1, const float* b1, const float* w2, const float* b2,
-                                          const float* X, float* H1, float* H2, int tid) {
-    const int j = tid & 63, sg = tid >> 6;
-    float wr[NOBS];
-#pragma unroll
-    for (int i = 0; i < NOBS; ++i) wr[i] = w1[j * NOBS + i];
-#pragma unroll 4
-    for (int v = 0; v < SPW; ++v) {
-        const int s = sg * SPW + v;
-        float a = 0.0f;
-#pragma unroll
-        for (int i = 0; i < NOBS; ++i) a += wr[i] * X[s * NOBS + i];
-        H1[s * HP + j] = tanhf(a + b1[j]);
-    }
-    __syncthreads();
-    float acc[SPW];
-#pragma unroll
-    for (int v = 0; v < SPW; ++v) acc[v] = 0.0f;
-    for (int i4 = 0; i4 < H / 4; ++i4) {
-        const float4 w = *reinterpret_cast<const float4*>(&w2[j * HP + 4 * i4]);
-#pragma unroll
-        for (int v = 0; v < SPW; ++v) {
-            const float4 h = *reinterpret_cast<const float4*>(&H1[(sg * SPW + v) * HP + 4 * i4]);
-            acc[v] += w.x * h.x + w.y * h.y + w.z * h.z + w.w * h.w;
-        }
-    }
-#pragma unroll
-    for (int v = 0; v < SPW; ++v) H2[(sg * SPW + v) * HP + j] = tanhf(acc[v] + b2[j]);
-    __syncthreads();
-}
-
-// head outputs of sample s = tid / LPS (its LPS lanes q own units UPL*q .. UPL*q+UPL-1)
-template <int NOUT>
-__device__ __forceinline__ void head_fwd(const float* w3, const float* b3, const float* H2, int tid, float out[NOUT]) {
-    const int s = tid / LPS, q = tid % LPS;
-#pragma unroll
-    for (int k = 0; k < NOUT; ++k) {
-        float p = 0.0f;
-#pragma unroll
-        for (int c = 0; c < UPL; ++c) p += w3[k * H + UPL * q + c] * H2[s * HP + UPL * q + c];
-#pragma unroll
-        for (int off = 1; off < LPS; off <<= 1) p += __shfl_xor(p, off, 64);
-        out[k] = p + b3[k];
-    }
-}
-
-// ---- backward of one head + trunk; GOUT[s][k] = dL/d out_k (row stride 8).
-// Writes the block's partial gradients of W1 b1 W2 b2 W3 b3 at the given offsets.
-// H1 is overwritten by dL/d(pre-activation of layer 1).
-template <int NOUT>
-__device__ __forceinline__ void trunk_bwd(const float* w2, const float* w3, const float* X, float* H1,
-                                          const float* H2, float* G2, const float* GOUT, int tid, float* out,
-                                          int o_w1, int o_b1, int o_w2, int o_b2, int o_w3, int o_b3) {
-    const int j = tid & 63, wq = tid >> 6;
-    // dW3[k][j] = sum_s GOUT[s][k] H2[s][j];  db3[k] = sum_s GOUT[s][k]
-    for (int k = wq; k < NOUT; k += NW) {
-        float a = 0.0f;
-        for (int s = 0; s < TS; ++s) a += GOUT[s * 8 + k] * H2[s * HP + j];
-        out[o_w3 + k * H + j] = a;
-    }
-    if (tid < NOUT) {
-        float a = 0.0f;
-        for (int s = 0; s < TS; ++s) a += GOUT[s * 8 + tid];
-        out[o_b3 + tid] = a;
-    }
-    // G2[s][j] = (sum_k GOUT[s][k] W3[k][j]) * (1 - H2^2)
-    {
-        float w3r[NOUT];
-#pragma unroll
-        for (int k = 0; k < NOUT; ++k) w3r[k] = w3[k * H + j];
-#pragma unroll 4
-        for (int v = 0; v < SPW; ++v) {
-            const int s = wq * SPW + v;
-            float g = 0.0f;
-#pragma unroll
-            for (int k = 0; k < NOUT; ++k) g += GOUT[s * 8 + k] * w3r[k];
-            const float h = H2[s * HP + j];
-            G2[s * HP + j] = g * (1.0f - h * h);
-        }
-    }
-    __syncthreads();
-    // dW2[j][i] = sum_s G2[s][j] H1[s][i]  (lane j, wave wq owns i = CPW*wq ..); db2[j]
-    {
-        float acc[CPW];
-#pragma unroll
-        for (int c = 0; c < CPW; ++c) acc[c] = 0.0f;
-        float bsum = 0.0f;
-        for (int s = 0; s < TS; ++s) {
-            const float g = G2[s * HP + j];
-            bsum += g;
-            const float4* hr = reinterpret_cast<const float4*>(&H1[s * HP + CPW * wq]);
-#pragma unroll
-            for (int c4 = 0; c4 < CPW / 4; ++c4) {
-                const float4 h = hr[c4];
-                acc[4 * c4 + 0] += g * h.x;
-                acc[4 * c4 + 1] += g * h.y;
-                acc[4 * c4 + 2] += g * h.z;
-                acc[4 * c4 + 3] += g * h.w;
-            }
-        }
-        float4* dst = reinterpret_cast<float4*>(out + o_w2 + j * H + CPW * wq);  // o_w2 % 4 == 0
-#pragma unroll
-        for (int c4 = 0; c4 < CPW / 4; ++c4)
-            dst[c4] = make_float4(acc[4 * c4], acc[4 * c4 + 1], acc[4 * c4 + 2], acc[4 * c4 + 3]);
-        if (wq == 0) out[o_b2 + j] = bsum;
-    }
-    __syncthreads();
-    // G1[s][i] = (sum_j G2[s][j] W2[j][i]) * (1 - H1^2), in place of H1 (lane i, wave = sample group)
-    {
-        const int i = j;
-        float acc[SPW];
-#pragma unroll
-        for (int v = 0; v < SPW; ++v) acc[v] = 0.0f;
-        for (int j4 = 0; j4 < H / 4; ++j4) {
-            const float wa = w2[(4 * j4 + 0) * HP + i], wb = w2[(4 * j4 + 1) * HP + i];
-            const float wc = w2[(4 * j4 + 2) * HP + i], wd = w2[(4 * j4 + 3) * HP + i];
-#pragma unroll
-            for (int v = 0; v < SPW; ++v) {
-                const float4 g = *reinterpret_cast<const float4*>(&G2[(wq * SPW + v) * HP + 4 * j4]);
-                acc[v] += g.x * wa + g.y * wb + g.z * wc + g.w * wd;
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < SPW; ++v) {
-            const int s = wq * SPW + v;
-            const float h = H1[s * HP + i];
-            H1[s * HP + i] = acc[v] * (1.0f - h * h);
-        }
-    }
-    __syncthreads();
-    // dW1[j][i] = sum_s G1[s][j] X[s][i]  (i = wq, wq+NW, ...); db1[j] (wave NW-1)
-    for (int i = wq; i < NOBS; i += NW) {
-        float a = 0.0f;
-        for (int s = 0; s < TS; ++s) a += H1[s * HP + j] * X[s * NOBS + i];
-        out[o_w1 + j * NOBS + i] = a;
-    }
-    if (wq == NW - 1) {
-        float a = 0.0f;
-        for (int s = 0; s < TS; ++s) a += H1[s * HP + j];
-        out[o_b1 + j] = a;
-    }
-    __syncthreads();
-}
-
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
 }
 
-__global__ __launch_bounds__(kThreads) void k_ppo_grad(GradParams P) {
-    __shared__ __attribute__((aligned(16))) float aw1[H * NOBS], ab1[H], aw2[H * HP], ab2[H], aw3[NACT * H], ab3[8], ls[8];
-    __shared__ __attribute__((aligned(16))) float cw1[H * NOBS], cb1[H], cw2[H * HP], cb2[H], cw3[H], cb3[4];
-    __shared__ __attribute__((aligned(16))) float X[TS * NOBS], AH1[TS * HP], AH2[TS * HP], CH1[TS * HP],
-        CH2[TS * HP], G2[TS * HP];
-    __shared__ __attribute__((aligned(16))) float GM[TS * 8], GV[TS * 8];
-    __shared__ float red[NW][16];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < H * NOBS; i += kThreads) {
-        aw1[i] = P.w.p[0][i];
-        cw1[i] = P.w.p[7][i];
-    }
-    for (int i = tid; i < H * H; i += kThreads) {
-        aw2[(i >> 6) * HP + (i & 63)] = P.w.p[2][i];
-        cw2[(i >> 6) * HP + (i & 63)] = P.w.p[9][i];
-    }
-    for (int i = tid; i < H; i += kThreads) {
-        ab1[i] = P.w.p[1][i];
-        ab2[i] = P.w.p[3][i];
-        cb1[i] = P.w.p[8][i];
-        cb2[i] = P.w.p[10][i];
-        cw3[i] = P.w.p[11][i];
-    }
-    for (int i = tid; i < NACT * H; i += kThreads) aw3[i] = P.w.p[4][i];
-    if (tid < NACT) {
-        ab3[tid] = P.w.p[5][tid];
-        ls[tid] = P.w.p[6][tid];
-    }
-    if (tid == 0) cb3[0] = P.w.p[12][0];
-    // lanes LPS*s .. LPS*s+LPS-1 hold sample s
-    const int s = tid / LPS, q = tid % LPS;
-    const int m = blockIdx.x * TS + s;
-    const bool live = m < P.mb;
-    const int64_t row = live ? P.idx[m] : 0;
-    for (int i = q; i < NOBS; i += LPS) X[s * NOBS + i] = live ? P.obs[row * NOBS + i] : 0.0f;
-    __syncthreads();
-
-    trunk_fwd(aw1, ab1, aw2, ab2, X, AH1, AH2, tid);
-    float mean[NACT];
-    head_fwd<NACT>(aw3, ab3, AH2, tid, mean);
-    trunk_fwd(cw1, cb1, cw2, cb2, X, CH1, CH2, tid);
-    float value;
-    head_fwd<1>(cw3, cb3, CH2, tid, &value);
-
-    // ---- per-sample PPO loss and its derivative (train.py:200-236), every lane of the sample
-    float st[NSTAT + NACT];  // pg, vl, ent, -logratio, (r-1)-logratio, clipped, dL/dlogstd[6]
-#pragma unroll
-    for (int k = 0; k < NSTAT + NACT; ++k) st[k] = 0.0f;
-    float gm[NACT] = {0, 0, 0, 0, 0, 0}, gv = 0.0f;
-    if (live) {
-        const float inv_n = 1.0f / (float)P.mb;
-        float z[NACT], sd[NACT], logp = 0.0f, ent = 0.0f;
-#pragma unroll
-        for (int k = 0; k < NACT; ++k) {
-            sd[k] = expf(ls[k]);
-            z[k] = (P.act[row * NACT + k] - mean[k]) / sd[k];
-            logp += -0.5f * z[k] * z[k] - ls[k] - kHalfLog2Pi;
-            ent += 0.5f + kHalfLog2Pi + ls[k];
-        }
-        const float lr = logp - P.logp[row];
-        const float r = expf(lr);
-        float A = P.adv[row];
-        if (P.adv_stats) A = (A - P.adv_stats[0]) / (P.adv_stats[1] + 1e-8f);
-        const float pg1 = -A * r;
-        const float rc = fminf(fmaxf(r, P.clip_lo), P.clip_hi);
-        const float pg2 = -A * rc;
-        // torch.maximum backward: the larger input takes the gradient, ties split it
-        const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
-        const float w2 = pg2 > pg1 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
-        const float pass = (r >= P.clip_lo && r <= P.clip_hi) ? 1.0f : 0.0f;  // clamp backward
-        const float g_logp = inv_n * (w1 * -A + w2 * -A * pass) * r;
-#pragma unroll
-        for (int k = 0; k < NACT; ++k) {
-            gm[k] = g_logp * z[k] / sd[k];
-            st[NSTAT + k] = g_logp * (z[k] * z[k] - 1.0f);
-        }
-        const float R = P.ret[row], V = P.val[row];
-        float vl, dv;
-        if (P.clip_vloss) {
-            const float d = value - V;
-            const float vc = V + fminf(fmaxf(d, -P.clip), P.clip);
-            const float vu = (value - R) * (value - R), vcc = (vc - R) * (vc - R);
-            vl = fmaxf(vu, vcc);
-            const float wu = vu > vcc ? 1.0f : (vu == vcc ? 0.5f : 0.0f);
-            const float wc = vcc > vu ? 1.0f : (vu == vcc ? 0.5f : 0.0f);
-            const float dpass = (d >= -P.clip && d <= P.clip) ? 1.0f : 0.0f;
-            dv = wu * 2.0f * (value - R) + wc * 2.0f * (vc - R) * dpass;
-        } else {
-            vl = (value - R) * (value - R);
-            dv = 2.0f * (value - R);
-        }
-        gv = P.vf_coef * 0.5f * inv_n * dv;
-        st[0] = fmaxf(pg1, pg2);
-        st[1] = vl;
-        st[2] = ent;
-        st[3] = -lr;
-        st[4] = (r - 1.0f) - lr;
-        st[5] = fabsf(r - 1.0f) > P.clip ? 1.0f : 0.0f;
-    }
-    if (q == 0) {
-#pragma unroll
-        for (int k = 0; k < NACT; ++k) GM[s * 8 + k] = gm[k];
-        GV[s * 8] = gv;
-    }
-    // block sums of the statistics and dL/dlogstd (one contribution per sample)
-#pragma unroll
-    for (int k = 0; k < NSTAT + NACT; ++k) {
-        const float v = wave_sum(q == 0 ? st[k] : 0.0f);
-        if ((tid & 63) == 0) red[tid >> 6][k] = v;
-    }
-    __syncthreads();
-    float* out = P.ws + (size_t)blockIdx.x * PSTRIDE;
-    if (tid < NSTAT + NACT) {
-        float v = 0.0f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) v += red[w][tid];
-        if (tid < NSTAT)
-            out[NP + tid] = v;
-        else
-            out[O_LS + tid - NSTAT] = v;
-    }
-    trunk_bwd<1>(cw2, cw3, X, CH1, CH2, G2, GV, tid, out, O_CW1, O_CB1, O_CW2, O_CB2, O_CW3, O_CB3);
-    trunk_bwd<NACT>(aw2, aw3, X, AH1, AH2, G2, GM, tid, out, O_AW1, O_AB1, O_AW2, O_AB2, O_AW3, O_AB3);
-}
-
 // ============================================================================
-// k_ppo_grad_mfma: the same computation on f32 MFMA (v_mfma_f32_16x16x4_f32,
-// exact f32 FMA chains).
+// k_ppo_grad_mfma: the minibatch gradient on f32 MFMA (v_mfma_f32_16x16x4_f32,
+// exact f32 FMA chains; round 1's VALU kernel, 64 samples per block in LDS,
+// measured slower and was removed).
 //
 // The PPO loss separates by head: the clipped surrogate and the entropy depend
 // only on actor_mean / actor_logstd, the value loss only on the critic.  A
@@ -1185,15 +903,9 @@ __global__ __launch_bounds__(MT) void k_ppo_grad_mfma(GradParams P) {
 }
 
 int grad_blocks(int mb) {
-    // RT_PPO_GRAD_BLOCKS caps the grid (tiles-per-wave experiments)
-    static const int cap = [] {
-        const char* e = std::getenv("RT_PPO_GRAD_BLOCKS");
-        const int v = e ? std::atoi(e) : 0;
-        return v > 0 && v < kMaxGradBlocks ? v : kMaxGradBlocks;
-    }();
     const int tiles = (mb + 15) / 16;
     const int b = (tiles + NPAIR - 1) / NPAIR;
-    return b < cap ? b : cap;
+    return b < kMaxGradBlocks ? b : kMaxGradBlocks;
 }
 
 constexpr int kReduceCols = 64;
@@ -1259,12 +971,17 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(ReduceParams P) {
     if (lane == 0 && P.norm_part) P.norm_part[blockIdx.x] = sq;
 }
 
-// ||grad||^2 partials of a flat gradient (after a data-parallel all-reduce)
-__global__ __launch_bounds__(256) void k_gnorm(const float* g, int64_t n, int64_t per_block, float* norm_part) {
+// ||grad / div||^2 partials of a flat gradient after a data-parallel SUM
+// all-reduce (div = world size: the average, torch's grad.div_(world))
+__global__ __launch_bounds__(256) void k_gnorm(const float* g, int64_t n, int64_t per_block, float div,
+                                               float* norm_part) {
     __shared__ float part[4];
     float a = 0.0f;
     const int64_t lo = (int64_t)blockIdx.x * per_block, hi = lo + per_block < n ? lo + per_block : n;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) a += g[i] * g[i];
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const float x = div != 1.0f ? g[i] / div : g[i];
+        a += x * x;
+    }
     a = wave_sum(a);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
     __syncthreads();
@@ -1285,6 +1002,7 @@ struct AdamParams {
     float step_size;  // -lr / (1 - beta1^t)
     float bc2_sqrt;   // sqrt(1 - beta2^t)
     float eps;
+    float grad_div;   // the gradient is divided by this first (1: as is; world size: DP average)
 };
 
 // clip_grad_norm_ + torch.optim.Adam (foreach op order), one element per
@@ -1303,7 +1021,8 @@ __global__ __launch_bounds__(256) void k_adam(AdamParams P) {
     const float coef = coef_s;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= P.n) return;
-    const float g = P.grad[i] * coef;
+    const float g0 = P.grad_div != 1.0f ? P.grad[i] / P.grad_div : P.grad[i];  // IEEE division
+    const float g = g0 * coef;
     P.grad[i] = g;
     float m = P.m[i];
     m = m + P.lerp_w * (g - m);                   // exp_avg.lerp_(grad, 1 - beta1)
@@ -1313,129 +1032,6 @@ __global__ __launch_bounds__(256) void k_adam(AdamParams P) {
     P.param[i] = P.param[i] + P.step_size * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
     P.m[i] = m;
     P.v[i] = v;
-}
-
-// ---- k_ppo_reduce + k_adam in one launch (opt-in, RT_PPO_FUSED_ADAM=1) ------
-// Every block reduces its 64 columns as k_ppo_reduce does; the block whose
-// arrival on a counter comes last then runs the clip and the Adam step of all
-// parameters (k_adam's arithmetic, same bits).  The hand-off is
-// MI355X_MICROARCH.md's first measured row (no release fence, whose L2
-// write-back made the first fused version slower): the gradient
-// and the norm partials are stored `sc1`, every wave waits for its stores
-// (`s_waitcnt vmcnt(0)`), a workgroup barrier, ONE lane's agent-scope atomic
-// add; the block whose add returns nblk - 1 reads them back with `sc1` loads
-// -- its adding wave after the add returned, the others after a workgroup
-// barrier.  One block per CU (the LDS request below), hipMalloc'd memory.
-// The counter (the workspace's last norm slot) is zeroed by rt_ppo_update
-// before its first launch and re-armed by the last block.
-struct ReduceAdamParams {
-    ReduceParams R;
-    AdamParams A;
-    unsigned* counter;
-};
-
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-constexpr int kReduceAdamLds = 96 * 1024;  // > 80 KiB: one block per CU (the hand-off's measured condition)
-
-__global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
-    extern __shared__ float dyn[];
-    float (*part)[kReduceCols] = reinterpret_cast<float (*)[kReduceCols]>(dyn);
-    __shared__ int last_s;
-    __shared__ float coef_s;
-    const ReduceParams& P = Q.R;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int p = blockIdx.x * kReduceCols + lane;
-    const bool ok = p < NP + NSTAT;
-    float x[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int b = w + 16 * k;
-        x[k] = (ok && b < P.nblk) ? P.ws[(size_t)b * PSTRIDE + p] : 0.0f;
-    }
-#pragma unroll
-    for (int h = 8; h > 0; h >>= 1)
-#pragma unroll
-        for (int k = 0; k < h; ++k) x[k] += x[k + h];
-    part[w][lane] = x[0];
-    __syncthreads();
-    if (w == 0) {
-        float a = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) a += part[k][lane];
-        float sq = 0.0f;
-        if (ok) {
-            if (p < NP) {
-                int t = 0;
-#pragma unroll
-                for (int k = 1; k < 13; ++k) t += p >= kTensorOff[k] ? 1 : 0;
-                if (t == 6) a += -P.ent_coef;
-                st_sc1(&P.grad.p[t][p - kTensorOff[t]], a);
-                sq = a * a;
-            } else {
-                const int k = p - NP;
-                float v = a * P.inv_n;
-                if (k == 1) v *= 0.5f;
-                P.stats[k] = v;
-                if (P.stats_accum) P.stats_accum[k] += v;
-            }
-        }
-        sq = wave_sum(sq);
-        if (lane == 0) st_sc1(&P.norm_part[blockIdx.x], sq);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-        last_s = __hip_atomic_fetch_add(Q.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (unsigned)(gridDim.x - 1);
-    __syncthreads();
-    if (!last_s) return;
-    // ---- the last block: clip coefficient, then Adam over all parameters
-    const AdamParams& A = Q.A;
-    if (threadIdx.x < 64) {
-        float t = 0.0f;
-        if (A.max_norm > 0.0f)
-            for (int k = threadIdx.x; k < A.n_part; k += 64) t += ld_sc1(&A.norm_part[k]);
-        t = wave_sum(t);
-        if (threadIdx.x == 0) {
-            coef_s = A.max_norm > 0.0f ? fminf(A.max_norm / (sqrtf(t) + 1e-6f), 1.0f) : 1.0f;
-            __hip_atomic_store(Q.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-        }
-    }
-    __syncthreads();
-    const float coef = coef_s;
-    constexpr int U = (NP + 1023) / 1024;  // 10 parameters per thread, loads in flight together
-    float g[U], m[U], v[U], q[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int i = u * 1024 + threadIdx.x;
-        if (i < A.n) {
-            g[u] = ld_sc1(&A.grad[i]);
-            m[u] = A.m[i];
-            v[u] = A.v[i];
-            q[u] = A.param[i];
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int i = u * 1024 + threadIdx.x;
-        if (i >= A.n) continue;
-        const float gc = g[u] * coef;
-        A.grad[i] = gc;
-        float mm = m[u];
-        mm = mm + A.lerp_w * (gc - mm);
-        float vv = v[u] * A.beta2;
-        vv = vv + A.one_minus_beta2 * gc * gc;
-        const float denom = sqrtf(vv) / A.bc2_sqrt + A.eps;
-        A.param[i] = q[u] + A.step_size * (mm / denom);
-        A.m[i] = mm;
-        A.v[i] = vv;
-    }
 }
 
 // ---- per-epoch shuffle and minibatch advantage statistics ------------------
@@ -1576,15 +1172,6 @@ __global__ __launch_bounds__(256) void k_adv_finalize(const double* sums, int64_
     stats[2 * i + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
 }
 
-// RT_PPO_GRAD_KERNEL=valu selects the VALU kernel (A/B comparisons); default MFMA
-bool rt_ppo_use_mfma() {
-    static const int v = [] {
-        const char* e = std::getenv("RT_PPO_GRAD_KERNEL");
-        return (e && std::strcmp(e, "valu") == 0) ? 0 : 1;
-    }();
-    return v != 0;
-}
-
 // Arithmetic of k_ppo_grad_mfma's two 64x64 products (rt_ppo_set_precision;
 // the initial value from RT_PPO_PREC=f32|bf16x3, default f32)
 int g_ppo_prec = [] {
@@ -1592,24 +1179,12 @@ int g_ppo_prec = [] {
     return (e && std::strcmp(e, "bf16x3") == 0) ? kPrecBf16x3 : kPrecF32;
 }();
 
-// RT_PPO_FUSED_ADAM=1: rt_ppo_update launches k_ppo_reduce_adam instead of
-// k_ppo_reduce + k_adam -- bitwise the same update, measured slower (13.1 us
-// vs 5.1 + 5.6: the last block's Adam over all 10,061 parameters is
-// VALU-bound on one CU), kept for A/B runs
-bool use_reduce_adam() {
-    static const int v = [] {
-        const char* e = std::getenv("RT_PPO_FUSED_ADAM");
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    return v != 0;
-}
-
 ReduceParams reduce_params(float* const* grads_d, int32_t mb, const rt_ppo_hparams* hp, float* ws_d,
                            int64_t ws_floats, float* stats_d, float* accum_d) {
     ReduceParams R{};
     for (int i = 0; i < 13; ++i) R.grad.p[i] = grads_d[i];
     R.ws = ws_d;
-    R.nblk = rt_ppo_use_mfma() ? grad_blocks(mb) : (mb + TS - 1) / TS;
+    R.nblk = grad_blocks(mb);
     R.stats = stats_d;
     R.stats_accum = accum_d;
     R.norm_part = ws_d + (ws_floats - kNormSlots);
@@ -1620,10 +1195,8 @@ ReduceParams reduce_params(float* const* grads_d, int32_t mb, const rt_ppo_hpara
 
 int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* b,
                     const int64_t* idx_d, int32_t mb, const float* adv_stats_d, const rt_ppo_hparams* hp,
-                    float* ws_d, int64_t ws_floats, float* stats_d, float* accum_d, hipStream_t st,
-                    int with_reduce = 1) {
-    const bool use_mfma = rt_ppo_use_mfma();
-    const int nblk = use_mfma ? grad_blocks(mb) : (mb + TS - 1) / TS;
+                    float* ws_d, int64_t ws_floats, float* stats_d, float* accum_d, hipStream_t st) {
+    const int nblk = grad_blocks(mb);
     if ((int64_t)nblk * PSTRIDE + kNormSlots > ws_floats)
         return rt_internal_fail(RT_EINVAL, "rt_ppo_grad: workspace too small");
     GradParams G{};
@@ -1644,14 +1217,12 @@ int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const r
     G.clip_vloss = hp->clip_vloss;
     G.vf_coef = hp->vf_coef;
     G.ws = ws_d;
-    if (use_mfma && g_ppo_prec == kPrecBf16x3)
+    if (g_ppo_prec == kPrecBf16x3)
         hipLaunchKernelGGL(k_ppo_grad_mfma<kPrecBf16x3>, dim3(nblk), dim3(MT), 0, st, G);
-    else if (use_mfma)
-        hipLaunchKernelGGL(k_ppo_grad_mfma<kPrecF32>, dim3(nblk), dim3(MT), 0, st, G);
     else
-        hipLaunchKernelGGL(k_ppo_grad, dim3(nblk), dim3(kThreads), 0, st, G);
+        hipLaunchKernelGGL(k_ppo_grad_mfma<kPrecF32>, dim3(nblk), dim3(MT), 0, st, G);
     R = reduce_params(grads_d, mb, hp, ws_d, ws_floats, stats_d, accum_d);
-    if (with_reduce) hipLaunchKernelGGL(k_ppo_reduce, dim3(kReduceBlocks), dim3(1024), 0, st, R);
+    hipLaunchKernelGGL(k_ppo_reduce, dim3(kReduceBlocks), dim3(1024), 0, st, R);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
@@ -1660,7 +1231,7 @@ int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const r
 // norm_part: the kReduceBlocks partials k_ppo_reduce left (fresh = true), or
 // scratch for k_gnorm over the (all-reduced) flat gradient
 AdamParams adam_params(int64_t n, float* p, float* g, float* m, float* v, int64_t step, double lr,
-                       const rt_ppo_hparams* hp, float* norm_part) {
+                       const rt_ppo_hparams* hp, float* norm_part, float grad_div) {
     AdamParams A{};
     A.n = n;
     A.param = p;
@@ -1678,15 +1249,16 @@ AdamParams adam_params(int64_t n, float* p, float* g, float* m, float* v, int64_
     A.step_size = (float)(-(lr / (1.0 - std::pow(b1, (double)step))));
     A.bc2_sqrt = (float)std::pow(1.0 - std::pow(b2, (double)step), 0.5);
     A.eps = hp->adam_eps;
+    A.grad_div = grad_div;
     return A;
 }
 
 int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step, double lr,
-                const rt_ppo_hparams* hp, float* norm_part, bool fresh, hipStream_t st) {
-    const AdamParams A = adam_params(n, p, g, m, v, step, lr, hp, norm_part);
+                const rt_ppo_hparams* hp, float* norm_part, bool fresh, float grad_div, hipStream_t st) {
+    const AdamParams A = adam_params(n, p, g, m, v, step, lr, hp, norm_part, grad_div);
     if (A.max_norm > 0.0f && !fresh) {
         const int64_t per = (n + kReduceBlocks - 1) / kReduceBlocks;
-        hipLaunchKernelGGL(k_gnorm, dim3(kReduceBlocks), dim3(256), 0, st, g, n, per, norm_part);
+        hipLaunchKernelGGL(k_gnorm, dim3(kReduceBlocks), dim3(256), 0, st, g, n, per, grad_div, norm_part);
     }
     hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
     hipError_t e = hipGetLastError();
@@ -1710,8 +1282,7 @@ bool bad_batch(const rt_ppo_batch* b) {
 
 extern "C" int64_t rt_ppo_workspace_floats(int32_t minibatch_size) {
     if (minibatch_size < 1) return 0;
-    const int64_t a = (int64_t)((minibatch_size + TS - 1) / TS), b = grad_blocks(minibatch_size);
-    return (a > b ? a : b) * PSTRIDE + kNormSlots;
+    return (int64_t)grad_blocks(minibatch_size) * PSTRIDE + kNormSlots;
 }
 
 extern "C" int32_t rt_ppo_num_params(void) { return NP; }
@@ -1740,11 +1311,13 @@ extern "C" int rt_ppo_grad(const float* const* params_d, float* const* grads_d, 
 }
 
 extern "C" int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp_avg_d, float* exp_avg_sq_d,
-                            int64_t step, double lr, const rt_ppo_hparams* hp, float* workspace_d, void* stream) {
-    if (n < 1 || !param_d || !grad_d || !exp_avg_d || !exp_avg_sq_d || step < 1 || !hp || !workspace_d)
+                            int64_t step, double lr, const rt_ppo_hparams* hp, int32_t grad_div, float* workspace_d,
+                            void* stream) {
+    if (n < 1 || !param_d || !grad_d || !exp_avg_d || !exp_avg_sq_d || step < 1 || !hp || !workspace_d ||
+        grad_div < 1 || grad_div > (1 << 24))
         return rt_internal_fail(RT_EINVAL, "rt_adam_step: bad argument");
     return adam_launch(n, param_d, grad_d, exp_avg_d, exp_avg_sq_d, step, lr, hp, workspace_d, false,
-                       reinterpret_cast<hipStream_t>(stream));
+                       (float)grad_div, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
@@ -1760,37 +1333,14 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
         return rt_internal_fail(RT_EINVAL, "rt_ppo_update: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     float* norm_part = workspace_d + (workspace_floats - kNormSlots);
-    const bool fused = use_reduce_adam();
-    if (fused) {
-        static bool attr = false;
-        if (!attr) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_reduce_adam),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kReduceAdamLds);
-            if (e != hipSuccess) return rt_internal_fail(RT_EDEVICE, hipGetErrorString(e));
-            attr = true;
-        }
-        // the arrival counter: the workspace's last norm slot (unused by the partials)
-        const hipError_t e = hipMemsetAsync(norm_part + (kNormSlots - 1), 0, sizeof(unsigned), st);
-        if (e != hipSuccess) return rt_internal_fail(RT_EDEVICE, hipGetErrorString(e));
-    }
     for (int i = 0; i < n_minibatches; ++i) {
         int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
                                  adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,
-                                 stats_d, stats_accum_d, st, fused ? 0 : 1);
+                                 stats_d, stats_accum_d, st);
         if (rc) return rc;
-        if (!fused) {
-            rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part,
-                             true, st);
-            if (rc) return rc;
-            continue;
-        }
-        ReduceAdamParams Q{};
-        Q.R = reduce_params(grads_d, mb_size, hp, workspace_d, workspace_floats, stats_d, stats_accum_d);
-        Q.A = adam_params(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part);
-        Q.counter = reinterpret_cast<unsigned*>(norm_part + (kNormSlots - 1));
-        hipLaunchKernelGGL(k_ppo_reduce_adam, dim3(kReduceBlocks), dim3(1024), kReduceAdamLds, st, Q);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+        rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part,
+                         true, 1.0f, st);
+        if (rc) return rc;
     }
     return RT_OK;
 }

@@ -43,25 +43,14 @@
 namespace {
 
 constexpr int kStepThreads = 256;
-#ifndef RT_DENSE_UNROLL
-#define RT_DENSE_UNROLL 8
-#endif
-#ifndef RT_SLICE_VEC
-#define RT_SLICE_VEC 8192
-#endif
-constexpr int kUnroll = RT_DENSE_UNROLL;
+constexpr int kUnroll = 8;  // k_dense: float4 loads in flight per thread (4/8 measured equal)
 // Library events order work between the library's own streams on one device
 // (the pipelined rollout's fork / turns / join) or time kernels; neither needs
 // the system-scope release + acquire (L2 writeback and invalidate) a default
 // event record performs.  Kernel boundaries keep their device-scope release.
-#ifndef RT_EVENT_SYSFENCE
-#define RT_EVENT_SYSFENCE 0
-#endif
-constexpr unsigned kEventNoSysFence = RT_EVENT_SYSFENCE ? 0u : hipEventDisableSystemFence;
-#ifndef RT_PDENSE_U
-#define RT_PDENSE_U 4  // persistent dense rollout: float4 loads per lane per register set (two sets)
-#endif  // float4 loads in flight per thread
-constexpr int kSliceVec = RT_SLICE_VEC;   // k_dense slice: 8192 float4 = 128 KiB of dose
+constexpr unsigned kEventNoSysFence = hipEventDisableSystemFence;
+constexpr int kPDenseU = 4;  // persistent dense rollout: float4 loads per lane per register set (two sets)
+constexpr int kSliceVec = 8192;          // k_dense slice: 8192 float4 = 128 KiB of dose
 constexpr int kMaxTumourVoxels = 16384;  // tumour voxels (op slots n + n-1 < 2^16; k_finish LDS per wave)
 constexpr int kMaxGridDim = 1024;
 constexpr int kMaxPlanLevels = 64;       // levels of a tumour's sum plan (LDS copy in k_finish)
@@ -692,15 +681,9 @@ __device__ __forceinline__ float4 load_nt(const float4* p) {
 }
 
 // RESET envs' rows are zeroed by zero_reset_share, not by their slices.
-// XFER (k_dense_rollout): the env's mode is read with an L1-bypassing
-// non-temporal load (the same block re-reads it every phase, after another
-// kernel rewrote it) and the partials are stored `sc1` (write-through), so the
-// hand-off needs no acquire or release fence (MI355X_MICROARCH.md valid forms).
-template <bool XFER = false>
 __device__ __forceinline__ void dense_item(const DenseParams& P, int sl, int e) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int mode = XFER ? __builtin_nontemporal_load(&P.st.setup[e].mode) : P.st.setup[e].mode;
-    if (mode != MODE_STEP) return;
+    if (P.st.setup[e].mode != MODE_STEP) return;
     const float4* d4 = reinterpret_cast<const float4*>(P.st.dose + (size_t)e * P.G.Vpad);
     const int n = P.lung_n;
     const int q0 = sl * P.vec_per_slice;
@@ -747,13 +730,8 @@ __device__ __forceinline__ void dense_item(const DenseParams& P, int sl, int e) 
             c += s_cnt[w];
             t += s_sum[w];
         }
-        if (XFER) {
-            __hip_atomic_store(P.part_cnt + (size_t)e * P.slices + sl, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(P.part_sum + (size_t)e * P.slices + sl, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            P.part_cnt[(size_t)e * P.slices + sl] = c;
-            P.part_sum[(size_t)e * P.slices + sl] = t;
-        }
+        P.part_cnt[(size_t)e * P.slices + sl] = c;
+        P.part_sum[(size_t)e * P.slices + sl] = t;
     }
     __syncthreads();  // s_cnt / s_sum are reused by the next item of a persistent block
 }
@@ -789,8 +767,6 @@ constexpr int kZeroBlocks = 256;  // grid k_dense: blocks that zero RESET rows (
 
 // zero_reset_share: part `part` of n_parts of the zeroing of the RESET rows
 // among envs [e_begin, e_begin + n_env) (reset_dose, environment.py:104).
-// XFER: modes by non-temporal loads, zeros by `sc1` 16-B stores (see dense_item)
-template <bool XFER = false>
 __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, int part, int n_parts) {
     __shared__ int s_w[kStepThreads / 64];
     __shared__ int s_env;
@@ -799,7 +775,7 @@ __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, i
     const int a0 = min(tid * per, n_env), a1 = min(a0 + per, n_env);
     const uint8_t* mb = P.st.mode_b + e_begin;
     int c = 0;
-    for (int e = a0; e < a1; ++e) c += (XFER ? __builtin_nontemporal_load(mb + e) : mb[e]) == MODE_RESET;
+    for (int e = a0; e < a1; ++e) c += mb[e] == MODE_RESET;
     int R;
     const int pre = block_excl_scan(c, s_w, &R);
     if (R == 0) return;  // block-uniform
@@ -812,7 +788,7 @@ __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, i
         if (r >= pre && r < pre + c) {  // this thread's env range holds reset rank r
             int k = (int)(r - pre);
             for (int e = a0; e < a1; ++e) {
-                if ((XFER ? __builtin_nontemporal_load(mb + e) : mb[e]) == MODE_RESET && k-- == 0) {
+                if (mb[e] == MODE_RESET && k-- == 0) {
                     s_env = e_begin + e;
                     break;
                 }
@@ -825,12 +801,7 @@ __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, i
         typedef float nf4 __attribute__((ext_vector_type(4)));
         nf4* d4 = reinterpret_cast<nf4*>(P.st.dose + (size_t)e * P.G.Vpad);
         const nf4 z = {0.f, 0.f, 0.f, 0.f};
-        if (XFER) {
-            for (int64_t q = q0 + tid; q < q1; q += kStepThreads)
-                asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(d4 + q), "v"(z) : "memory");
-        } else {
-            for (int64_t q = q0 + tid; q < q1; q += kStepThreads) __builtin_nontemporal_store(z, d4 + q);
-        }
+        for (int64_t q = q0 + tid; q < q1; q += kStepThreads) __builtin_nontemporal_store(z, d4 + q);
     }
 }
 
@@ -858,87 +829,7 @@ __global__ __launch_bounds__(256) void k_dense_persist(DenseParams P, int n_env)
     zero_reset_share(P, P.e_begin, n_env, blockIdx.x, gridDim.x);
 }
 
-// ---------------------------------------------------------------------------
-// Device hand-off of the pipelined dense rollout (rt_env_set_dense_handoff 1):
-// ONE launch streams every group's lung segments for every step of the
-// rollout call, phase (t, g) after phase (t, g - 1), so the dose stream has no
-// kernel boundary, ramp or tail between the groups' turns.  Group g's
-// policy/march kernel of step t is followed on its stream by a stream write
-// beam_seq[g] = beam_base[g] + t + 1; a block polls that word (one lane, `sc1`
-// loads, s_sleep) before its share of the phase, streams its items and zeroes
-// its share of the RESET rows, then publishes: every wave vmcnt(0) -> barrier
-// -> one agent atomic add on done_cnt[g].  No fences: everything the block
-// reads that another kernel wrote since its last phase bypasses L1 (the
-// mode bytes and the dose rows by non-temporal loads), and everything the
-// finish kernel reads is stored `sc1` (write-through), the first valid form
-// of MI355X_MICROARCH.md's hand-off table.  (With an acquire and a release
-// fence per block and phase -- 1536 L2 write-backs per phase -- the step took
-// 0.45 ms instead of 0.28.)  Group g's k_finish of step t waits on its stream
-// for done_cnt[g] >= done_base[g] + grid * (t + 1) (hipStreamWaitValue64).
-// No block ever waits on another block, only on host-stream work ordered
-// before it; a wait longer than timeout_ticks (a stream op that never came)
-// sets *err and the block stops waiting, so the launch always drains.
-// ---------------------------------------------------------------------------
 constexpr int kMaxRolloutGroups = 4;
-
-struct DenseRolloutParams {
-    DenseParams P;                       // e_begin set per phase
-    int32_t bounds[kMaxRolloutGroups + 1];
-    int32_t G, n_steps;
-    uint64_t* beam_seq;                  // [G], 128-B apart (stride 16 words)
-    uint64_t* done_cnt;                  // [G], 128-B apart
-    uint64_t beam_base[kMaxRolloutGroups];
-    uint32_t* err;                       // host-visible, sticky
-    uint64_t timeout_ticks;              // s_memrealtime ticks (100 MHz)
-};
-
-constexpr int kSeqStride = 16;  // uint64 words between two groups' hand-off words (one 128-B line each)
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(56))) void k_dense_rollout(DenseRolloutParams R0) {
-    bool waiting = true;  // lane 0 of the block: false after a timeout
-    const int n_phases = R0.n_steps * R0.G;
-    for (int p = 0; p < n_phases; ++p) {
-            // the parameters through a laundered kernarg pointer, per phase:
-            // kept live across the loops they took 106 SGPRs, and 6 blocks per
-            // CU at 128 SGPRs a wave left no SGPRs for the policy kernel's
-            // waves, which the blocks wait on (MI355X_MICROARCH.md residency:
-            // 800 SGPRs per SIMD)
-            typedef const __attribute__((address_space(4))) DenseRolloutParams* KPtr;
-            KPtr ap = (KPtr)(__builtin_amdgcn_kernarg_segment_ptr());
-            asm volatile("" : "+s"(ap));
-            const DenseRolloutParams& R = *(const DenseRolloutParams*)ap;
-            const int t = p / R.G, g = p - t * R.G;
-            if (threadIdx.x == 0) {
-                const uint64_t want = R.beam_base[g] + (uint64_t)t + 1;
-                uint64_t* w = R.beam_seq + g * kSeqStride;
-                if (waiting && __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-                        __builtin_amdgcn_s_sleep(4);
-                        if (__builtin_amdgcn_s_memrealtime() - t0 > R.timeout_ticks) {
-                            __hip_atomic_store(R.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            waiting = false;
-                            break;
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-            const int e_begin = R.bounds[g];
-            const int n_env = R.bounds[g + 1] - e_begin;
-            const int slices = R.P.slices;
-            const int n_items = n_env * slices;
-            for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-                dense_item<true>(R.P, it % slices, e_begin + it / slices);
-            zero_reset_share<true>(R.P, e_begin, n_env, blockIdx.x, gridDim.x);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                __hip_atomic_fetch_add(R.done_cnt + g * kSeqStride, (uint64_t)1, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-}
 
 // Store 4 consecutive voxels [v0, v0+4) of one obs channel row.
 __device__ __forceinline__ void store4(float* row, int v0, int V, bool aligned4, float a, float b, float c,
@@ -1188,17 +1079,11 @@ __device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const 
     return result >= 0 ? tv[result] : 0.0f;
 }
 
-// KG > 1 (k_finish): the tumour gather issues the loads of KG voxels per lane
-// (their row positions, then their doses) before using any of them, so a
-// 586-voxel tumour costs two dependent HBM round trips per 64 * KG voxels
-// instead of two per 64.  Beside the saturating dose stream of the pipelined
-// rollout a round trip is several microseconds; the fused step kernels (tight
-// register budgets) keep the one-voxel-per-iteration loop (KG = 1).
 // PF (k_finish): the step's independent scalars (the env's dense partial
 // sums, t, episode return / length) are loaded before the tumour gather and
 // the nearest tumour voxel's index travels with the distance argmin, so the
 // tail issues no dependent load (each one a few us beside the dose stream).
-template <int KG = 1, bool PF = false>
+template <bool PF = false>
 __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char* wave_lds) {
     float* tvals = reinterpret_cast<float*>(wave_lds);
     if (lane == 0) RT_STAMP(e, 5);
@@ -1274,32 +1159,9 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
             if constexpr (PF) bvox = v;
         }
     };
-    if constexpr (KG == 1) {
-        for (int i = lane; i < nt; i += 64) {
-            const int v = tv[i];
-            voxel(i, v, tc[i], dose[tp[i]], (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u);
-        }
-    } else {
-        for (int i0 = lane; i0 < nt; i0 += 64 * KG) {
-            int pos[KG], vv[KG];
-            uint32_t cc[KG], lb[KG];
-            float xv[KG];
-#pragma unroll
-            for (int k = 0; k < KG; ++k) {
-                const int i = min(i0 + 64 * k, nt - 1);
-                pos[k] = tp[i];
-                vv[k] = tv[i];
-                cc[k] = tc[i];
-            }
-#pragma unroll
-            for (int k = 0; k < KG; ++k) {
-                xv[k] = dose[pos[k]];
-                lb[k] = P.lib.lung_bits[vv[k] >> 5];
-            }
-#pragma unroll
-            for (int k = 0; k < KG; ++k)
-                if (i0 + 64 * k < nt) voxel(i0 + 64 * k, vv[k], cc[k], xv[k], (lb[k] >> (vv[k] & 31)) & 1u);
-        }
+    for (int i = lane; i < nt; i += 64) {
+        const int v = tv[i];
+        voxel(i, v, tc[i], dose[tp[i]], (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u);
     }
     ctum = wave_sum_i(ctum);
 #pragma unroll
@@ -1386,28 +1248,17 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     if (P.vision) vision_scatter(P, e, lane, pose, m, wave_lds);
 }
 
-// k_finish's tumour gather batch (voxels per lane in flight; finish_env).  1:
-// batching 4 or 8 voxels per lane (VGPRs 78 -> 106) made the pipelined dense
-// step slower, 0.2756 -> 0.2774 / 0.2812-0.2911 ms; A/B builds
-#ifndef RT_FINISH_KG
-#define RT_FINISH_KG 1
-#endif
-// k_finish's early loads of the tail's scalars (finish_env PF; A/B builds)
-#ifndef RT_FINISH_PF
-#define RT_FINISH_PF 1
-#endif
-// RT_CHAIN_PRIO (A/B builds): wave issue priority (s_setprio) of the latency
-// chain's kernels (k_finish, k_step_policy) against the co-running dose stream
-#ifndef RT_CHAIN_PRIO
-#define RT_CHAIN_PRIO 0
-#endif
+// k_finish: one wave per env.  The tail's scalars are loaded before the
+// tumour gather (finish_env<true>).  Measured and not kept: 4 or 8
+// tumour voxels per lane in flight (VGPRs 78 -> 106, the pipelined step
+// slower) and wave issue priority for the latency chain (s_setprio 3: the
+// co-running dose stream loses issue slots).
 __global__ __launch_bounds__(256) void k_finish(FinishParams P) {
-    if (RT_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(RT_CHAIN_PRIO);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int e = P.e_begin + blockIdx.x * P.wpb + w;
     if (e >= P.N) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm_raw[];
-    finish_env<RT_FINISH_KG, RT_FINISH_PF != 0>(P, e, lane, fsm_raw + (size_t)w * P.wave_lds);
+    finish_env<true>(P, e, lane, fsm_raw + (size_t)w * P.wave_lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1438,7 +1289,6 @@ struct PolicyStepParams {
 
 template <bool FINISH>
 __global__ __launch_bounds__(1024) void k_step_policy(BeamParams B, FinishParams F, PolicyStepParams Q) {
-    if (RT_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(RT_CHAIN_PRIO);
     extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
     rtpol::Lds& L = *reinterpret_cast<rtpol::Lds*>(psm);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1494,7 +1344,7 @@ __global__ __launch_bounds__(1024) void k_step_policy(BeamParams B, FinishParams
 // rounds in another order than k_dense's slices.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void dense_env(const FinishParams& P, int e, int lane) {
-    constexpr int U = RT_PDENSE_U;
+    constexpr int U = kPDenseU;
     const float4* d4 = reinterpret_cast<const float4*>(P.st.dose + (size_t)e * P.G.Vpad);
     const int n = P.lung_n;
     const int nq = (n + 3) >> 2;
@@ -1958,17 +1808,6 @@ struct rt_env {
     int rollout_groups = 2;  // DESIGN.md §3 "Pipelined dense rollout"
     hipStream_t pipe[kMaxRolloutGroups] = {};
     hipEvent_t pev[1 + 2 * kMaxRolloutGroups] = {};  // fork, dense[G], join[G]
-    // device hand-off (rt_env_set_dense_handoff 1): the dose stream (own
-    // hardware queue: a CU-masked stream is never pooled), the hand-off words
-    // (beam_seq[g], done_cnt[g], monotonic across calls) and the host's next
-    // bases, the sticky timeout flag (host pinned)
-    int dense_handoff = 0;
-    hipStream_t dstream = nullptr;
-    hipEvent_t dev_ev[2] = {};           // dose stream's join, spare
-    uint64_t* seq_d = nullptr;           // beam_seq at [g * kSeqStride], done_cnt at [(kMaxRolloutGroups + g) * kSeqStride]
-    uint64_t beam_next[kMaxRolloutGroups] = {};
-    uint64_t done_next[kMaxRolloutGroups] = {};
-    uint32_t* err_h = nullptr;
     std::vector<void*> allocs;
 };
 
@@ -2002,10 +1841,6 @@ void free_env(rt_env* env) {
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t q : env->pipe)
         if (q) (void)hipStreamDestroy(q);
-    for (hipEvent_t e : env->dev_ev)
-        if (e) (void)hipEventDestroy(e);
-    if (env->dstream) (void)hipStreamDestroy(env->dstream);
-    if (env->err_h) (void)hipHostFree(env->err_h);
     for (void* p : env->allocs) (void)hipFree(p);
     (void)hipSetDevice(cur);
     delete env;
@@ -2261,11 +2096,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     size_t wave_bytes = (size_t)2 * max_n * sizeof(float) + std::max(plan_bytes, hash_bytes);
     wave_bytes = (wave_bytes + 15) / 16 * 16;
     env->finish_wave_lds = (int)wave_bytes;
-    env->finish_wpb = 4;
-    if (const char* fw = std::getenv("RT_FINISH_WPB")) {  // experiments: k_finish waves per block (1, 2, 4)
-        const int v = std::atoi(fw);
-        if (v == 1 || v == 2 || v == 4) env->finish_wpb = v;
-    }
+    env->finish_wpb = 4;  // 1 / 2 waves per block measured 4 % slower
     while (env->finish_wpb > 1 && (size_t)env->finish_wpb * wave_bytes > 160 * 1024) env->finish_wpb /= 2;
     env->finish_smem = (size_t)env->finish_wpb * wave_bytes;
     if (env->finish_smem > 160 * 1024) { free_env(env); return fail(RT_ELIMIT, "LDS budget exceeded"); }
@@ -2281,16 +2112,9 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     env->fused_smem = fused_bytes(env->fused_wpb);
     // pipelined dense rollout: small policy blocks, so that they find room on
     // CUs beside the other env group's k_dense blocks (a 16-wave block needs a
-    // whole CU's registers; RT_PIPE_WPB overrides, experiments)
-    {
-        const char* pw = std::getenv("RT_PIPE_WPB");
-        int w = pw ? std::atoi(pw) : 8;
-        if (w < 1 || w > 16) w = 8;
-        env->pipe_wpb = std::min(w, env->fused_wpb);
-        env->pipe_smem = fused_bytes(env->pipe_wpb);
-        const char* pb = std::getenv("RT_DENSE_PERSIST");  // experiments: 0 = grid k_dense
-        if (pb) env->pipe_dense_bpc = std::max(0, std::atoi(pb));
-    }
+    // whole CU's registers)
+    env->pipe_wpb = std::min(8, env->fused_wpb);
+    env->pipe_smem = fused_bytes(env->pipe_wpb);
     // k_rollout_policy: the parameters once per block, then 16 per-wave
     // regions (h1 during the policy, the finish scratch after it); tumours
     // above the region's plan capacity keep their plan slots in gscratch
@@ -2633,45 +2457,7 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
     Q.seed = ps->seed;
     Q.id_base = ps->env_id_base;
     Q.wpb = wpb;
-    static const bool serial = [] {
-        const char* v = std::getenv("RT_PIPE_SERIAL");  // experiments: 0 = no k_dense turns
-        return !(v && v[0] == '0');
-    }();
     const size_t Nn = (size_t)N;
-    const bool dev = piped && env->dense_handoff;
-    DenseRolloutParams R{};
-    if (dev) {
-        // the whole call's dose stream: one k_dense_rollout launch on the
-        // dose stream, before any group's work is queued (it only waits on
-        // words the group streams write later)
-        if (*(volatile uint32_t*)env->err_h)
-            return fail(RT_EDEVICE, "rt_env_rollout_policy: a device hand-off wait timed out in an earlier call");
-        R.P.G = env->G;
-        R.P.lung_thr = env->C.lung_thr;
-        R.P.st = env->st;
-        R.P.lung_bits = env->lib.lung_bits;
-        R.P.part_cnt = env->part_cnt;
-        R.P.part_sum = env->part_sum;
-        R.P.slices = env->slices;
-        R.P.vec_per_slice = env->vec_per_slice;
-        R.P.lung_n = env->lung_n;
-        for (int g = 0; g <= G; ++g) R.bounds[g] = bounds[g];
-        R.G = G;
-        R.n_steps = r->n_steps;
-        R.beam_seq = env->seq_d;
-        R.done_cnt = env->seq_d + kMaxRolloutGroups * kSeqStride;
-        for (int g = 0; g < G; ++g) R.beam_base[g] = env->beam_next[g];
-        R.err = env->err_h;
-        R.timeout_ticks = 200000000;  // 2 s at 100 MHz: only a stream op that never comes waits this long
-        RT_HIP(hipStreamWaitEvent(env->dstream, env->pev[0], 0));
-        hipEvent_t* ev = next_timing_slot(env);
-        if (ev) (void)hipEventRecord(ev[0], env->dstream), (void)hipEventRecord(ev[1], env->dstream);
-        hipLaunchKernelGGL(k_dense_rollout, dim3(env->pipe_dense_bpc * env->num_cu), dim3(kStepThreads), 0,
-                           env->dstream, R);
-        RT_LAUNCH_CHECK("k_dense_rollout");
-        if (ev) (void)hipEventRecord(ev[2], env->dstream), (void)hipEventRecord(ev[3], env->dstream);
-    }
-    const uint64_t grid_dense = (uint64_t)env->pipe_dense_bpc * env->num_cu;
     for (int t = 0; t < r->n_steps; ++t) {
         Q.obs_in = t == 0 ? ps->obs_in : obs_d;
         Q.done_in = t == 0 ? ps->done_in : terminated_d;
@@ -2685,7 +2471,7 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
         float* info = r->info_store ? r->info_store + (size_t)t * Nn * RT_INFO_W : nullptr;
         for (int g = 0; g < G; ++g) {
             const int e0 = bounds[g], e1 = bounds[g + 1];
-            hipEvent_t* ev = dev ? nullptr : next_timing_slot(env);
+            hipEvent_t* ev = next_timing_slot(env);
             if (ev) (void)hipEventRecord(ev[0], S[g]);
             BeamParams bp = beam_params(env, false, Q.act_store, nullptr, nullptr);
             FinishParams fp = finish_params(env, obs_d, rew, terminated_d, info);
@@ -2694,17 +2480,9 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
             hipLaunchKernelGGL(k_step_policy<false>, dim3((e1 - e0 + wpb - 1) / wpb), dim3(64 * wpb), smem,
                                S[g], bp, fp, Q);
             RT_LAUNCH_CHECK("k_step_policy");
-            if (dev) {
-                RT_HIP(hipStreamWriteValue64(S[g], env->seq_d + g * kSeqStride, env->beam_next[g] + t + 1, 0));
-                RT_HIP(hipStreamWaitValue64(S[g], env->seq_d + (kMaxRolloutGroups + g) * kSeqStride,
-                                            env->done_next[g] + grid_dense * (t + 1), hipStreamWaitValueGte,
-                                            ~0ull));
-                if (const int rc = launch_finish(env, obs_d, rew, terminated_d, info, S[g], e0, e1)) return rc;
-                continue;
-            }
             // k_dense turns in a ring: group g of step t after group g-1 of step t
             // (group 0 after group G-1 of step t-1)
-            hipEvent_t wait = (piped && serial && (t > 0 || g > 0)) ? dense_ev[(g + G - 1) % G] : nullptr;
+            hipEvent_t wait = (piped && (t > 0 || g > 0)) ? dense_ev[(g + G - 1) % G] : nullptr;
             int rc = launch_dense_finish(env, obs_d, rew, terminated_d, info, S[g], ev, e0, e1, wait,
                                          piped ? dense_ev[g] : nullptr, piped ? env->pipe_dense_bpc : 0);
             if (rc) return rc;
@@ -2716,48 +2494,6 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
             RT_HIP(hipStreamWaitEvent(s, join_ev[g], 0));
         }
     }
-    if (dev) {
-        RT_HIP(hipEventRecord(env->dev_ev[0], env->dstream));
-        RT_HIP(hipStreamWaitEvent(s, env->dev_ev[0], 0));
-        for (int g = 0; g < G; ++g) {
-            env->beam_next[g] += (uint64_t)r->n_steps;
-            env->done_next[g] += grid_dense * (uint64_t)r->n_steps;
-        }
-    }
-    return RT_OK;
-}
-
-// Device hand-off resources, made on first use: the dose stream on its own
-// hardware queue (a CU-masked stream gets a dedicated queue; a pooled one could
-// sit behind a group stream's wait and never start), its join event, the
-// hand-off words and the host-visible timeout flag.
-static int ensure_handoff(rt_env* env) {
-    if (env->dstream) return RT_OK;
-    if (!env->pipe[0]) return fail(RT_EINVAL, "dense hand-off: dense visionless handles only");
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    RT_HIP(hipSetDevice(env->device));
-    std::vector<uint32_t> mask((env->num_cu + 31) / 32, 0u);
-    for (int c = 0; c < env->num_cu; ++c) mask[c / 32] |= 1u << (c % 32);
-    hipError_t e = hipExtStreamCreateWithCUMask(&env->dstream, (uint32_t)mask.size(), mask.data());
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&env->dev_ev[0], hipEventDisableTiming | kEventNoSysFence);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&env->dev_ev[1], hipEventDisableTiming | kEventNoSysFence);
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&env->err_h), 64, hipHostMallocCoherent);
-    if (e == hipSuccess) *env->err_h = 0;
-    int rc = e == hipSuccess ? RT_OK : fail(RT_EDEVICE, std::string("dense hand-off setup: ") + hipGetErrorString(e));
-    if (!rc) rc = dev_alloc(env, &env->seq_d, (size_t)2 * kMaxRolloutGroups * kSeqStride);
-    if (!rc && hipMemset(env->seq_d, 0, (size_t)2 * kMaxRolloutGroups * kSeqStride * 8) != hipSuccess)
-        rc = fail(RT_EDEVICE, "dense hand-off: hipMemset failed");
-    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = fail(RT_EDEVICE, "dense hand-off: sync failed");
-    (void)hipSetDevice(cur);
-    return rc;
-}
-
-int rt_env_set_dense_handoff(rt_env* env, int32_t mode) {
-    if (!env || mode < 0 || mode > 1) return fail(RT_EINVAL, "rt_env_set_dense_handoff: mode must be 0 (events) or 1 (device)");
-    if (mode == 1)
-        if (const int rc = ensure_handoff(env)) return rc;
-    env->dense_handoff = mode;
     return RT_OK;
 }
 

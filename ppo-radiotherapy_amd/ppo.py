@@ -542,12 +542,14 @@ class PPOTrainer:
                                          None if adv is None else adv.data_ptr() + 8 * i, hp,
                                          self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
                                          self._ppo_accum.data_ptr(), stream), "rt_ppo_grad")
-                self._allreduce_(self.flat_grad)
+                # SUM all-reduce; rt_adam_step divides by the world size itself
+                # (grad.div_(world) without a kernel of its own)
+                self._allreduce_(self.flat_grad, average=False)
                 self._adam_step += 1
                 _lib.check(L.rt_adam_step(n, self.flat_param.data_ptr(), self.flat_grad.data_ptr(),
                                           self._exp_avg.data_ptr(), self._exp_avg_sq.data_ptr(),
-                                          self._adam_step, lr, hp, self._norm_ws.data_ptr(), stream),
-                           "rt_adam_step")
+                                          self._adam_step, lr, hp, self.world, self._norm_ws.data_ptr(),
+                                          stream), "rt_adam_step")
         self._last_stats = torch.cat([self._ppo_stats[:5], (self._ppo_accum[5] / total).reshape(1)])
         return total
 

@@ -177,12 +177,6 @@ class RadiotherapyVecEnv:
         """Env groups of the dense-mode rollout_policy: 2..4 (pipelined streams; default 2), 1 or 0 (persistent)."""
         _lib.check(self._L.rt_env_set_rollout_groups(self._h, int(groups)), "rt_env_set_rollout_groups")
 
-    def set_dense_handoff(self, mode: int):
-        """How the pipelined dense rollout hands the dose stream between env
-        groups: 0 = a k_dense launch per turn ordered by events, 1 = one
-        k_dense_rollout launch per call gated by device hand-off words."""
-        _lib.check(self._L.rt_env_set_dense_handoff(self._h, int(mode)), "rt_env_set_dense_handoff")
-
     def set_next_tumours(self, ids):
         t = torch.as_tensor(np.asarray(ids), dtype=torch.int32, device=self.device)
         _lib.check(self._L.rt_env_set_next_tumours(self._h, _lib.ptr(t), _lib.stream_handle()),
@@ -274,6 +268,15 @@ class RadiotherapyVecEnv:
             pos = _tensor_from_ptr(ip, (V,), torch.int32, self.device).long()
             return flat[:, pos].reshape(self.num_envs, *self.grid)
         return flat[:, :V].reshape(self.num_envs, *self.grid)
+
+    def dose_index(self):
+        """i32 [D*H*W] row position of each C-order voxel in the dose rows when
+        the handle keeps them lung-first (rt_env_dose_index; a view of
+        library memory), else None (C-order rows)."""
+        ip = self._L.rt_env_dose_index(self._h)
+        if not ip:
+            return None
+        return _tensor_from_ptr(ip, (int(np.prod(self.grid)),), torch.int32, self.device)
 
     def kernel_timing(self, capacity: int):
         """Record HIP events around k_beam/k_dense/k_finish for the next

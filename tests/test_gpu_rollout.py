@@ -78,16 +78,12 @@ def _compare(a, b, it, loose_dose_lung=False):
     assert torch.equal(a.env.dose(), b.env.dose())
 
 
-@pytest.mark.parametrize("step_mode,big,groups,handoff", [("incremental", 0, 0, 0), ("incremental", 1000, 0, 0),
-                                                           ("incremental", 12000, 0, 0), ("dense", 0, 2, 0),
-                                                           ("dense", 1000, 2, 0), ("dense", 0, 3, 0),
-                                                           ("dense", 1000, 4, 0), ("dense", 0, 1, 0),
-                                                           ("dense", 0, 0, 0), ("dense", 12000, 0, 0),
-                                                           ("dense", 0, 2, 1), ("dense", 1000, 3, 1),
-                                                           ("dense", 0, 4, 1)])
-def test_rollout_call_is_bitwise_the_stepwise_rollout(step_mode, big, groups, handoff):
-    """handoff 1: the dense groups' turns as ONE k_dense_rollout launch per
-    call, gated by device hand-off words (rt_env_set_dense_handoff)."""
+@pytest.mark.parametrize("step_mode,big,groups", [("incremental", 0, 0), ("incremental", 1000, 0),
+                                                   ("incremental", 12000, 0), ("dense", 0, 2),
+                                                   ("dense", 1000, 2), ("dense", 0, 3),
+                                                   ("dense", 1000, 4), ("dense", 0, 1),
+                                                   ("dense", 0, 0), ("dense", 12000, 0)])
+def test_rollout_call_is_bitwise_the_stepwise_rollout(step_mode, big, groups):
     from ppo_radiotherapy_amd import assets
 
     if not torch.cuda.is_available():
@@ -100,7 +96,6 @@ def test_rollout_call_is_bitwise_the_stepwise_rollout(step_mode, big, groups, ha
     b = _trainer(False, lib, n, step_mode)
     if step_mode == "dense":
         a.env.set_rollout_groups(groups)
-        a.env.set_dense_handoff(handoff)
     assert a.fused_rollout and not b.fused_rollout
     T = a.T
     # runs of storage rows per iteration: whole rollouts and split ones
@@ -139,12 +134,8 @@ def test_rollout_policy_rejects_vision_and_bad_groups():
         env.set_rollout_groups(5)
     with pytest.raises(_lib.RtError, match="groups"):
         env.set_rollout_groups(-1)
-    with pytest.raises(_lib.RtError, match="mode"):
-        env.set_dense_handoff(2)
     env.close()
     venv = RadiotherapyVecEnv(4, visionless=False, library=lib, device="cuda", seed=1)
     with pytest.raises(_lib.RtError, match="visionless"):
         venv.rollout_policy(ro)
-    with pytest.raises(_lib.RtError, match="hand-off"):
-        venv.set_dense_handoff(1)
     venv.close()
