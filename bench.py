@@ -124,6 +124,9 @@ def parse():
                     help="vision: conv1's forward products (rt_conv_set_precision) in the rollout and the update")
     ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="f32",
                     help="the fused update's 64x64 layer products (ppo_update_ms); the other is timed beside it")
+    ap.add_argument("--rocprof-stats", default=None,
+                    help="rocprofv3 --stats kernel_stats.csv of this same command (roofline.rocprof cross-check); "
+                         "default: the committed stats, labelled historical")
     ap.add_argument("--rehearse-same-device", action="store_true",
                     help="multi-rank rehearsal on one GPU: every rank on cuda:0, gloo instead of RCCL")
     a = ap.parse_args()
@@ -357,20 +360,39 @@ def stream_ceilings(dev, lib_obj, gib: float = 4.0, reps: int = 8) -> dict:
 
 
 PMC_FILE = os.path.join(REPO, "profiles", "r03", "r03_s2_k_dense_persist_pmc.json")
-# rocprofv3 --kernel-trace --stats of this bench's default command (tools/archive/r03/gpu_r03_s43.sh)
+# rocprofv3 --kernel-trace --stats of this bench's default command, committed
+# with a sidecar <csv>.meta.json naming the commit of the tree it was measured
+# on; used (labelled "historical") when --rocprof-stats does not name the
+# stats of the current run
 ROCPROF_FILE = os.path.join(REPO, "profiles", "r03", "r03_s43_kernel_stats.csv")
 
 
-def load_rocprof(kernel: str):
-    """Average duration (ms) and call count of `kernel` in the committed
-    rocprofv3 stats of the default bench command, or None."""
+def load_rocprof(kernel: str, path: str | None = None):
+    """Average duration (ms) and call count of `kernel` in rocprofv3 --stats
+    output: `path` (the stats of THIS run, --rocprof-stats) or the committed
+    file of the default command (historical, with the commit it was measured
+    on).  None when the kernel is not in it."""
     import csv
 
+    src = path or ROCPROF_FILE
     try:
-        for r in csv.DictReader(open(ROCPROF_FILE)):
+        for r in csv.DictReader(open(src)):
             if kernel in r["Name"]:
-                return {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"]),
-                        "source": os.path.relpath(ROCPROF_FILE, REPO)}
+                out = {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"]),
+                       "source": os.path.relpath(src, REPO) if src.startswith(REPO) else src}
+                if path is None:
+                    try:
+                        with open(src + ".meta.json") as f:
+                            meta = json.load(f)
+                    except OSError:
+                        meta = {}
+                    out["historical"] = True
+                    out["measured_at_commit"] = meta.get("commit")
+                    out["note"] = ("committed stats of this command on an earlier tree (not this run); pass "
+                                   "--rocprof-stats <kernel_stats.csv> of the current run to cross-check it")
+                else:
+                    out["historical"] = False
+                return out
     except Exception:
         return None
     return None
@@ -650,6 +672,8 @@ def main():
     kms, kcalls = env.kernel_timing_read()
     kms = {k: v * kcalls / K for k, v in kms.items()}  # per step (a persistent rollout launch spans many)
     env.kernel_timing(0)
+    # the march's dose lines on the beams of this pass's last step (roofline.march)
+    mlines = march_lines(env) if (not a.vision and not a.env_only and a.step_mode == "dense") else None
     kms = {k: max_over_ranks(v) for k, v in kms.items()}
     env_ms = sum(kms.values())  # k_beam start -> k_finish end, per step
     total_envs = a.envs * world
@@ -783,7 +807,7 @@ def main():
         # the same kernel in the committed rocprofv3 stats of this command: the
         # HIP-event interval above also spans the dispatch after the turn
         # hand-off (~9 us), rocprofv3 times the kernel alone
-        rp = load_rocprof("k_dense_persist")
+        rp = load_rocprof("k_dense_persist", a.rocprof_stats)
         if rp is not None:
             rp["achieved"] = bytes_launch / launches / (rp["avg_ms"] * 1e-3) / 1e9
             rp["frac"] = rp["achieved"] * 1e9 / HBM_PEAK
@@ -795,6 +819,7 @@ def main():
                                                           "nothing co-running (one-group pass)"}
     roof["step_frac_of_hbm"] = a.envs * 4 * Vl / (dt / K) / HBM_PEAK if not a.vision else None
     roof["timed_pass_ms_per_step"] = 1000 * dt_timed / K  # the instrumented pass (kernel times above)
+    rmw_ceil = None
     if rank == 0 and not a.env_only:
         from ppo_radiotherapy_amd import _lib
 
@@ -804,6 +829,26 @@ def main():
         roof["measured_ceiling_probe"] = ("rt_probe_stream over 4 GiB: non-temporal 16-B loads, 8 in flight per lane "
                                           "(read: reduced; copy: + plain 16-B stores, read+write bytes)")
         roof["frac_of_measured_ceiling"] = achieved / cel["read"]
+        rmw_ceil = random_rmw_ceiling(dev, _lib.load(), a.envs * V)
+        if mlines is not None and a.rollout_groups > 0:
+            # the beam march (draw_line.py:49-100 + environment.py:107-110) runs in
+            # k_step_policy (policy + pose + march, one wave per env): its random
+            # 128-B line read-modify-writes against the measured random-RMW rate
+            kp_ms = kms["k_beam"]  # per step: the k_step_policy launches of all env groups
+            rate = a.envs * mlines / (kp_ms * 1e-3)
+            roof["march"] = {
+                "kernel": "k_step_policy", "bound": "random-line RMW (latency/transactions)",
+                "model": "per env-step: the distinct 128-B dose lines the beam's splats touch, each read and written "
+                         "(2 x 128 B); the policy MLP and the f64 pose update run in the same kernel",
+                "lines_per_env_step": mlines, "kernel_ms_per_step": kp_ms, "line_rmw_per_s": rate,
+                "achieved_GBps": rate * 256 / 1e9, "frac_of_hbm_peak": rate * 256 / HBM_PEAK,
+                "probe_line_rmw_per_s": rmw_ceil, "frac": rate / rmw_ceil,
+                "timing": "library HIP events around k_step_policy on the env-group streams, instrumented pass"}
+            rpm = load_rocprof("k_step_policy", a.rocprof_stats)
+            if rpm is not None and launches > 1.5:
+                rpm["line_rmw_per_s"] = a.envs / launches * mlines / (rpm["avg_ms"] * 1e-3)
+                rpm["frac"] = rpm["line_rmw_per_s"] / rmw_ceil
+                roof["march"]["rocprof"] = rpm
 
     # ---------------- the other step formulation, same workload (policy in the loop)
     other = None
@@ -833,7 +878,7 @@ def main():
             from ppo_radiotherapy_amd import _lib
 
             bl, tl = incremental_transactions(env2, lib)
-            ceil = random_rmw_ceiling(dev, _lib.load(), a.envs * V)
+            ceil = rmw_ceil
             sps = a.envs * K / d2  # this rank's env steps/s
             ach_lines = sps * bl
             ach_bytes = sps * 128 * (2 * bl + tl)

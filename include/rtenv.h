@@ -414,8 +414,12 @@ typedef struct rt_conv_layer {
 } rt_conv_layer;
 
 /* Arithmetic of the C3D forward products (process-wide, initially
- * RT_CONV_PREC=f32|bf16x3 from the environment, else f32).  F32: exact f32
- * MFMA (the reference's torch Conv3d in f32; its cuDNN default allowed TF32).
+ * RT_CONV_PREC=f32|bf16x3 from the environment, else f32; PPOTrainer sets it
+ * per rollout step and update when its config names conv_precision).  F32:
+ * f32 throughout (the reference's torch Conv3d in f32; its cuDNN default
+ * allowed TF32) -- conv1's forward in the Winograd form F(2x2x2, 3x3x3) (f32
+ * transforms, products on exact f32 MFMA), the other stages direct on f32
+ * MFMA.
  * BF16X3: in conv1's forward kernel and the grouped stages' (groups 2 and 4)
  * forward and data-gradient kernels, every operand split into bf16 hi + lo
  * (round to nearest even), products hi*hi + hi*lo + lo*hi accumulated in f32

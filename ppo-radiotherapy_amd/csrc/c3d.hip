@@ -925,6 +925,314 @@ int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* ro
 }
 
 // ---------------------------------------------------------------------------
+// conv1 forward in the Winograd form F(2x2x2, 3x3x3) on f32 MFMA (the launched
+// f32 conv1 forward).  A 2x2x2 Winograd output tile is exactly one 2x2x2
+// pooling window, so a window's 8 conv outputs come out in ONE lane's
+// registers: the pooling max and its first-maximum index are plain register
+// compares (no DPP), and the 27 taps x 4 input channels of a direct conv
+// output (27 k-steps of 16x16x4 per 16 outputs x 16 channels) become 64
+// element-wise products per window, summed over the 4 input channels:
+//   M[xi][co][win] = sum_ci U[xi][co][ci] * V[xi][ci][win],  xi in 4x4x4,
+// one v_mfma_f32_16x16x4_f32 per xi and 16 windows (K = the 4 input
+// channels): 64 MFMAs per 16 windows against 216 direct (3.4x fewer).
+//   U = G w G^T (per axis G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]): the
+//       filter transform, once per block into registers (A operand: lane
+//       (co = l & 15, ci = l >> 4));
+//   V = B^T d B (per axis B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]): the
+//       4x4x4 input patch of the window, per lane (B operand: lane (window n
+//       = l & 15, ci = l >> 4)) from the plane ring, adds only;
+//   Y = A^T M A (per axis A^T = [1 1 1 0; 0 1 -1 -1]): applied axis by axis
+//       as the MFMAs of one (xi_x, xi_y) column complete (z, then y, then x).
+// Every operation is f32 (MFMA: exact FMA chains); the result differs from
+// the direct sum by rounding only (the transforms' adds and the halves of G
+// -- tests/test_gpu_c3d.py gates it against float64 torch like the direct
+// kernel).  The block streams z-planes through the same 6-slot LDS ring as
+// k_conv_ring (RingGeom / RingLoader: pooled row k needs planes 2k..2k+3,
+// the next two load by LDS DMA while the row computes); an item is one pooled
+// row py of the block's y band and 16 consecutive pooled x (x group xg).
+// U lives in LDS after the ring (16 KiB); registers hold half of V (32) and
+// the axis partial sums: 133 VGPRs, no spills.
+// ---------------------------------------------------------------------------
+constexpr int kWinoU = 16 * 64 * 4;  // floats of the transformed filter in LDS
+
+template <int PYB, int VEC, bool TRAIN>
+__global__ __launch_bounds__(512) void k_conv1_wino(RingParams P) {
+    extern __shared__ float xs[];
+    constexpr int NW = 8;
+    const Geom& g = P.rg.g;
+    const int SLOT = P.rg.SLOT;
+    const int b = blockIdx.z, py0 = blockIdx.x * PYB;
+    const int k0 = blockIdx.y * P.rg.ZC, k1 = min(g.PD, k0 + P.rg.ZC);
+    if (k0 >= k1) return;
+    const int lane = threadIdx.x & 63, n = lane & 15, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t srow = P.rows ? P.rows[b] : b;
+    const float* xb = P.x + srow * (int64_t)4 * g.D * g.H * g.W;
+    const int y0 = 2 * py0 - g.ph;
+
+    RingLoader<4, VEC, NW> ld;
+    ld.init(P.rg, y0, -g.pw, wave, lane);
+    auto load_plane = [&](int t, int slot) { ld.load(xb, P.rg, xs, t, slot, wave, lane); };
+    // ---- prologue DMA first: the filter transform below runs under it
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load_plane(2 * k0 + i, i);
+
+    // ---- U = G w G^T for (co = n, ci = gq), by wave 0 into LDS after the
+    // ring: us[(j * 64 + lane) * 4 + xz], j = xy * 4 + xx (one ds_read_b128 per
+    // (xi_x, xi_y) column gives its 4 xi_z values; registers hold only the
+    // patch transform and the output partial sums)
+    float* us = xs + kRing * SLOT;
+    if (wave == 0) {
+        const float* w = P.w + (n * 4 + gq) * 27;
+        float t[36];  // after the x axis: [kz][ky][xx]
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            const float w0 = w[3 * r], w1 = w[3 * r + 1], w2 = w[3 * r + 2];
+            t[4 * r] = w0;
+            t[4 * r + 1] = 0.5f * ((w0 + w1) + w2);
+            t[4 * r + 2] = 0.5f * ((w0 - w1) + w2);
+            t[4 * r + 3] = w2;
+        }
+        float s[48];  // after the y axis: [kz][xy][xx]
+#pragma unroll
+        for (int kz = 0; kz < 3; ++kz)
+#pragma unroll
+            for (int xx = 0; xx < 4; ++xx) {
+                const float a0 = t[(kz * 3) * 4 + xx], a1 = t[(kz * 3 + 1) * 4 + xx], a2 = t[(kz * 3 + 2) * 4 + xx];
+                s[(kz * 4) * 4 + xx] = a0;
+                s[(kz * 4 + 1) * 4 + xx] = 0.5f * ((a0 + a1) + a2);
+                s[(kz * 4 + 2) * 4 + xx] = 0.5f * ((a0 - a1) + a2);
+                s[(kz * 4 + 3) * 4 + xx] = a2;
+            }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {  // j = xy * 4 + xx; along z
+            const float a0 = s[j], a1 = s[16 + j], a2 = s[32 + j];
+            const float4 q = make_float4(a0, 0.5f * ((a0 + a1) + a2), 0.5f * ((a0 - a1) + a2), a2);
+            *reinterpret_cast<float4*>(us + (j * 64 + lane) * 4) = q;
+        }
+    }
+    float bias[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[r] = P.bias[4 * gq + r];
+    const int chan = g.PD * g.PH * g.PW;
+    float* ybase = P.y + ((int64_t)b * CO + 4 * gq) * chan;
+    uint8_t* abase = TRAIN ? P.amax + ((int64_t)b * CO + 4 * gq) * chan : nullptr;
+    const int nxg = (g.PW + 15) >> 4;
+    const int items = PYB * nxg;
+    const int pxmax = 2 * g.XT - 1;  // last window whose 4x4 patch lies inside the slot's XL columns
+
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    int sb = 0;  // ring slot of plane 2k
+    for (int k = k0; k < k1; ++k) {
+        if (k + 1 < k1) {  // planes of the next pooled row -> the two free slots
+            load_plane(2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4);
+            load_plane(2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5);
+        }
+        for (int it = wave; it < items; it += NW) {
+            const int r = it / nxg, xg = it - r * nxg;
+            const int py = py0 + r;
+            if (py >= g.PH) break;  // wave-uniform
+            const int px = 16 * xg + n;
+            // ---- in two halves of the x axis (xi_x = 2h, 2h + 1): V = B^T d B of
+            // the lane's 4x4x4 patch (channel gq), then M = U V over the 4 input
+            // channels (MFMA) and Y = A^T M A.  (Both halves at once kept all 64
+            // products in flight and spilled.)
+            const int xoff = gq * g.CS + 2 * r * g.YS + 2 * min(px, pxmax);
+            const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+            f4 Y[2][2][2];  // [ox][oy][oz]
+            f4 Sx[2][2][2];  // [xi_x & 1][oy][oz]: the y-axis sums of a column pair
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float v[32];  // [dz][dy][k] -> [xz][xy][k], xi_x = 2h + k
+                int xo = xoff;
+                asm volatile("" : "+v"(xo));  // the halves' patch reads stay separate (no CSE)
+#pragma unroll
+                for (int dz = 0; dz < 4; ++dz) {
+                    int sl = sb + dz;
+                    sl = sl >= kRing ? sl - kRing : sl;
+                    const float* p = xs + sl * SLOT + xo;
+#pragma unroll
+                    for (int dy = 0; dy < 4; ++dy) {
+                        const float2 a = *reinterpret_cast<const float2*>(p + dy * g.YS);
+                        const float2 c = *reinterpret_cast<const float2*>(p + dy * g.YS + 2);
+                        float* q = v + (dz * 4 + dy) * 2;
+                        if (h == 0) {  // B^T along x, rows 0, 1
+                            q[0] = a.x - c.x;
+                            q[1] = a.y + c.x;
+                        } else {       // rows 2, 3
+                            q[0] = c.x - a.y;
+                            q[1] = a.y - c.y;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int dz = 0; dz < 4; ++dz)  // along y
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        float* q = v + dz * 8 + k;
+                        const float d0 = q[0], d1 = q[2], d2 = q[4], d3 = q[6];
+                        q[0] = d0 - d2;
+                        q[2] = d1 + d2;
+                        q[4] = d2 - d1;
+                        q[6] = d1 - d3;
+                    }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {  // along z
+                    const float d0 = v[j], d1 = v[8 + j], d2 = v[16 + j], d3 = v[24 + j];
+                    v[j] = d0 - d2;
+                    v[8 + j] = d1 + d2;
+                    v[16 + j] = d2 - d1;
+                    v[24 + j] = d1 - d3;
+                }
+                // software-pipelined columns (xi_x, xi_y): the MFMAs of column c
+                // are issued before the sums of column c - 1, whose results pass
+                // through an empty asm so they are formed here (left free, the
+                // compiler sinks every column's sums below all 64 MFMAs and
+                // their 256 accumulator registers spill)
+                f4 pm[4];
+                auto column_sums = [&](const f4 (&m)[4], int xx, int xy) {
+                    const f4 t0 = (m[0] + m[1]) + m[2], t1 = (m[1] - m[2]) - m[3];  // A^T along z
+                    f4(&S)[2][2] = Sx[xx & 1];
+                    if (xy == 0) {  // A^T along y: rows (1 1 1 0), (0 1 -1 -1)
+                        S[0][0] = t0;
+                        S[0][1] = t1;
+                    } else if (xy == 1) {
+                        S[0][0] += t0;
+                        S[0][1] += t1;
+                        S[1][0] = t0;
+                        S[1][1] = t1;
+                    } else if (xy == 2) {
+                        S[0][0] += t0;
+                        S[0][1] += t1;
+                        S[1][0] -= t0;
+                        S[1][1] -= t1;
+                    } else {
+                        S[1][0] -= t0;
+                        S[1][1] -= t1;
+                    }
+                    if (xy == 0)
+                        asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]));
+                    else
+                        asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]));
+                    if (xy == 3) {
+#pragma unroll
+                        for (int oy = 0; oy < 2; ++oy)
+#pragma unroll
+                            for (int oz = 0; oz < 2; ++oz) {  // A^T along x
+                                if (xx == 0) {
+                                    Y[0][oy][oz] = S[oy][oz];
+                                } else if (xx == 1) {
+                                    Y[0][oy][oz] += S[oy][oz];
+                                    Y[1][oy][oz] = S[oy][oz];
+                                } else if (xx == 2) {
+                                    Y[0][oy][oz] += S[oy][oz];
+                                    Y[1][oy][oz] -= S[oy][oz];
+                                } else {
+                                    Y[1][oy][oz] -= S[oy][oz];
+                                }
+                            }
+                    }
+                };
+#pragma unroll
+                for (int c = 0; c <= 8; ++c) {  // column c = k * 4 + xy of this half
+                    f4 m[4];
+                    if (c < 8) {
+                        const int k = c >> 2, xy = c & 3, xx = 2 * h + k;
+                        const int j = xy * 4 + xx, jv = xy * 2 + k;
+                        const float4 uc = *reinterpret_cast<const float4*>(us + (j * 64 + lane) * 4);
+                        m[0] = mfma4(uc.x, v[jv], zero);
+                        m[1] = mfma4(uc.y, v[8 + jv], zero);
+                        m[2] = mfma4(uc.z, v[16 + jv], zero);
+                        m[3] = mfma4(uc.w, v[24 + jv], zero);
+                    }
+                    if (c > 0) column_sums(pm, 2 * h + ((c - 1) >> 2), (c - 1) & 3);
+                    if (c < 8)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) pm[i] = m[i];
+                }
+            }
+            // ---- epilogue: bias, ReLU, the window max + first argmax in (z, y, x) order
+            const int cz0 = 2 * k - g.pd, cy0 = 2 * py - g.ph, cx0 = 2 * px - g.pw;
+            bool vo[8];
+#pragma unroll
+            for (int o = 0; o < 8; ++o) {
+                const int oz = o >> 2, oy = (o >> 1) & 1, ox = o & 1;
+                vo[o] = (unsigned)(cz0 + oz) < (unsigned)g.cd & (unsigned)(cy0 + oy) < (unsigned)g.ch &
+                        (unsigned)(cx0 + ox) < (unsigned)g.cw;
+            }
+            const bool st = px < g.PW;
+            const int oidx = (k * g.PH + py) * g.PW + px;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                float m = -INFINITY;
+                int km = 0;
+#pragma unroll
+                for (int o = 0; o < 8; ++o) {
+                    const float val = vo[o] ? fmaxf(Y[o & 1][(o >> 1) & 1][o >> 2][rr] + bias[rr], 0.0f) : -INFINITY;
+                    if (TRAIN) km = val > m ? o : km;  // strict: the first maximum keeps its index
+                    m = fmaxf(m, val);
+                }
+                if (st) {
+                    ybase[rr * chan + oidx] = m;
+                    if (TRAIN) abase[rr * chan + oidx] = (uint8_t)(km | (m > 0.0f ? 8 : 0));
+                }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next row has landed
+        __syncthreads();                     // ... every wave's; and nobody still reads the slots reloaded next
+        sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
+    }
+}
+
+template <int PYB, int VEC>
+int launch_wino(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
+                const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+    RingParams P{x, rows, w, bias, y, amax, rg};
+    const size_t lds = ((size_t)kRing * rg.SLOT + kWinoU) * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        if (const int rc_lds = allow_big_lds(&k_conv1_wino<PYB, VEC, true>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv1_wino<PYB, VEC, false>)) return rc_lds;
+        attr = true;
+    }
+    dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, B);
+    if (amax)
+        hipLaunchKernelGGL((k_conv1_wino<PYB, VEC, true>), grid, dim3(512), lds, st, P);
+    else
+        hipLaunchKernelGGL((k_conv1_wino<PYB, VEC, false>), grid, dim3(512), lds, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+// conv1's f32 forward: the Winograd kernel with the widest y band (4, 2, 1
+// pooled rows) whose 6-slot ring fits 160 KiB (one 8-wave block per CU by
+// registers); RT_ELIMIT when none does (the caller takes the direct ring)
+int launch_fwd_wino(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
+                    const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+    const bool vec4 = L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    auto fits = [&](const RingGeom& rg, int vec) {
+        return ((size_t)kRing * rg.SLOT + kWinoU) * sizeof(float) <= 160 * 1024 &&
+               (rg.npiece + 7) / 8 <= (vec == 4 ? ring_max_pieces<4, 4>() : ring_max_pieces<4, 1>()) &&
+               rg.g.W >= vec;
+    };
+    if (vec4) {
+        RingGeom rg = make_ring_geom<4, 4, 4>(L, B, 512);
+        if (fits(rg, 4)) return launch_wino<4, 4>(rg, B, x, rows, w, bias, y, amax, st);
+        rg = make_ring_geom<4, 2, 4>(L, B, 512);
+        if (fits(rg, 4)) return launch_wino<2, 4>(rg, B, x, rows, w, bias, y, amax, st);
+    }
+    RingGeom rg = make_ring_geom<4, 4, 1>(L, B, 512);
+    if (fits(rg, 1)) return launch_wino<4, 1>(rg, B, x, rows, w, bias, y, amax, st);
+    rg = make_ring_geom<4, 2, 1>(L, B, 512);
+    if (fits(rg, 1)) return launch_wino<2, 1>(rg, B, x, rows, w, bias, y, amax, st);
+    rg = make_ring_geom<4, 1, 1>(L, B, 512);
+    if (fits(rg, 1)) return launch_wino<1, 1>(rg, B, x, rows, w, bias, y, amax, st);
+    return RT_ELIMIT;
+}
+
+// ---------------------------------------------------------------------------
 // Grouped stage (groups = 2) on the plane ring in the z-shift form.  The dense
 // ring kernel above multiplies zero weights for the other group's channels
 // (2x the useful MFMA work).  Here a block works on ONE group's 8 input
@@ -2989,7 +3297,10 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     if (RT_C3D_EXP == 3) return fwd_tile(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);  // A/B builds
     int rc = RT_ELIMIT;
     if (L->cin == 4) {
-        rc = launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+        // f32: the Winograd kernel; bf16x3 (and planes too wide for its ring):
+        // the direct ring kernel
+        if (g_conv_prec == 0) rc = launch_fwd_wino(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+        if (rc == RT_ELIMIT) rc = launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     } else if (L->groups == 1) {
         rc = launch_fwd_ring<16, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     } else {

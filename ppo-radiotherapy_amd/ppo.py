@@ -137,14 +137,16 @@ class PPOTrainer:
             if prec not in _lib.PPO_PREC:
                 raise ValueError(f"update_precision {prec!r}: expected one of {sorted(_lib.PPO_PREC)}")
             self._update_prec = _lib.PPO_PREC[prec]
-        # arithmetic of the C3D conv1 forward (vision agent): "f32" (the
-        # reference's) or "bf16x3" (rt_conv_set_precision, process-wide; set
-        # only when the config names it)
-        if hasattr(cfg, "conv_precision"):
-            cprec = str(cfg.conv_precision)
-            if cprec not in _lib.CONV_PREC:
-                raise ValueError(f"conv_precision {cprec!r}: expected one of {sorted(_lib.CONV_PREC)}")
-            _lib.check(_lib.load().rt_conv_set_precision(_lib.CONV_PREC[cprec]), "rt_conv_set_precision")
+        # arithmetic of the C3D forward products (vision agent): "f32" (the
+        # reference's) or "bf16x3".  rt_conv_set_precision is process-wide, so
+        # the trainer sets it at the start of every rollout step and update of
+        # its own (_apply_conv_precision); None (the default) leaves the
+        # library's setting (RT_CONV_PREC at load, else f32) alone
+        cprec = getattr(cfg, "conv_precision", None)
+        if cprec is not None and str(cprec) not in _lib.CONV_PREC:
+            raise ValueError(f"conv_precision {cprec!r}: expected one of {sorted(_lib.CONV_PREC)}")
+        self._conv_prec = None if cprec is None else _lib.CONV_PREC[str(cprec)]
+        self._apply_conv_precision()
         # one flat gradient bucket; every param.grad is a view of it
         self.flat_grad = torch.zeros(n, dtype=self.params[0].dtype, **kw)
         off = 0
@@ -199,6 +201,10 @@ class PPOTrainer:
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
         self.iteration = 0
+
+    def _apply_conv_precision(self):
+        if self._conv_prec is not None and self.device.type == "cuda":
+            _lib.check(_lib.load().rt_conv_set_precision(self._conv_prec), "rt_conv_set_precision")
 
     # parameter order of the fused kernels (include/rtenv.h rt_policy_sample)
     POLICY_ORDER = ["actor_mean.0.weight", "actor_mean.0.bias", "actor_mean.2.weight", "actor_mean.2.bias",
@@ -273,6 +279,7 @@ class PPOTrainer:
         """One vectorised step of train.py:138-161 (policy sample + env step)."""
         if self.fused_policy:
             return self._rollout_step_fused(step, env_events)
+        self._apply_conv_precision()
         if self.compact_obs:
             self.env.snapshot(self.dose_snap[step], self.pose_snap[step], self.tumour_snap[step])
         else:
@@ -557,6 +564,7 @@ class PPOTrainer:
         """train.py:183-248: update_epochs x num_minibatches optimizer steps."""
         if self.fused_update:
             return self._update_fused()
+        self._apply_conv_precision()
         self._bind_batch()
         dev = self.device
         stats_sum = torch.zeros(6, device=dev)

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 O=gpurun_out/r04_s2
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_rollout.py tests/test_gpu_trainer.py tests/test_gpu_dp.py tests/test_gpu_rccl.py tests/test_gpu_headline.py > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_rollout.py tests/test_gpu_trainer.py tests/test_gpu_dp.py tests/test_gpu_rccl.py tests/test_gpu_headline.py "tests/test_gpu_c3d.py::test_features_extractor_matches_torch_modules" > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 timeout -k 10 300 python3 tools/probe_first_window.py > $O/probe.jsonl 2> $O/probe.err || { tail -30 $O/probe.err; exit 1; }
 cat $O/probe.jsonl | cut -c1-150
