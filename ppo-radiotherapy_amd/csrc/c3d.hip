@@ -41,52 +41,10 @@ extern "C" int rt_internal_fail(int code, const char* msg);
 
 namespace {
 
-// experiment knob (kernel-variant A/B builds only, tools/build_variant.py):
-// 1 = forward epilogue reduced to one store per tile, 2 = forward without the
-// input-tile load
-#ifndef RT_C3D_EXP
-#define RT_C3D_EXP 0
-#endif
-// ring forward epilogue: transposed window reduction (1) or one reduction per
-// channel (0, the round-2 form; A/B builds)
-#ifndef RT_EPI_T
-#define RT_EPI_T 1
-#endif
-// blocks the z-shift forward / data-gradient grids aim for when they split z into
-// chunks (A/B builds): 2048 (no split at 512 samples) beat 4096 / 8192 -- a block
-// that sweeps the whole depth pays its weight load and ring prologue once
-#ifndef RT_ZS_BLOCKS
-#define RT_ZS_BLOCKS 2048
-#endif
-// waves per SIMD the ring weight gradient is compiled for (A/B builds)
-#ifndef RT_WG_WPE
-#define RT_WG_WPE 2
-#endif
-// dense ring weight gradient: 1 = the next row's dY operands loaded into a
-// second register set at the row start (beside the plane DMA) instead of the
-// rolling one-register-per-tile prefetch (A/B builds)
-#ifndef RT_WG_DYB
-#define RT_WG_DYB 0
-#endif
-// z-shift forward: widest y band tried first, and (when defined) waves per SIMD
-// it is compiled for (A/B builds: 4 pooled rows at 4 waves per SIMD = two
-// blocks per CU measured 1.59 vs 1.34 ms for conv2, 4 rows at 2 waves 1.47)
-#ifndef RT_ZS_FWD_MAXPYB
-#define RT_ZS_FWD_MAXPYB 8
-#endif
-#ifdef RT_ZS_FWD_WPE
-#define RT_ZS_FWD_ATTR __attribute__((amdgpu_waves_per_eu(RT_ZS_FWD_WPE)))
-#else
-#define RT_ZS_FWD_ATTR
-#endif
-// widest y band of the z-shift weight gradient (A/B builds)
-#ifndef RT_WZ_MAXPYB
-#define RT_WZ_MAXPYB 2
-#endif
-// weight-gradient ring slot stride residue (see make_ring_geom)
-#ifndef RT_WG_SR
-#define RT_WG_SR 12
-#endif
+// blocks the z-shift forward / data-gradient grids aim for when they split z
+// into chunks: 2048 (no split at 512 samples) beat 4096 / 8192 -- a block that
+// sweeps the whole depth pays its weight load and ring prologue once
+constexpr int kZsBlocks = 2048;
 
 constexpr int CO = 16;
 constexpr int kThreads = 512;      // weight-gradient kernel: 8 waves = position groups x column groups
@@ -384,7 +342,7 @@ __global__ __launch_bounds__(conv_threads<CIN>()) void k_conv_relu_pool(FwdParam
     const int64_t srow = P.rows ? P.rows[b] : b;
     const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
     const int z0 = 2 * pz0 - g.pd, y0 = 2 * py0 - g.ph, x0 = -g.pw;
-    if (RT_C3D_EXP != 2) load_tile<CIN, conv_threads<CIN>()>(xs, xb, g, z0, y0, x0);
+    load_tile<CIN, conv_threads<CIN>()>(xs, xb, g, z0, y0, x0);
     float af[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) af[s] = a_frag<CIN, G>(P.w, s, c, gq);
@@ -403,10 +361,6 @@ __global__ __launch_bounds__(conv_threads<CIN>()) void k_conv_relu_pool(FwdParam
     float* ybase = P.y + ((int64_t)b * CO + 4 * gq + myr) * chan;
     uint8_t* abase = TRAIN ? P.amax + ((int64_t)b * CO + 4 * gq + myr) * chan : nullptr;
     conv_core<CIN, PYB>(xs, af, g, PZB * PYB, [&](const f4 (&acc)[2], int row, int xp) {
-        if constexpr (RT_C3D_EXP == 1) {
-            ybase[(row * 64 + xp * 2) & 1023] = acc[0][0] + acc[1][1] + acc[0][2] + acc[1][3];
-            return;
-        }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int tx = 2 * xp + u;
@@ -774,9 +728,9 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
     for (int r = 0; r < 4; ++r) bias[r] = P.bias[4 * gq + r];
     const int zc = c >> 3, yc = (c >> 2) & 1, xc = c & 3;
     const int widx = zc * 4 + yc * 2 + (xc & 1);  // rank of the lane in its pooling window
-    // after the window reduction the lane stores channel 4g + myr: RT_EPI_T
-    // (transposed reduction, below) leaves channel 2 (xc & 1) + yc on it
-    const int myr = RT_EPI_T ? 2 * (xc & 1) + yc : widx & 3;
+    // after the window reduction the lane stores channel 4g + myr: the
+    // transposed reduction (below) leaves channel 2 (xc & 1) + yc on it
+    const int myr = 2 * (xc & 1) + yc;
     const bool storer = widx < 4;
     const int chan = g.PD * g.PH * g.PW;
     const int cbase = (4 * gq + myr) * chan;       // element offset of this lane's channel in the sample
@@ -798,74 +752,54 @@ __global__ __launch_bounds__(NTH) void k_conv_ring(RingParams P) {
             const int px = 2 * tx + (xc >> 1);
             float mine = 0.0f;
             int kmine = 0;
-            if constexpr (RT_EPI_T) {
-                // transposed window reduction: each DPP step halves the
-                // channels a lane keeps while it reduces over a window bit
-                // (bit 0: xor 1; bit 2: row_ror 4, the partner's bit 2 always
-                // differs; bit 3: row_ror 8, same channel) -- 3 / 6 DPP moves
-                // for the 4 channels instead of 12 / 24.  (value, index) pairs
-                // combine as max value, smallest window index among equals:
-                // torch's first maximum in (z, y, x) order.
-                int vi[4];
+            // transposed window reduction: each DPP step halves the
+            // channels a lane keeps while it reduces over a window bit
+            // (bit 0: xor 1; bit 2: row_ror 4, the partner's bit 2 always
+            // differs; bit 3: row_ror 8, same channel) -- 3 / 6 DPP moves
+            // for the 4 channels instead of 12 / 24.  (value, index) pairs
+            // combine as max value, smallest window index among equals:
+            // torch's first maximum in (z, y, x) order.
+            int vi[4];
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr)
-                    vi[rr] = __float_as_int(valid ? fmaxf(acc[u][rr] + bias[rr], 0.0f) : -INFINITY);
-                const bool b0 = (c & 1) != 0, b2 = ((c >> 2) & 1) != 0;
-                auto comb = [](int& v, int& k, int rv, int rk) {
-                    const int m = max(v, rv);
-                    k = min(v == m ? k : 8, rv == m ? rk : 8);
-                    v = m;
-                };
-                int va = b0 ? vi[2] : vi[0], vb = b0 ? vi[3] : vi[1];
-                const int ra = __builtin_amdgcn_mov_dpp(b0 ? vi[0] : vi[2], 0xB1, 0xF, 0xF, true);
-                const int rb = __builtin_amdgcn_mov_dpp(b0 ? vi[1] : vi[3], 0xB1, 0xF, 0xF, true);
-                int ka = widx, kb = widx;
-                if constexpr (TRAIN) {
-                    comb(va, ka, ra, widx ^ 1);
-                    comb(vb, kb, rb, widx ^ 1);
-                } else {
-                    va = max(va, ra);
-                    vb = max(vb, rb);
-                }
-                int v = b2 ? vb : va, k = b2 ? kb : ka;
-                const int rv2 = __builtin_amdgcn_mov_dpp(b2 ? va : vb, 0x124, 0xF, 0xF, true);
-                if constexpr (TRAIN) {
-                    const int rk2 = __builtin_amdgcn_mov_dpp(b2 ? ka : kb, 0x124, 0xF, 0xF, true);
-                    comb(v, k, rv2, rk2);
-                    const int rv3 = __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, true);
-                    const int rk3 = __builtin_amdgcn_mov_dpp(k, 0x128, 0xF, 0xF, true);
-                    comb(v, k, rv3, rk3);
-                    kmine = k;
-                } else {
-                    v = max(v, rv2);
-                    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, true));
-                }
-                mine = __int_as_float(v);
+            for (int rr = 0; rr < 4; ++rr)
+                vi[rr] = __float_as_int(valid ? fmaxf(acc[u][rr] + bias[rr], 0.0f) : -INFINITY);
+            const bool b0 = (c & 1) != 0, b2 = ((c >> 2) & 1) != 0;
+            auto comb = [](int& v, int& k, int rv, int rk) {
+                const int m = max(v, rv);
+                k = min(v == m ? k : 8, rv == m ? rk : 8);
+                v = m;
+            };
+            int va = b0 ? vi[2] : vi[0], vb = b0 ? vi[3] : vi[1];
+            const int ra = __builtin_amdgcn_mov_dpp(b0 ? vi[0] : vi[2], 0xB1, 0xF, 0xF, true);
+            const int rb = __builtin_amdgcn_mov_dpp(b0 ? vi[1] : vi[3], 0xB1, 0xF, 0xF, true);
+            int ka = widx, kb = widx;
+            if constexpr (TRAIN) {
+                comb(va, ka, ra, widx ^ 1);
+                comb(vb, kb, rb, widx ^ 1);
             } else {
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    const float v = valid ? fmaxf(acc[u][rr] + bias[rr], 0.0f) : -INFINITY;
-                    const float m = win_max(v);
-                    mine = rr == myr ? m : mine;
-                    if constexpr (TRAIN) {
-                        const int k = win_min(v == m ? widx : 8);  // torch: first maximum in (z, y, x) window order
-                        kmine = rr == myr ? k : kmine;
-                    }
-                }
+                va = max(va, ra);
+                vb = max(vb, rb);
             }
+            int v = b2 ? vb : va, k = b2 ? kb : ka;
+            const int rv2 = __builtin_amdgcn_mov_dpp(b2 ? va : vb, 0x124, 0xF, 0xF, true);
+            if constexpr (TRAIN) {
+                const int rk2 = __builtin_amdgcn_mov_dpp(b2 ? ka : kb, 0x124, 0xF, 0xF, true);
+                comb(v, k, rv2, rk2);
+                const int rv3 = __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, true);
+                const int rk3 = __builtin_amdgcn_mov_dpp(k, 0x128, 0xF, 0xF, true);
+                comb(v, k, rv3, rk3);
+                kmine = k;
+            } else {
+                v = max(v, rv2);
+                v = max(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, true));
+            }
+            mine = __int_as_float(v);
             const bool st = ok && storer && tx < g.XT && py < g.PH && px < g.PW;
             const int o = cbase + (pz * g.PH + py) * g.PW + px;
-            if constexpr (RT_C3D_EXP == 5) {
-                if (st) {
-                    P.y[(int64_t)b * CO * chan + o] = mine;
-                    if constexpr (TRAIN) P.amax[(int64_t)b * CO * chan + o] = (uint8_t)(kmine | (mine > 0.0f ? 8 : 0));
-                }
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mine), ysrd, st ? 4 * o : INT32_MIN, 0, 0);
-                if constexpr (TRAIN)
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kmine | (mine > 0.0f ? 8 : 0)), asrd,
-                                                         st ? o : INT32_MIN, 0, 0);
-            }
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mine), ysrd, st ? 4 * o : INT32_MIN, 0, 0);
+            if constexpr (TRAIN)
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kmine | (mine > 0.0f ? 8 : 0)), asrd,
+                                                     st ? o : INT32_MIN, 0, 0);
         }
     };
 
@@ -1276,7 +1210,7 @@ RingGeom make_ring_geom_zs(const rt_conv_layer* L, int B) {
     r.npiece = (r.SLOT + 63) / 64;
     r.nyb = (g.PH + PYB - 1) / PYB;
     const int64_t per_chunk = (int64_t)r.nyb * B * G;
-    int nzc = (int)std::min<int64_t>(g.PD, std::max<int64_t>(1, (RT_ZS_BLOCKS + per_chunk - 1) / per_chunk));
+    int nzc = (int)std::min<int64_t>(g.PD, std::max<int64_t>(1, (kZsBlocks + per_chunk - 1) / per_chunk));
     r.ZC = (g.PD + nzc - 1) / nzc;
     r.ZC = (r.ZC + G / 2 - 1) / (G / 2) * (G / 2);  // whole tiles (G / 2 pooled rows each) per chunk
     return r;
@@ -1302,7 +1236,7 @@ constexpr int ring_zs_slots() {
 // B = Wext hi / lo images in registers; the accumulator layout and the
 // epilogue are the f32 kernel's.
 template <int G, int PYB, bool TRAIN, bool BF = false>
-__global__ __launch_bounds__(512) RT_ZS_FWD_ATTR void k_conv_ring_zs(RingParams P) {
+__global__ __launch_bounds__(512) void k_conv_ring_zs(RingParams P) {
     extern __shared__ float xs[];
     constexpr int CPG = CO / G, NW = 8, ZX = G + 2, KS = CPG * ZX * 9 / 4, NB = KS / 9, NR = ring_zs_slots<G>();
     constexpr int NV = ZX * (CPG / 4) * 9, NVB = (NV + 7) / 8;  // bf16x3: k values per lane group, MFMAs
@@ -1556,7 +1490,7 @@ int launch_ring_zs(const rt_conv_layer* L, int32_t B, const float* x, const int6
                (rg.npiece + 7) / 8 <= ring_max_pieces<CO / G, 1>();
     };
     RingGeom rg = make_ring_geom_zs<G, 8>(L, B);
-    if (RT_ZS_FWD_MAXPYB >= 8 && fits(rg)) return launch_ring_zs_k<G, 8>(rg, B, x, rows, w, bias, y, amax, st);
+    if (fits(rg)) return launch_ring_zs_k<G, 8>(rg, B, x, rows, w, bias, y, amax, st);
     rg = make_ring_geom_zs<G, 4>(L, B);
     if (fits(rg)) return launch_ring_zs_k<G, 4>(rg, B, x, rows, w, bias, y, amax, st);
     rg = make_ring_geom_zs<G, 2>(L, B);
@@ -1582,7 +1516,7 @@ template <int CIN, int G>
 int launch_fwd_ring(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
                     const float* bias, float* y, uint8_t* amax, hipStream_t st) {
     constexpr int NTH = 512;
-    const bool vec4 = RT_C3D_EXP != 4 && CIN == 4 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
+    const bool vec4 = CIN == 4 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     auto fits = [&](const RingGeom& rg, int vec, size_t budget) {
         return (size_t)kRing * rg.SLOT * sizeof(float) <= budget &&
@@ -1591,18 +1525,6 @@ int launch_fwd_ring(const rt_conv_layer* L, int32_t B, const float* x, const int
                rg.g.W >= vec;
     };
     constexpr int PY_BIG = CIN == 4 ? 4 : 2;
-    if constexpr (CIN == 4) {
-        // RT_C3D_FWD_NTH=256 (A/B runs): 4-wave blocks on 2-row bands (4 blocks per CU)
-        static const bool small = [] {
-            const char* e = std::getenv("RT_C3D_FWD_NTH");
-            return e && std::atoi(e) == 256;
-        }();
-        if (small && vec4) {
-            const RingGeom rg = make_ring_geom<CIN, 2, 4>(L, B, 256);
-            if ((size_t)kRing * rg.SLOT * sizeof(float) <= 40 * 1024 && (rg.npiece + 3) / 4 <= ring_max_pieces<CIN, 4>())
-                return launch_ring_p<CIN, G, 2, 4, 256>(rg, B, x, rows, w, bias, y, amax, st);
-        }
-    }
     for (const size_t budget : {(size_t)(CIN == 4 ? 80 : 160) * 1024, (size_t)160 * 1024}) {
         if constexpr (CIN == 4) {
             if (vec4) {
@@ -1734,30 +1656,6 @@ constexpr int ncol_tiles() {
     return (CIN * 27 + 1 + 15) / 16;
 }
 constexpr int kWgradTiles = 7;  // column tiles per wave
-// ring weight gradient: column tiles per wave.  RT_WG_KT4=4 (A/B builds) runs
-// conv1's 7 tiles padded to 8 as 2 column groups of 4 x 4 position groups:
-// 122 VGPRs, 4 waves per SIMD (2 blocks per CU) instead of 2, but +1/7 MFMAs,
-// twice the dY loads and narrower y bands -- measured 15 % slower
-#ifndef RT_WG_KT4
-#define RT_WG_KT4 7
-#endif
-template <int CIN>
-constexpr int wg_kt() {
-    return CIN == 4 ? RT_WG_KT4 : kWgradTiles;
-}
-template <int CIN>
-constexpr int wg_wc() {  // column groups
-    return (ncol_tiles<CIN>() + wg_kt<CIN>() - 1) / wg_kt<CIN>();
-}
-template <int CIN>
-constexpr int wg_nct() {  // padded column tiles: a partial row holds 16 * wg_nct columns
-    return wg_wc<CIN>() * wg_kt<CIN>();
-}
-template <int CIN>
-constexpr int wg_wpe() {
-    return wg_kt<CIN>() < kWgradTiles ? 4 : RT_WG_WPE;
-}
-
 struct WgradParams {
     const float* x;
     const int64_t* rows;
@@ -1889,15 +1787,8 @@ __global__ __launch_bounds__(kThreads) void k_conv_wgrad(WgradParams P) {
     }
 }
 
-// Weight gradient, z-ring version (the launched one): a block owns a y band
-// of one sample at a time (samples blockIdx.z, + gridDim.z, ...) and sweeps
-// its pooled z rows with the forward's plane ring; the dY operand of the next
-// pooled row (pooled gradient + argmax byte per lane and position tile) is
-// loaded into registers together with the next planes' DMA, so one wait +
-// barrier per row covers both.  Column tiles and the MFMA mapping are those
-// of k_conv_wgrad.
-constexpr int kWgMaxTiles = 8;  // position tiles per wave and pooled row
-
+// Weight-gradient ring parameters (k_conv_wgrad_sparse): the forward's plane
+// ring over a y band of one sample at a time.
 struct WgradRingParams {
     const float* x;
     const int64_t* rows;
@@ -1908,318 +1799,11 @@ struct WgradRingParams {
     RingGeom rg;
 };
 
-template <int CIN, int PYB, int VEC>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VEC == 4 ? wg_wpe<CIN>() : RT_WG_WPE))) void k_conv_wgrad_ring(WgradRingParams P) {
-    extern __shared__ float xs[];
-    constexpr int NW = kThreads / 64;
-    constexpr int KT = wg_kt<CIN>();      // column tiles per wave
-    constexpr int NCT = wg_nct<CIN>();    // padded column tiles
-    constexpr int WC = wg_wc<CIN>();      // column groups (2 for conv1, 4 for the 16-channel stages)
-    constexpr int WP = NW / WC;           // position groups
-    // trailing tiles of a wave that can hold constant columns (k >= CIN*27)
-    constexpr int KC = NCT * 16 - CIN * 27 > 16 ? 2 : 1;
-    static_assert(NW % WC == 0 && KC <= KT, "column tiles");
-    const Geom& g = P.rg.g;
-    const int SLOT = P.rg.SLOT;
-    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wc = wave % WC, wp = wave / WC;
-    const int t0c = wc * KT;
-    const int py0 = blockIdx.x * PYB;
-    const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
-    RingLoader<CIN, VEC, NW> ld;
-    ld.init(P.rg, y0, x0, wave, lane);
-    // column 16(t0c + T) + c = (ci, tap): 4 * (in-plane LDS offset + g) + dz
-    // (one register per tile), or a constant B.  Only the wave's last tile
-    // can hold constants (columns CIN*27 .. NCT*16-1: conv1's tile 6, the
-    // 16-channel stages' tile 27), so one register carries them.
-    int kpk[KT];
-    float kconst[KC];  // tiles KT-KC..: -1 = gather, else the constant B value
-#pragma unroll
-    for (int j = 0; j < KC; ++j) kconst[j] = -1.0f;
-#pragma unroll
-    for (int T = 0; T < KT; ++T) {
-        const int k = 16 * (t0c + T) + c;
-        if (k < CIN * 27) {
-            const int ci = k / 27, q = k % 27;
-            kpk[T] = (ci * g.CS + ((q / 3) % 3) * g.YS + q % 3 + gq) * 4 + q / 9;
-        } else {
-            kpk[T] = gq * 4;
-            if (T >= KT - KC) kconst[T - (KT - KC)] = k == CIN * 27 ? 1.0f : 0.0f;
-        }
-    }
-    f4 acc[KT];
-#pragma unroll
-    for (int T = 0; T < KT; ++T) acc[T] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    const int ntile = PYB * g.XT;                     // position tiles per pooled row
-    const int ntw = (ntile - wp + WP - 1) / WP;       // this wave's: t = wp + WP * i
-    const int chan = g.PD * g.PH * g.PW;
-    for (int b = blockIdx.z; b < P.B; b += gridDim.z) {
-        const int64_t srow = P.rows ? P.rows[b] : b;
-        const float* xb = P.x + srow * (int64_t)CIN * g.D * g.H * g.W;
-        const uint8_t* amb = P.am + ((int64_t)b * CO + c) * chan;
-        const float* dpb = P.dP + ((int64_t)b * CO + c) * chan;
-        // one register per tile: tile i's dY of row k + 1 is loaded as soon as
-        // row k has consumed it (a rolling prefetch; a second buffer loaded at
-        // the row start measured 18 % slower in the z-shift kernel)
-        int abyte[kWgMaxTiles];
-        float ad[kWgMaxTiles];
-#if RT_WG_DYB
-        int abyte2[kWgMaxTiles] = {};
-        float ad2[kWgMaxTiles] = {};
-#endif
-        // lane (c, g) of tile t: channel c at the 4 positions 4q + g, all in pooled window px = 2tx + (g >> 1)
-        auto load_to = [&](int k, int i, int (&ab)[kWgMaxTiles], float (&av)[kWgMaxTiles]) {
-            const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
-            const int py = py0 + r, px = 2 * tx + (gq >> 1);
-            const bool ok = i < ntw && py < g.PH && px < g.PW;
-            const int o = (k * g.PH + py) * g.PW + px;
-            ab[i] = ok ? amb[o] : 0;
-            av[i] = ok ? dpb[o] : 0.0f;
-        };
-        auto load_a = [&](int k, int i) { load_to(k, i, abyte, ad); };
-        __syncthreads();  // the previous sample's ring reads are done
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ld.load(xb, P.rg, xs, i, i, wave, lane);
-#pragma unroll
-        for (int i = 0; i < kWgMaxTiles; ++i) load_a(0, i);
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        __syncthreads();
-        int sb = 0;
-        for (int k = 0; k < g.PD; ++k) {
-            const bool more = k + 1 < g.PD;
-            if (more) {
-                ld.load(xb, P.rg, xs, 2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4, wave, lane);
-                ld.load(xb, P.rg, xs, 2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5, wave, lane);
-#if RT_WG_DYB
-#pragma unroll
-                for (int i = 0; i < kWgMaxTiles; ++i) load_to(k + 1, i, abyte2, ad2);
-#endif
-            }
-            // per z-plane of the tile (q >> 1); the y half (q & 1) joins the
-            // wave-uniform tile offset
-            int kaddr[2][KT];
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int T = 0; T < KT; ++T) {
-                    int sl = sb + h + (kpk[T] & 3);
-                    sl = sl >= kRing ? sl - kRing : sl;
-                    kaddr[h][T] = sl * SLOT + (kpk[T] >> 2);
-                }
-#pragma unroll
-            for (int i = 0; i < kWgMaxTiles; ++i) {
-                if (i >= ntw) continue;
-                const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
-                if (py0 + r >= g.PH) continue;  // a tile row past the last pooled row: A = 0, no MFMAs
-                const int toff = 2 * r * g.YS + 4 * tx;
-                const int byte = abyte[i];
-                const float d = ad[i];
-                if (!RT_WG_DYB && more) load_a(k + 1, i);
-                // B gathered per z half (RT_WG_WPE 4: fewer live registers)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    float bv[2][KT];
-#pragma unroll
-                    for (int q = 0; q < 2; ++q)
-#pragma unroll
-                        for (int T = 0; T < KT; ++T)
-                            bv[q][T] = (T < KT - KC || kconst[T >= KT - KC ? T - (KT - KC) : 0] < 0.0f)
-                                           ? xs[kaddr[h][T] + toff + q * g.YS]
-                                           : kconst[T >= KT - KC ? T - (KT - KC) : 0];
-#pragma unroll
-                    for (int q = 0; q < 2; ++q) {  // position n = 4(2h + q) + g: zc = h, yc = q, xc = g
-                        const float a = ((byte & 8) && (byte & 7) == h * 4 + q * 2 + (gq & 1)) ? d : 0.0f;
-#pragma unroll
-                        for (int T = 0; T < KT; ++T) acc[T] = mfma4(a, bv[q][T], acc[T]);
-                    }
-                }
-            }
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-            __syncthreads();
-            sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
-#if RT_WG_DYB
-#pragma unroll
-            for (int i = 0; i < kWgMaxTiles; ++i) {
-                abyte[i] = abyte2[i];
-                ad[i] = ad2[i];
-            }
-#endif
-        }
-    }
-    // D (lane (c, g)): rows co = 4g + r, column 16T + c; the WP position
-    // groups are summed through LDS (the ring's space) in a fixed order
-    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    float* out = P.part + (size_t)blk * (CO * NCT * 16);
-    constexpr int REG = CO * NCT * 16;
-    __syncthreads();
-    float* R = xs;
-#pragma unroll
-    for (int T = 0; T < KT; ++T)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) R[wp * REG + (4 * gq + r) * (NCT * 16) + 16 * (t0c + T) + c] = acc[T][r];
-    __syncthreads();
-    for (int i = threadIdx.x; i < REG; i += kThreads) {
-        float v = R[i];
-#pragma unroll
-        for (int k = 1; k < WP; ++k) v += R[k * REG + i];
-        out[i] = v;
-    }
-}
-
-// Weight gradient of the groups = 2 stage in the z-shift form (one ring of all
-// 16 channels, as k_conv_wgrad_ring): D[m = (co, s)][n = (ci, tz', ty, tx)] =
-// sum over the (y, x) positions of a pooled row of dY[co][2k + s][y][x] *
-// X[ci][2k + tz'][y + ty][x + tx], per group (rows = its 8 output channels x
-// the row's 2 conv planes s, columns = its 8 input channels x 4 ring planes x
-// 9 in-plane taps = 18 column tiles); dW[co][ci][tz] = sum_s D[(co, s)][(ci,
-// tz + s)].  A position tile is 2 rows x 4 x of one plane pair (2 k-steps, z
-// folded into the rows): 2 x 36 column tiles x 2 k-steps per 16 dense
-// positions against 28 x 4 in the dense form (1.56x fewer MFMAs).  Lane (c, g)
-// holds row (co = c >> 1, s = c & 1) at positions x = 4tx + g, one pooling
-// window per tile as in the dense kernel.  db by VALU sums of the A values.
-// Waves: 4 column groups (group = wc / 2, tiles (wc % 2) * 9 ..) x 2 position groups.
-constexpr int kWzTiles = 9;
-
-template <int PYB, int MT>
-__global__ __launch_bounds__(kThreads) void k_conv_wgrad_ring_zs(WgradRingParams P) {
-    extern __shared__ float xs[];
-    constexpr int G = 2, CPG = CO / G, NW = kThreads / 64, WC = 4, WP = NW / WC, NCOL = CPG * 36;
-    const Geom& g = P.rg.g;
-    const int SLOT = P.rg.SLOT;
-    const int lane = threadIdx.x & 63, c = lane & 15, gq = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wc = wave % WC, wp = wave / WC, grp = wc / 2, t0 = (wc % 2) * kWzTiles;
-    const bool dbw = wc % 2 == 0;  // the waves that also sum db (one per group and position group)
-    const int py0 = blockIdx.x * PYB;
-    const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
-    RingLoader<16, 1, NW> ld;
-    ld.init(P.rg, y0, x0, wave, lane);
-    // column 16(t0 + T) + c of the group = (ci, tz', ty, tx): in-plane LDS offset and ring plane tz'
-    int kin[kWzTiles], kdz[kWzTiles];
-#pragma unroll
-    for (int T = 0; T < kWzTiles; ++T) {
-        const int n = 16 * (t0 + T) + c, ci = n / 36, rem = n % 36, q9 = rem % 9;
-        kin[T] = (grp * CPG + ci) * g.CS + (q9 / 3) * g.YS + q9 % 3;
-        kdz[T] = rem / 9;
-    }
-    f4 acc[kWzTiles];
-#pragma unroll
-    for (int T = 0; T < kWzTiles; ++T) acc[T] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    float dbacc = 0.0f;
-    const int ntile = PYB * g.XT;
-    const int ntw = (ntile - wp + WP - 1) / WP;
-    const int chan = g.PD * g.PH * g.PW;
-    const int co = grp * CPG + (c >> 1), sz = c & 1;
-    for (int b = blockIdx.z; b < P.B; b += gridDim.z) {
-        const int64_t srow = P.rows ? P.rows[b] : b;
-        const float* xb = P.x + srow * (int64_t)CO * g.D * g.H * g.W;
-        const uint8_t* amb = P.am + ((int64_t)b * CO + co) * chan;
-        const float* dpb = P.dP + ((int64_t)b * CO + co) * chan;
-        // one register per tile: tile i's dY of row k + 1 is loaded as soon as
-        // row k has consumed it (a rolling prefetch without a second buffer)
-        int abyte[MT];
-        float ad[MT];
-        // lane (c, g) of tile t = (r, tx): window (co, k, py0 + r, 2tx + (g >> 1))
-        auto load_a = [&](int k, int i) {
-            const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
-            const int py = py0 + r, px = 2 * tx + (gq >> 1);
-            const bool ok = i < ntw && py < g.PH && px < g.PW;
-            const int o = (k * g.PH + py) * g.PW + px;
-            abyte[i] = ok ? amb[o] : 0;
-            ad[i] = ok ? dpb[o] : 0.0f;
-        };
-        __syncthreads();  // the previous sample's ring reads are done
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ld.load(xb, P.rg, xs, i, i, wave, lane);
-#pragma unroll
-        for (int i = 0; i < MT; ++i) load_a(0, i);
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        __syncthreads();
-        int sb = 0;
-        for (int k = 0; k < g.PD; ++k) {
-            const bool more = k + 1 < g.PD;
-            if (more) {
-                ld.load(xb, P.rg, xs, 2 * k + 4, sb + 4 >= kRing ? sb + 4 - kRing : sb + 4, wave, lane);
-                ld.load(xb, P.rg, xs, 2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5, wave, lane);
-            }
-            int kaddr[kWzTiles];
-#pragma unroll
-            for (int T = 0; T < kWzTiles; ++T) {
-                int sl = sb + kdz[T];
-                sl = sl >= kRing ? sl - kRing : sl;
-                kaddr[T] = sl * SLOT + gq + kin[T];
-            }
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                if (i >= ntw) continue;  // (not break: a multi-exit loop of 16 stays rolled)
-                const int t = wp + WP * i, r = t / g.XT, tx = t - r * g.XT;
-                if (py0 + r >= g.PH) continue;  // a tile row past the last pooled row: A = 0, no MFMAs
-                const int toff = 2 * r * g.YS + 4 * tx;
-                const int byte = abyte[i];
-                const float d = ad[i];
-                if (more) load_a(k + 1, i);
-                float bv[2][kWzTiles];
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-#pragma unroll
-                    for (int T = 0; T < kWzTiles; ++T) bv[q][T] = xs[kaddr[T] + toff + q * g.YS];
-                float a[2];
-#pragma unroll
-                for (int q = 0; q < 2; ++q)  // k-step q = conv row 2r + q; window rank (s, q, g & 1)
-                    a[q] = ((byte & 8) && (byte & 7) == sz * 4 + q * 2 + (gq & 1)) ? d : 0.0f;
-                if (dbw) dbacc += a[0] + a[1];
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-#pragma unroll
-                    for (int T = 0; T < kWzTiles; ++T) acc[T] = mfma4(a[q], bv[q][T], acc[T]);
-            }
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-            __syncthreads();
-            sb = sb + 2 >= kRing ? sb + 2 - kRing : sb + 2;
-        }
-    }
-    // D (lane (c, g)): row m = 4g + r = (co, s), column 16(t0 + T) + c of the
-    // group -> LDS [WP][G][16][NCOL], db lanes -> [WP][G][64]; then the s pairs,
-    // position groups (and db lanes) are summed in a fixed order
-    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    constexpr int NCT = ncol_tiles<16>();
-    float* out = P.part + (size_t)blk * (CO * NCT * 16);
-    __syncthreads();
-    float* R = xs;
-    float* Rdb = xs + WP * G * 16 * NCOL;
-#pragma unroll
-    for (int T = 0; T < kWzTiles; ++T)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) R[((wp * G + grp) * 16 + 4 * gq + r) * NCOL + 16 * (t0 + T) + c] = acc[T][r];
-    if (dbw) Rdb[(wp * G + grp) * 64 + lane] = dbacc;
-    __syncthreads();
-    for (int i = threadIdx.x; i < G * CPG * CPG * 27; i += kThreads) {
-        const int gg = i / (CPG * CPG * 27), rem = i % (CPG * CPG * 27), col = rem / (CPG * 27),
-                  rem2 = rem % (CPG * 27), cil = rem2 / 27, q = rem2 % 27;
-        float v = 0.0f;
-#pragma unroll
-        for (int w2 = 0; w2 < WP; ++w2)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-                v += R[((w2 * G + gg) * 16 + 2 * col + s2) * NCOL + cil * 36 + (q / 9 + s2) * 9 + q % 9];
-        out[(gg * CPG + col) * (NCT * 16) + (gg * CPG + cil) * 27 + q] = v;
-    }
-    if (threadIdx.x < CO) {
-        const int gg = threadIdx.x / CPG, col = threadIdx.x % CPG;
-        float v = 0.0f;
-        for (int w2 = 0; w2 < WP; ++w2)
-            for (int l = 0; l < 4; ++l)
-                for (int s2 = 0; s2 < 2; ++s2) v += Rdb[(w2 * G + gg) * 64 + 16 * l + 2 * col + s2];
-        out[threadIdx.x * (NCT * 16) + 16 * 27] = v;
-    }
-}
-
 // ---- weight gradient through the pooling argmax (the launched one) ----------
 // dW[co][ci][tap] = sum over pooled windows w of dY[co][w] * X[ci][p(co, w) + tap],
 // p = the conv position the window's argmax names; db[co] = sum_w dY[co][w].
-// The dense form (k_conv_wgrad_ring) multiplies every conv position's
-// gradient, 7 of 8 of which the max-pool zeroed; here each (co, window) is
+// The dense form (an MFMA ring kernel, removed) multiplies every
+// conv position's gradient, 7 of 8 of which the max-pool zeroed; here each (co, window) is
 // one 27-tap gather of its argmax patch, 1/8 of the multiply-adds, as f32
 // FMAs on the VALU with the patch read from the forward's plane ring.
 // Thread = (window stream s, output channel co, in-group input channel cig):
@@ -2254,9 +1838,6 @@ RingGeom make_sparse_geom(const rt_conv_layer* L, int B) {
 }
 
 constexpr int kWgSparseMaxG = 4;  // a band row holds <= NT * 4 (channel, window) entries
-#ifndef RT_WGS_U
-#define RT_WGS_U 1  // windows per loop iteration of k_conv_wgrad_sparse (2: A/B builds)
-#endif
 
 template <int CIN, int G, int PYB, int NT>
 __global__ __launch_bounds__(NT) void k_conv_wgrad_sparse(WgradRingParams P) {
@@ -2383,22 +1964,6 @@ __global__ __launch_bounds__(NT) void k_conv_wgrad_sparse(WgradRingParams P) {
                 px -= g.PW;
                 ++r;
             }
-#if RT_WGS_U == 2
-            // two windows per iteration: both gathers in flight before the FMAs
-            for (; w + NS < nwin && py0 + r < g.PH; w += 2 * NS) {
-                int r2 = r, px2 = px;
-                advance(r2, px2);
-                float va[27], vb[27];
-                const float ga = gather(w, r, px, va);
-                const bool second = py0 + r2 < g.PH;  // uniform
-                const float gb = second ? gather(w + NS, r2, px2, vb) : 0.0f;
-                accumulate(ga, va);
-                if (second) accumulate(gb, vb);
-                r = r2;
-                px = px2;
-                advance(r, px);
-            }
-#endif
             for (; w < nwin; w += NS) {
                 if (py0 + r >= g.PH) break;  // uniform: the band's rows past the volume
                 float v[27];
@@ -2977,7 +2542,7 @@ RingGeom make_dgrad_ring_geom_zs(const rt_conv_layer* L, int B) {
     r.SLOT = round_mod(CO / G * g.CS, 16);
     const int KD = (g.D + 1) / 2;
     const int64_t per_chunk = (int64_t)r.nyb * B * G;
-    const int nzc = (int)std::min<int64_t>(KD, std::max<int64_t>(1, (RT_ZS_BLOCKS + per_chunk - 1) / per_chunk));
+    const int nzc = (int)std::min<int64_t>(KD, std::max<int64_t>(1, (kZsBlocks + per_chunk - 1) / per_chunk));
     r.ZC = (KD + nzc - 1) / nzc;
     r.ZC = (r.ZC + G / 2 - 1) / (G / 2) * (G / 2);  // whole tile rows per chunk
     return r;
@@ -3065,125 +2630,7 @@ int launch_wgrad(const rt_conv_layer* L, int32_t B, const float* x, const int64_
     return RT_OK;
 }
 
-// ring weight gradient: plan (y band, DMA width) and launch
-template <int CIN, int PYB, int VEC>
-int launch_wgrad_ring_k(const RingGeom& rg, int32_t B, int gz, const float* x, const int64_t* rows,
-                        const float* dP, const uint8_t* am, float* ws, hipStream_t st) {
-    WgradRingParams P{x, rows, dP, am, ws, B, rg};
-    constexpr int NCT = wg_nct<CIN>();
-    constexpr int WC = wg_wc<CIN>(), WP = (kThreads / 64) / WC;
-    const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * CO * NCT * 16) * sizeof(float);
-    static bool attr = false;
-    if (!attr) {
-        if (const int rc_lds = allow_big_lds(&k_conv_wgrad_ring<CIN, PYB, VEC>)) return rc_lds;
-        attr = true;
-    }
-    hipLaunchKernelGGL((k_conv_wgrad_ring<CIN, PYB, VEC>), dim3(rg.nyb, 1, gz), dim3(kThreads), lds, st, P);
-    return RT_OK;
-}
-
-// weight-gradient ring grids: at most this many blocks (samples looped per block; A/B builds)
-#ifndef RT_WG_BLOCKS
-#define RT_WG_BLOCKS 512
-#endif
-constexpr int kWgradRingBlocks = RT_WG_BLOCKS;
-
-template <int PYB, int MT>
-int launch_wgrad_ring_zs_k(const RingGeom& rg, int32_t B, int gz, const float* x, const int64_t* rows,
-                           const float* dP, const uint8_t* am, float* ws, hipStream_t st) {
-    WgradRingParams P{x, rows, dP, am, ws, B, rg};
-    constexpr int WP = kThreads / 64 / 4;
-    const size_t lds =
-        std::max((size_t)kRing * rg.SLOT, (size_t)WP * 2 * 16 * (CO / 2 * 36) + WP * 2 * 64) * sizeof(float);
-    static bool attr = false;
-    if (!attr) {
-        if (const int rc_lds = allow_big_lds(&k_conv_wgrad_ring_zs<PYB, MT>)) return rc_lds;
-        attr = true;
-    }
-    hipLaunchKernelGGL((k_conv_wgrad_ring_zs<PYB, MT>), dim3(rg.nyb, 1, gz), dim3(kThreads), lds, st, P);
-    return RT_OK;
-}
-
-template <int CIN>
-int launch_wgrad_ring(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
-                      const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
-    constexpr int NCT = wg_nct<CIN>();
-    constexpr int WC = wg_wc<CIN>(), WP = (kThreads / 64) / WC;
-    size_t budget = (CIN == 4 ? 80 : 160) * 1024;  // conv1 retries with 160 KiB below (wide planes)
-    const bool vec4 = RT_C3D_EXP != 4 && CIN == 4 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
-                      (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    auto fits = [&](const RingGeom& rg, int vec) {
-        const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * CO * NCT * 16) * sizeof(float);
-        return lds <= budget &&
-               (rg.npiece + kThreads / 64 - 1) / (kThreads / 64) <=
-                   (vec == 4 ? ring_max_pieces<CIN, 4>() : ring_max_pieces<CIN, 1>()) &&
-               (rg.g.PYB_tiles + WP - 1) / WP <= kWgMaxTiles && rg.g.W >= vec;
-    };
-    int rc = RT_ELIMIT, nblk = 0;
-    auto go = [&](const RingGeom& rg, auto launch) {
-        const int gz = std::max(1, std::min<int>(B, kWgradRingBlocks / std::max(1, rg.nyb)));
-        nblk = rg.nyb * gz;
-        if ((int64_t)nblk * CO * NCT * 16 > ws_floats) return rt_internal_fail(RT_EINVAL, "rt_conv_wgrad: workspace too small");
-        return launch(rg, gz);
-    };
-    constexpr int PY_BIG = CIN == 4 ? 4 : 2;
-    // groups = 2 with no pool padding: the z-shift kernel (RT_C3D_WGZS=0: the dense one, A/B runs)
-    static const bool zs_env = [] {
-        const char* e = std::getenv("RT_C3D_WGZS");
-        return !(e && e[0] == '0');
-    }();
-    const bool zs = zs_env && L->groups == 2 && L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0;
-    if constexpr (CIN == 16) {
-        // z-shift: wider y bands (more MFMA work per row barrier), up to 16 tiles per wave
-        auto zs_fits = [&](const RingGeom& rg, int pyb, int mt) {
-            const size_t lds = std::max((size_t)kRing * rg.SLOT, (size_t)WP * 2 * 16 * (CO / 2 * 36) + WP * 2 * 64);
-            return lds * sizeof(float) <= budget && (rg.npiece + 7) / 8 <= ring_max_pieces<16, 1>() &&
-                   (pyb * rg.g.XT + WP - 1) / WP <= mt;
-        };
-#define RT_WZ_TRY(PYB_, MT_)                                                                          \
-    if (zs && rc == RT_ELIMIT) {                                                                      \
-        RingGeom rg = make_ring_geom<CIN, PYB_, 1, RT_WG_SR>(L, B, kThreads);                         \
-        if (zs_fits(rg, PYB_, MT_))                                                                   \
-            rc = go(rg, [&](const RingGeom& r, int gz) {                                              \
-                return launch_wgrad_ring_zs_k<PYB_, MT_>(r, B, gz, x, rows, dP, am, ws, st);          \
-            });                                                                                       \
-    }
-        if (RT_WZ_MAXPYB >= 4) RT_WZ_TRY(4, 16)
-        RT_WZ_TRY(2, 8)
-        RT_WZ_TRY(1, 8)
-#undef RT_WZ_TRY
-    }
-#define RT_WG_TRY(PYB_, VEC_)                                                                          \
-    {                                                                                                 \
-        RingGeom rg = make_ring_geom<CIN, PYB_, VEC_, RT_WG_SR>(L, B, kThreads);                      \
-        rg.g.PYB_tiles = PYB_ * rg.g.XT;                                                              \
-        if (rc == RT_ELIMIT && fits(rg, VEC_))                                                        \
-            rc = go(rg, [&](const RingGeom& r, int gz) {                                              \
-                return launch_wgrad_ring_k<CIN, PYB_, VEC_>(r, B, gz, x, rows, dP, am, ws, st);       \
-            });                                                                                       \
-    }
-    for (int pass = 0; pass < (CIN == 4 ? 2 : 1) && rc == RT_ELIMIT; ++pass) {
-        if (pass) budget = 160 * 1024;
-        if constexpr (CIN == 4) {
-            if (vec4) {
-                RT_WG_TRY(PY_BIG, 4)
-                RT_WG_TRY(PY_BIG / 2, 4)
-                RT_WG_TRY(PY_BIG / 4, 4)
-            }
-        }
-        RT_WG_TRY(PY_BIG, 1)
-        RT_WG_TRY(PY_BIG / 2, 1)
-        if constexpr (PY_BIG / 4 >= 1) RT_WG_TRY(PY_BIG / 4, 1)
-    }
-#undef RT_WG_TRY
-    if (rc != RT_OK) return rc;  // RT_ELIMIT: the caller falls back to the tile kernel
-    const int nout = CO * (L->cin / L->groups) * 27 + CO;
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3((nout + 63) / 64), dim3(64 * kRedWaves), 0, st, (const float*)ws, nblk, L->cin,
-                       L->groups, NCT * 16, dw, db);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
-    return RT_OK;
-}
+constexpr int kWgradRingBlocks = 512;  // sparse weight-gradient grid (256 / 1024 blocks measured within 1-2 %)
 
 // the sparse weight gradient: two-row bands (one-row for wide 16-channel
 // planes), one partial row per block, k_wgrad_reduce over ncol = cin*27 + 1
@@ -3219,20 +2666,10 @@ int launch_wgrad_sparse_k(const rt_conv_layer* L, int32_t B, const float* x, con
 template <int CIN, int G>
 int launch_wgrad_sparse(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                         const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
-    static const int nt = [] {
-        const char* e = std::getenv("RT_WGS_NT");
-        return e && std::atoi(e) == 512 ? 512 : 256;
-    }();
-    static const int pyb2 = [] {  // RT_WGS_PYB=2 (A/B runs): two-row bands first (measured slower at 256 threads)
-        const char* e = std::getenv("RT_WGS_PYB");
-        return e && e[0] == '2';
-    }();
-    int rc = RT_ELIMIT;
-    if (nt == 256) {
-        if (pyb2) rc = launch_wgrad_sparse_k<CIN, G, 2, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
-        if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 1, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
-        if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 2, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
-    }
+    // 256-thread blocks on one-row bands (512-thread blocks and two-row bands
+    // measured 3-4 % slower), the others where those do not fit
+    int rc = launch_wgrad_sparse_k<CIN, G, 1, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
+    if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 2, 256>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
     if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 2, 512>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
     if (rc == RT_ELIMIT) rc = launch_wgrad_sparse_k<CIN, G, 1, 512>(L, B, x, rows, dP, am, dw, db, ws, ws_floats, st);
     return rc;
@@ -3294,7 +2731,6 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     if (bad_layer(L) || batch < 1 || batch > 65535 || !x_d || !w_d || !b_d || !y_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_fwd: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (RT_C3D_EXP == 3) return fwd_tile(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);  // A/B builds
     int rc = RT_ELIMIT;
     if (L->cin == 4) {
         // f32: the Winograd kernel; bf16x3 (and planes too wide for its ring):
@@ -3304,12 +2740,8 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     } else if (L->groups == 1) {
         rc = launch_fwd_ring<16, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     } else {
-        // grouped stages: the z-shift ring kernel (RT_C3D_ZS=0: the dense ring kernel, A/B runs)
-        static const bool zs = [] {
-            const char* e = std::getenv("RT_C3D_ZS");
-            return !(e && e[0] == '0');
-        }();
-        if (zs && (int64_t)batch * L->groups <= 65535)
+        // grouped stages: the z-shift ring kernel, else the dense ring kernel
+        if ((int64_t)batch * L->groups <= 65535)
             rc = L->groups == 2 ? launch_ring_zs<2>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st)
                                 : launch_ring_zs<4>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
         if (rc == RT_ELIMIT)
@@ -3325,11 +2757,10 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
 
 extern "C" int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* L, int32_t batch) {
     if (bad_layer(L) || batch < 1) return 0;
-    // ring: at most kWgradRingBlocks partial rows (one per block); the tile
-    // kernel (fallback for planes too wide for the ring) may need more
-    const int64_t ring = (int64_t)kWgradRingBlocks * CO * (L->cin == 4 ? wg_nct<4>() : wg_nct<16>()) * 16;
-    const int64_t sparse = (int64_t)2 * kWgradRingBlocks * CO * (L->cin * 27 + 1);  // 256-thread blocks: 2x the rows
-    return std::max(std::max(ring, sparse), wgrad_tile_ws(L, batch));
+    // the sparse ring kernel: at most 2 x kWgradRingBlocks partial rows (256-thread
+    // blocks); the tile kernel (fallback for planes too wide for the ring) may need more
+    const int64_t sparse = (int64_t)2 * kWgradRingBlocks * CO * (L->cin * 27 + 1);
+    return std::max(sparse, wgrad_tile_ws(L, batch));
 }
 
 extern "C" int rt_conv_relu_pool_wgrad(const rt_conv_layer* L, int32_t batch, const float* x_d, const int64_t* rows_d,
@@ -3338,29 +2769,17 @@ extern "C" int rt_conv_relu_pool_wgrad(const rt_conv_layer* L, int32_t batch, co
     if (bad_layer(L) || batch < 1 || !x_d || !dy_d || !argmax_d || !dw_d || !db_d || !ws_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_wgrad: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // the gather through the pooling argmax (RT_C3D_WGSPARSE=0: the dense MFMA ring kernels, A/B runs)
-    static const bool sparse = [] {
-        const char* e = std::getenv("RT_C3D_WGSPARSE");
-        return !(e && e[0] == '0');
-    }();
-    if (sparse && RT_C3D_EXP != 3) {
-        int rc = RT_ELIMIT;
-        if (L->cin == 4)
-            rc = launch_wgrad_sparse<4, 1>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
-        else if (L->groups == 1)
-            rc = launch_wgrad_sparse<16, 1>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
-        else if (L->groups == 2)
-            rc = launch_wgrad_sparse<16, 2>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
-        else
-            rc = launch_wgrad_sparse<16, 4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
-        if (rc != RT_ELIMIT) return rc;
-    }
-    if (RT_C3D_EXP != 3) {
-        const int rc = L->cin == 4
-                           ? launch_wgrad_ring<4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st)
-                           : launch_wgrad_ring<16>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
-        if (rc != RT_ELIMIT) return rc;
-    }
+    // the gather through the pooling argmax; planes too wide for its ring: the tile kernel
+    int rc = RT_ELIMIT;
+    if (L->cin == 4)
+        rc = launch_wgrad_sparse<4, 1>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+    else if (L->groups == 1)
+        rc = launch_wgrad_sparse<16, 1>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+    else if (L->groups == 2)
+        rc = launch_wgrad_sparse<16, 2>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+    else
+        rc = launch_wgrad_sparse<16, 4>(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
+    if (rc != RT_ELIMIT) return rc;
     return wgrad_tile(L, batch, x_d, rows_d, dy_d, argmax_d, dw_d, db_d, ws_d, ws_floats, st);
 }
 
@@ -3369,23 +2788,15 @@ extern "C" int rt_conv_relu_pool_dgrad(const rt_conv_layer* L, int32_t batch, co
     if (bad_layer(L) || L->cin != 16 || batch < 1 || batch > 65535 || !w_d || !dy_d || !argmax_d || !dx_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_dgrad: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // the ring kernel (RT_C3D_DGR=0: the tile kernel, A/B runs)
-    static const bool ring = [] {
-        const char* e = std::getenv("RT_C3D_DGR");
-        return !(e && e[0] == '0');
-    }();
-    // grouped stages: the z-shift form (RT_C3D_DGZS=0: the dense ring kernel, A/B runs)
-    static const bool zs = [] {
-        const char* e = std::getenv("RT_C3D_DGZS");
-        return !(e && e[0] == '0');
-    }();
+    // grouped stages: the z-shift ring kernel; then the dense ring kernel; the
+    // tile kernel for padded pools
     const bool pad0 = L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0;
-    if (ring && zs && pad0 && L->groups > 1 && (int64_t)batch * L->groups <= 65535) {
+    if (pad0 && L->groups > 1 && (int64_t)batch * L->groups <= 65535) {
         const int rc = L->groups == 2 ? launch_dgrad_ring_zs<2>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
                                       : launch_dgrad_ring_zs<4>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
         if (rc != RT_ELIMIT) return rc;
     }
-    if (ring && pad0) {
+    if (pad0) {
         const int rc = L->groups == 1   ? launch_dgrad_ring<1>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
                        : L->groups == 2 ? launch_dgrad_ring<2>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
                                         : launch_dgrad_ring<4>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
