@@ -859,101 +859,130 @@ int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* ro
 }
 
 // ---------------------------------------------------------------------------
-// conv1 forward in the Winograd form F(2x2x2, 3x3x3) on f32 MFMA (the launched
-// f32 conv1 forward).  A 2x2x2 Winograd output tile is exactly one 2x2x2
-// pooling window, so a window's 8 conv outputs come out in ONE lane's
-// registers: the pooling max and its first-maximum index are plain register
-// compares (no DPP), and the 27 taps x 4 input channels of a direct conv
-// output (27 k-steps of 16x16x4 per 16 outputs x 16 channels) become 64
-// element-wise products per window, summed over the 4 input channels:
+// Forward in the Winograd form F(2x2x2, 3x3x3) on f32 MFMA: conv1 and the
+// grouped stages (groups 2 and 4; the launched f32 forward of all three).  A
+// 2x2x2 Winograd output tile is exactly one 2x2x2 pooling window, so a
+// window's 8 conv outputs come out in ONE lane's registers: the pooling max
+// and its first-maximum index are plain register compares (no DPP), and the
+// 27 taps of a direct conv output become 64 element-wise products per window:
 //   M[xi][co][win] = sum_ci U[xi][co][ci] * V[xi][ci][win],  xi in 4x4x4,
-// one v_mfma_f32_16x16x4_f32 per xi and 16 windows (K = the 4 input
-// channels): 64 MFMAs per 16 windows against 216 direct (3.4x fewer).
+// one v_mfma_f32_16x16x4_f32 per xi, 16 windows and 4 input channels of the
+// block's group (K), chained over the group's CPG / 4 channel quads:
+//   conv1 (CPG 4, 16 outputs):  64 MFMAs per 16 windows, 216 direct;
+//   conv2 (groups 2, CPG 8):   128 per group (rows of the other group's 8
+//                              outputs are zero), 2 x 128 against the direct
+//                              z-shift form's 576 for both groups;
+//   conv3 (groups 4, CPG 4):    64 per group (12 zero rows), 4 x 64 vs 432.
 //   U = G w G^T (per axis G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]): the
-//       filter transform, once per block into registers (A operand: lane
-//       (co = l & 15, ci = l >> 4));
+//       filter transform, once per block into LDS (A operand: lane (co = l &
+//       15, ci = l >> 4); rows co >= COG hold zeros);
 //   V = B^T d B (per axis B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]): the
 //       4x4x4 input patch of the window, per lane (B operand: lane (window n
 //       = l & 15, ci = l >> 4)) from the plane ring, adds only;
 //   Y = A^T M A (per axis A^T = [1 1 1 0; 0 1 -1 -1]): applied axis by axis
 //       as the MFMAs of one (xi_x, xi_y) column complete (z, then y, then x).
-// Every operation is f32 (MFMA: exact FMA chains); the result differs from
-// the direct sum by rounding only (the transforms' adds and the halves of G
-// -- tests/test_gpu_c3d.py gates it against float64 torch like the direct
-// kernel).  The block streams z-planes through the same 6-slot LDS ring as
-// k_conv_ring (RingGeom / RingLoader: pooled row k needs planes 2k..2k+3,
-// the next two load by LDS DMA while the row computes); an item is one pooled
-// row py of the block's y band and 16 consecutive pooled x (x group xg).
-// U lives in LDS after the ring (16 KiB); registers hold half of V (32) and
-// the axis partial sums: 133 VGPRs, no spills.
+// Every operation is f32 (MFMA: exact FMA chains); the result differs from the
+// direct sum by rounding only (measured error vs float64 below the direct f32
+// kernel's, tools/wino_err.py; tests/test_gpu_c3d.py gates it against float64
+// torch like the direct kernels).  The block streams z-planes of its group's
+// CPG channels through the 6-slot LDS ring of k_conv_ring (pooled row k needs
+// planes 2k..2k+3, the next two load by LDS DMA while the row computes); an
+// item is 16 consecutive windows of the block's y band (row-major over
+// (py, px)), one per lane group column n.
 // ---------------------------------------------------------------------------
-constexpr int kWinoU = 16 * 64 * 4;  // floats of the transformed filter in LDS
+template <int CPG>
+constexpr int wino_u_floats() {  // U in LDS: 16 columns x 64 lanes x 4 xi_z x CPG / 4 quads
+    return 16 * 64 * 4 * (CPG / 4);
+}
 
-template <int PYB, int VEC, bool TRAIN>
-__global__ __launch_bounds__(512) void k_conv1_wino(RingParams P) {
+struct WinoParams {
+    const float* x;
+    const int64_t* rows;  // sample b reads x row rows[b] (null: b)
+    const float* w;       // [16][CPG][27]
+    const float* bias;
+    float* y;
+    uint8_t* amax;        // null: inference
+    RingGeom rg;          // the group's CPG channels per slot
+    int32_t G;            // groups (blockIdx.z = sample * G + group)
+    int32_t pyb;          // pooled rows per y band
+};
+
+template <int CPG, int COG, int VEC, int NTH, bool TRAIN>
+__global__ __launch_bounds__(NTH) void k_conv_wino(WinoParams P) {
     extern __shared__ float xs[];
-    constexpr int NW = 8;
+    constexpr int NW = NTH / 64;
+    constexpr int NS = CPG / 4;  // channel quads (MFMA k-steps) per xi
     const Geom& g = P.rg.g;
     const int SLOT = P.rg.SLOT;
-    const int b = blockIdx.z, py0 = blockIdx.x * PYB;
+    const int b = blockIdx.z / P.G, grp = blockIdx.z - b * P.G;
+    const int PYB = P.pyb, py0 = blockIdx.x * PYB;
     const int k0 = blockIdx.y * P.rg.ZC, k1 = min(g.PD, k0 + P.rg.ZC);
     if (k0 >= k1) return;
     const int lane = threadIdx.x & 63, n = lane & 15, gq = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t srow = P.rows ? P.rows[b] : b;
-    const float* xb = P.x + srow * (int64_t)4 * g.D * g.H * g.W;
+    const int cin = CPG * P.G;
+    const float* xb = P.x + (srow * cin + (int64_t)grp * CPG) * g.D * g.H * g.W;
     const int y0 = 2 * py0 - g.ph;
 
-    RingLoader<4, VEC, NW> ld;
+    RingLoader<CPG, VEC, NW, 16> ld;
     ld.init(P.rg, y0, -g.pw, wave, lane);
     auto load_plane = [&](int t, int slot) { ld.load(xb, P.rg, xs, t, slot, wave, lane); };
     // ---- prologue DMA first: the filter transform below runs under it
 #pragma unroll
     for (int i = 0; i < 4; ++i) load_plane(2 * k0 + i, i);
 
-    // ---- U = G w G^T for (co = n, ci = gq), by wave 0 into LDS after the
-    // ring: us[(j * 64 + lane) * 4 + xz], j = xy * 4 + xx (one ds_read_b128 per
-    // (xi_x, xi_y) column gives its 4 xi_z values; registers hold only the
-    // patch transform and the output partial sums)
+    // ---- U = G w G^T for (co = n, ci = 4s + gq), by wave 0 into LDS after the
+    // ring: us[(j * 64 + lane) * 4 NS + xz * NS + s], j = xy * 4 + xx (one or
+    // two ds_read_b128 per (xi_x, xi_y) column give its 4 xi_z x NS values)
     float* us = xs + kRing * SLOT;
     if (wave == 0) {
-        const float* w = P.w + (n * 4 + gq) * 27;
-        float t[36];  // after the x axis: [kz][ky][xx]
 #pragma unroll
-        for (int r = 0; r < 9; ++r) {
-            const float w0 = w[3 * r], w1 = w[3 * r + 1], w2 = w[3 * r + 2];
-            t[4 * r] = w0;
-            t[4 * r + 1] = 0.5f * ((w0 + w1) + w2);
-            t[4 * r + 2] = 0.5f * ((w0 - w1) + w2);
-            t[4 * r + 3] = w2;
-        }
-        float s[48];  // after the y axis: [kz][xy][xx]
+        for (int s = 0; s < NS; ++s) {
+            const bool live = n < COG;
+            const float* w = P.w + ((grp * COG + (live ? n : 0)) * CPG + 4 * s + gq) * 27;
+            float t[36];  // after the x axis: [kz][ky][xx]
 #pragma unroll
-        for (int kz = 0; kz < 3; ++kz)
-#pragma unroll
-            for (int xx = 0; xx < 4; ++xx) {
-                const float a0 = t[(kz * 3) * 4 + xx], a1 = t[(kz * 3 + 1) * 4 + xx], a2 = t[(kz * 3 + 2) * 4 + xx];
-                s[(kz * 4) * 4 + xx] = a0;
-                s[(kz * 4 + 1) * 4 + xx] = 0.5f * ((a0 + a1) + a2);
-                s[(kz * 4 + 2) * 4 + xx] = 0.5f * ((a0 - a1) + a2);
-                s[(kz * 4 + 3) * 4 + xx] = a2;
+            for (int r = 0; r < 9; ++r) {
+                const float w0 = live ? w[3 * r] : 0.0f, w1 = live ? w[3 * r + 1] : 0.0f;
+                const float w2 = live ? w[3 * r + 2] : 0.0f;
+                t[4 * r] = w0;
+                t[4 * r + 1] = 0.5f * ((w0 + w1) + w2);
+                t[4 * r + 2] = 0.5f * ((w0 - w1) + w2);
+                t[4 * r + 3] = w2;
             }
+            float sy[48];  // after the y axis: [kz][xy][xx]
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {  // j = xy * 4 + xx; along z
-            const float a0 = s[j], a1 = s[16 + j], a2 = s[32 + j];
-            const float4 q = make_float4(a0, 0.5f * ((a0 + a1) + a2), 0.5f * ((a0 - a1) + a2), a2);
-            *reinterpret_cast<float4*>(us + (j * 64 + lane) * 4) = q;
+            for (int kz = 0; kz < 3; ++kz)
+#pragma unroll
+                for (int xx = 0; xx < 4; ++xx) {
+                    const float a0 = t[(kz * 3) * 4 + xx], a1 = t[(kz * 3 + 1) * 4 + xx];
+                    const float a2 = t[(kz * 3 + 2) * 4 + xx];
+                    sy[(kz * 4) * 4 + xx] = a0;
+                    sy[(kz * 4 + 1) * 4 + xx] = 0.5f * ((a0 + a1) + a2);
+                    sy[(kz * 4 + 2) * 4 + xx] = 0.5f * ((a0 - a1) + a2);
+                    sy[(kz * 4 + 3) * 4 + xx] = a2;
+                }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {  // j = xy * 4 + xx; along z
+                const float a0 = sy[j], a1 = sy[16 + j], a2 = sy[32 + j];
+                float* q = us + (j * 64 + lane) * 4 * NS + s;
+                q[0] = a0;
+                q[NS] = 0.5f * ((a0 + a1) + a2);
+                q[2 * NS] = 0.5f * ((a0 - a1) + a2);
+                q[3 * NS] = a2;
+            }
         }
     }
     float bias[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bias[r] = P.bias[4 * gq + r];
+    for (int r = 0; r < 4; ++r) bias[r] = 4 * gq + r < COG ? P.bias[grp * COG + 4 * gq + r] : 0.0f;
     const int chan = g.PD * g.PH * g.PW;
-    float* ybase = P.y + ((int64_t)b * CO + 4 * gq) * chan;
-    uint8_t* abase = TRAIN ? P.amax + ((int64_t)b * CO + 4 * gq) * chan : nullptr;
-    const int nxg = (g.PW + 15) >> 4;
-    const int items = PYB * nxg;
-    const int pxmax = 2 * g.XT - 1;  // last window whose 4x4 patch lies inside the slot's XL columns
+    const bool lane_co = 4 * gq < COG;  // this lane group's 4 rows are outputs of the group
+    float* ybase = P.y + ((int64_t)b * CO + grp * COG + (lane_co ? 4 * gq : 0)) * chan;
+    uint8_t* abase = TRAIN ? P.amax + ((int64_t)b * CO + grp * COG + (lane_co ? 4 * gq : 0)) * chan : nullptr;
+    const int nwin = min(PYB, g.PH - py0) * g.PW;  // windows of the band
+    const int items = (nwin + 15) >> 4;
 
     __builtin_amdgcn_s_waitcnt(0x0F70);
     __syncthreads();
@@ -964,66 +993,68 @@ __global__ __launch_bounds__(512) void k_conv1_wino(RingParams P) {
             load_plane(2 * k + 5, sb + 5 >= kRing ? sb + 5 - kRing : sb + 5);
         }
         for (int it = wave; it < items; it += NW) {
-            const int r = it / nxg, xg = it - r * nxg;
+            const int wi = min(16 * it + n, nwin - 1);  // lanes past the band repeat its last window (not stored)
+            const int r = wi / g.PW, px = wi - r * g.PW;
             const int py = py0 + r;
-            if (py >= g.PH) break;  // wave-uniform
-            const int px = 16 * xg + n;
-            // ---- in two halves of the x axis (xi_x = 2h, 2h + 1): V = B^T d B of
-            // the lane's 4x4x4 patch (channel gq), then M = U V over the 4 input
-            // channels (MFMA) and Y = A^T M A.  (Both halves at once kept all 64
-            // products in flight and spilled.)
-            const int xoff = gq * g.CS + 2 * r * g.YS + 2 * min(px, pxmax);
+            // ---- in two halves of the x axis (xi_x = 2h, 2h + 1): V = B^T d B
+            // of the lane's 4x4x4 patches (channels 4s + gq), then M = U V
+            // (MFMA, chained over the NS channel quads) and Y = A^T M A.  (Both
+            // halves at once kept all 64 products in flight and spilled.)
+            const int xoff = gq * g.CS + 2 * r * g.YS + 2 * px;
             const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
-            f4 Y[2][2][2];  // [ox][oy][oz]
+            f4 Y[2][2][2];   // [ox][oy][oz]
             f4 Sx[2][2][2];  // [xi_x & 1][oy][oz]: the y-axis sums of a column pair
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                float v[32];  // [dz][dy][k] -> [xz][xy][k], xi_x = 2h + k
+                float v[NS][32];  // [s][dz][dy][kx] -> [s][xz][xy][kx], xi_x = 2h + kx
                 int xo = xoff;
                 asm volatile("" : "+v"(xo));  // the halves' patch reads stay separate (no CSE)
 #pragma unroll
-                for (int dz = 0; dz < 4; ++dz) {
-                    int sl = sb + dz;
-                    sl = sl >= kRing ? sl - kRing : sl;
-                    const float* p = xs + sl * SLOT + xo;
+                for (int s = 0; s < NS; ++s) {
 #pragma unroll
-                    for (int dy = 0; dy < 4; ++dy) {
-                        const float2 a = *reinterpret_cast<const float2*>(p + dy * g.YS);
-                        const float2 c = *reinterpret_cast<const float2*>(p + dy * g.YS + 2);
-                        float* q = v + (dz * 4 + dy) * 2;
-                        if (h == 0) {  // B^T along x, rows 0, 1
-                            q[0] = a.x - c.x;
-                            q[1] = a.y + c.x;
-                        } else {       // rows 2, 3
-                            q[0] = c.x - a.y;
-                            q[1] = a.y - c.y;
+                    for (int dz = 0; dz < 4; ++dz) {
+                        int sl = sb + dz;
+                        sl = sl >= kRing ? sl - kRing : sl;
+                        const float* p = xs + sl * SLOT + 4 * s * g.CS + xo;
+#pragma unroll
+                        for (int dy = 0; dy < 4; ++dy) {
+                            const float2 a = *reinterpret_cast<const float2*>(p + dy * g.YS);
+                            const float2 c = *reinterpret_cast<const float2*>(p + dy * g.YS + 2);
+                            float* q = v[s] + (dz * 4 + dy) * 2;
+                            if (h == 0) {  // B^T along x, rows 0, 1
+                                q[0] = a.x - c.x;
+                                q[1] = a.y + c.x;
+                            } else {       // rows 2, 3
+                                q[0] = c.x - a.y;
+                                q[1] = a.y - c.y;
+                            }
                         }
                     }
-                }
 #pragma unroll
-                for (int dz = 0; dz < 4; ++dz)  // along y
+                    for (int dz = 0; dz < 4; ++dz)  // along y
 #pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        float* q = v + dz * 8 + k;
-                        const float d0 = q[0], d1 = q[2], d2 = q[4], d3 = q[6];
-                        q[0] = d0 - d2;
-                        q[2] = d1 + d2;
-                        q[4] = d2 - d1;
-                        q[6] = d1 - d3;
+                        for (int kx = 0; kx < 2; ++kx) {
+                            float* q = v[s] + dz * 8 + kx;
+                            const float d0 = q[0], d1 = q[2], d2 = q[4], d3 = q[6];
+                            q[0] = d0 - d2;
+                            q[2] = d1 + d2;
+                            q[4] = d2 - d1;
+                            q[6] = d1 - d3;
+                        }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {  // along z
+                        const float d0 = v[s][j], d1 = v[s][8 + j], d2 = v[s][16 + j], d3 = v[s][24 + j];
+                        v[s][j] = d0 - d2;
+                        v[s][8 + j] = d1 + d2;
+                        v[s][16 + j] = d2 - d1;
+                        v[s][24 + j] = d1 - d3;
                     }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {  // along z
-                    const float d0 = v[j], d1 = v[8 + j], d2 = v[16 + j], d3 = v[24 + j];
-                    v[j] = d0 - d2;
-                    v[8 + j] = d1 + d2;
-                    v[16 + j] = d2 - d1;
-                    v[24 + j] = d1 - d3;
                 }
                 // software-pipelined columns (xi_x, xi_y): the MFMAs of column c
                 // are issued before the sums of column c - 1, whose results pass
                 // through an empty asm so they are formed here (left free, the
-                // compiler sinks every column's sums below all 64 MFMAs and
-                // their 256 accumulator registers spill)
+                // compiler sinks every column's sums below all the MFMAs and
+                // their accumulator registers spill)
                 f4 pm[4];
                 auto column_sums = [&](const f4 (&m)[4], int xx, int xy) {
                     const f4 t0 = (m[0] + m[1]) + m[2], t1 = (m[1] - m[2]) - m[3];  // A^T along z
@@ -1069,16 +1100,27 @@ __global__ __launch_bounds__(512) void k_conv1_wino(RingParams P) {
                     }
                 };
 #pragma unroll
-                for (int c = 0; c <= 8; ++c) {  // column c = k * 4 + xy of this half
+                for (int c = 0; c <= 8; ++c) {  // column c = kx * 4 + xy of this half
                     f4 m[4];
                     if (c < 8) {
-                        const int k = c >> 2, xy = c & 3, xx = 2 * h + k;
-                        const int j = xy * 4 + xx, jv = xy * 2 + k;
-                        const float4 uc = *reinterpret_cast<const float4*>(us + (j * 64 + lane) * 4);
-                        m[0] = mfma4(uc.x, v[jv], zero);
-                        m[1] = mfma4(uc.y, v[8 + jv], zero);
-                        m[2] = mfma4(uc.z, v[16 + jv], zero);
-                        m[3] = mfma4(uc.w, v[24 + jv], zero);
+                        const int kx = c >> 2, xy = c & 3, xx = 2 * h + kx;
+                        const int j = xy * 4 + xx, jv = xy * 2 + kx;
+                        const float* ub = us + (j * 64 + lane) * 4 * NS;
+                        float uc[4 * NS];
+#pragma unroll
+                        for (int q = 0; q < NS; ++q) {
+                            const float4 u4 = *reinterpret_cast<const float4*>(ub + 4 * q);
+                            uc[4 * q] = u4.x;
+                            uc[4 * q + 1] = u4.y;
+                            uc[4 * q + 2] = u4.z;
+                            uc[4 * q + 3] = u4.w;
+                        }
+#pragma unroll
+                        for (int xz = 0; xz < 4; ++xz) {
+                            m[xz] = mfma4(uc[xz * NS], v[0][xz * 8 + jv], zero);
+#pragma unroll
+                            for (int s = 1; s < NS; ++s) m[xz] = mfma4(uc[xz * NS + s], v[s][xz * 8 + jv], m[xz]);
+                        }
                     }
                     if (c > 0) column_sums(pm, 2 * h + ((c - 1) >> 2), (c - 1) & 3);
                     if (c < 8)
@@ -1095,7 +1137,7 @@ __global__ __launch_bounds__(512) void k_conv1_wino(RingParams P) {
                 vo[o] = (unsigned)(cz0 + oz) < (unsigned)g.cd & (unsigned)(cy0 + oy) < (unsigned)g.ch &
                         (unsigned)(cx0 + ox) < (unsigned)g.cw;
             }
-            const bool st = px < g.PW;
+            const bool st = lane_co & (16 * it + n < nwin);
             const int oidx = (k * g.PH + py) * g.PW + px;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
@@ -1107,7 +1149,7 @@ __global__ __launch_bounds__(512) void k_conv1_wino(RingParams P) {
                     if (TRAIN) km = val > m ? o : km;  // strict: the first maximum keeps its index
                     m = fmaxf(m, val);
                 }
-                if (st) {
+                if (st && 4 * gq + rr < COG) {
                     ybase[rr * chan + oidx] = m;
                     if (TRAIN) abase[rr * chan + oidx] = (uint8_t)(km | (m > 0.0f ? 8 : 0));
                 }
@@ -1119,50 +1161,105 @@ __global__ __launch_bounds__(512) void k_conv1_wino(RingParams P) {
     }
 }
 
-template <int PYB, int VEC>
-int launch_wino(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
-                const float* bias, float* y, uint8_t* amax, hipStream_t st) {
-    RingParams P{x, rows, w, bias, y, amax, rg};
-    const size_t lds = ((size_t)kRing * rg.SLOT + kWinoU) * sizeof(float);
+// Ring geometry of the Winograd forward: a y band of pyb pooled rows, XL =
+// 2 PW + 2 input columns (the last window's 4-wide patch), rows and channels
+// padded to the DMA width; z chunks until the grid has ~2048 blocks
+template <int CPG, int VEC>
+RingGeom make_wino_geom(const rt_conv_layer* L, int B, int G, int pyb) {
+    RingGeom r{};
+    Geom& g = r.g;
+    g.D = L->in_dims[0];
+    g.H = L->in_dims[1];
+    g.W = L->in_dims[2];
+    g.cd = g.D - 2;
+    g.ch = g.H - 2;
+    g.cw = g.W - 2;
+    g.pd = L->pool_pad[0];
+    g.ph = L->pool_pad[1];
+    g.pw = L->pool_pad[2];
+    g.PD = (g.cd + 2 * g.pd - 2) / 2 + 1;
+    g.PH = (g.ch + 2 * g.ph - 2) / 2 + 1;
+    g.PW = (g.cw + 2 * g.pw - 2) / 2 + 1;
+    g.XT = (g.PW + 1) / 2;
+    g.ZL = 4;
+    g.YL = 2 * pyb + 2;
+    g.XL = 2 * g.PW + 2;
+    g.YS = (g.XL + 3) / 4 * 4;
+    g.ZS = 0;
+    g.CS = g.YL * g.YS;
+    r.SLOT = CPG * g.CS;
+    r.npiece = (r.SLOT + 64 * VEC - 1) / (64 * VEC);
+    r.nyb = (g.PH + pyb - 1) / pyb;
+    const int64_t per_chunk = (int64_t)r.nyb * B * G;
+    const int nzc = (int)std::min<int64_t>(g.PD, std::max<int64_t>(1, (2048 + per_chunk - 1) / per_chunk));
+    r.ZC = (g.PD + nzc - 1) / nzc;
+    return r;
+}
+
+template <int CPG, int COG, int VEC, int NTH>
+int launch_wino_k(const RingGeom& rg, int pyb, int G, int32_t B, const float* x, const int64_t* rows,
+                  const float* w, const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+    WinoParams P{x, rows, w, bias, y, amax, rg, G, pyb};
+    const size_t lds = ((size_t)kRing * rg.SLOT + wino_u_floats<CPG>()) * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (const int rc_lds = allow_big_lds(&k_conv1_wino<PYB, VEC, true>)) return rc_lds;
-        if (const int rc_lds = allow_big_lds(&k_conv1_wino<PYB, VEC, false>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_wino<CPG, COG, VEC, NTH, true>)) return rc_lds;
+        if (const int rc_lds = allow_big_lds(&k_conv_wino<CPG, COG, VEC, NTH, false>)) return rc_lds;
         attr = true;
     }
-    dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, B);
+    dim3 grid(rg.nyb, (rg.g.PD + rg.ZC - 1) / rg.ZC, B * G);
     if (amax)
-        hipLaunchKernelGGL((k_conv1_wino<PYB, VEC, true>), grid, dim3(512), lds, st, P);
+        hipLaunchKernelGGL((k_conv_wino<CPG, COG, VEC, NTH, true>), grid, dim3(NTH), lds, st, P);
     else
-        hipLaunchKernelGGL((k_conv1_wino<PYB, VEC, false>), grid, dim3(512), lds, st, P);
+        hipLaunchKernelGGL((k_conv_wino<CPG, COG, VEC, NTH, false>), grid, dim3(NTH), lds, st, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
 }
 
-// conv1's f32 forward: the Winograd kernel with the widest y band (4, 2, 1
-// pooled rows) whose 6-slot ring fits 160 KiB (one 8-wave block per CU by
-// registers); RT_ELIMIT when none does (the caller takes the direct ring)
+// The f32 forward of conv1 and of the grouped stages in the Winograd form: the
+// widest y band (up to 2 item rounds per pooled row) whose ring + U fit the
+// 160 KiB of one block per CU; RT_ELIMIT when none does or the stage is not
+// one of those (groups 1 with 16 channels: the direct ring kernel)
 int launch_fwd_wino(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
                     const float* bias, float* y, uint8_t* amax, hipStream_t st) {
-    const bool vec4 = L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    auto fits = [&](const RingGeom& rg, int vec) {
-        return ((size_t)kRing * rg.SLOT + kWinoU) * sizeof(float) <= 160 * 1024 &&
-               (rg.npiece + 7) / 8 <= (vec == 4 ? ring_max_pieces<4, 4>() : ring_max_pieces<4, 1>()) &&
-               rg.g.W >= vec;
+    const int G = L->groups, cpg = L->cin / G;
+    if (!(L->cin == 4 || G == 2 || G == 4) || (int64_t)B * G > 65535) return RT_ELIMIT;
+    const bool vec4 = cpg == 4 && G == 1 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
+                      (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    const int nth = G == 4 ? 256 : 512;
+    auto plan = [&](auto cpg_c, auto vec_c, int& pyb_out) -> RingGeom {
+        constexpr int CPG_ = decltype(cpg_c)::value, VEC_ = decltype(vec_c)::value;
+        RingGeom best{};
+        pyb_out = 0;
+        const int ph = (L->in_dims[1] - 2 + 2 * L->pool_pad[1] - 2) / 2 + 1;
+        for (int pyb = 1; pyb <= ph; ++pyb) {
+            const RingGeom rg = make_wino_geom<CPG_, VEC_>(L, B, G, pyb);
+            const size_t lds = ((size_t)kRing * rg.SLOT + wino_u_floats<CPG_>()) * sizeof(float);
+            const int items = (pyb * rg.g.PW + 15) / 16;
+            if (lds > 160 * 1024 || (rg.npiece + nth / 64 - 1) / (nth / 64) > 16 || items > 2 * (nth / 64) ||
+                rg.g.W < VEC_)
+                break;
+            best = rg;
+            pyb_out = pyb;
+        }
+        return best;
     };
-    if (vec4) {
-        RingGeom rg = make_ring_geom<4, 4, 4>(L, B, 512);
-        if (fits(rg, 4)) return launch_wino<4, 4>(rg, B, x, rows, w, bias, y, amax, st);
-        rg = make_ring_geom<4, 2, 4>(L, B, 512);
-        if (fits(rg, 4)) return launch_wino<2, 4>(rg, B, x, rows, w, bias, y, amax, st);
+    int pyb = 0;
+    if (cpg == 4 && G == 1) {
+        if (vec4) {
+            const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{}, pyb);
+            if (pyb) return launch_wino_k<4, 16, 4, 512>(rg, pyb, 1, B, x, rows, w, bias, y, amax, st);
+        }
+        const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, pyb);
+        if (pyb) return launch_wino_k<4, 16, 1, 512>(rg, pyb, 1, B, x, rows, w, bias, y, amax, st);
+    } else if (G == 2) {
+        const RingGeom rg = plan(std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{}, pyb);
+        if (pyb) return launch_wino_k<8, 8, 1, 512>(rg, pyb, 2, B, x, rows, w, bias, y, amax, st);
+    } else {
+        const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, pyb);
+        if (pyb) return launch_wino_k<4, 4, 1, 256>(rg, pyb, 4, B, x, rows, w, bias, y, amax, st);
     }
-    RingGeom rg = make_ring_geom<4, 4, 1>(L, B, 512);
-    if (fits(rg, 1)) return launch_wino<4, 1>(rg, B, x, rows, w, bias, y, amax, st);
-    rg = make_ring_geom<4, 2, 1>(L, B, 512);
-    if (fits(rg, 1)) return launch_wino<2, 1>(rg, B, x, rows, w, bias, y, amax, st);
-    rg = make_ring_geom<4, 1, 1>(L, B, 512);
-    if (fits(rg, 1)) return launch_wino<1, 1>(rg, B, x, rows, w, bias, y, amax, st);
     return RT_ELIMIT;
 }
 
@@ -2732,11 +2829,12 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_fwd: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     int rc = RT_ELIMIT;
+    // f32: the Winograd kernel (conv1 and the grouped stages); bf16x3, groups 1
+    // with 16 channels and planes too wide for its ring: the direct kernels
+    if (g_conv_prec == 0) rc = launch_fwd_wino(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    if (rc != RT_ELIMIT) return rc;
     if (L->cin == 4) {
-        // f32: the Winograd kernel; bf16x3 (and planes too wide for its ring):
-        // the direct ring kernel
-        if (g_conv_prec == 0) rc = launch_fwd_wino(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
-        if (rc == RT_ELIMIT) rc = launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+        rc = launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     } else if (L->groups == 1) {
         rc = launch_fwd_ring<16, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     } else {

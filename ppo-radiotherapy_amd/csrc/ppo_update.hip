@@ -1034,6 +1034,110 @@ __global__ __launch_bounds__(256) void k_adam(AdamParams P) {
     P.v[i] = v;
 }
 
+// ---- k_ppo_reduce + clip + Adam in one launch (rt_ppo_update) ---------------
+// Every block reduces its 64 columns exactly as k_ppo_reduce does and stores
+// them to the gradient; its ||g||^2 partial goes to norm_part[block] by an
+// `sc1` store.  After the store has completed (s_waitcnt vmcnt(0)) ONE lane
+// adds 1 to an arrival counter (agent scope) and polls it (`sc1` loads) until
+// every block of the launch has arrived, then its wave reads the partials
+// with `sc1` loads (MI355X_MICROARCH.md hand-off table, first row: no fence)
+// and sums them in k_adam's order, so the clip coefficient is bitwise
+// k_adam's; the wave then runs clip + Adam on the block's OWN columns only --
+// no last-block serialisation (round 3's k_ppo_reduce_adam ran all 10,061
+// updates in the last block and lost to the two kernels).  The
+// kReduceBlocks blocks (16 waves, 4 KiB LDS each: >= 2 fit a CU) are all
+// resident at once on an otherwise idle stream, so the wait completes; a
+// bounded poll that runs out (hardware fault) poisons the step with NaN.
+// The counter (the workspace's last norm slot) is zeroed by rt_ppo_update
+// before its first launch; launch i waits for (i + 1) * kReduceBlocks.
+struct ReduceAdamParams {
+    ReduceParams R;
+    AdamParams A;
+    int32_t flat_off[13];  // flat index of each tensor's first element (params_d[t] - flat_param_d)
+    unsigned* counter;
+    unsigned target;
+};
+
+__global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
+    __shared__ float part[16][kReduceCols];
+    const ReduceParams& P = Q.R;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int p = blockIdx.x * kReduceCols + lane;
+    const bool ok = p < NP + NSTAT;
+    float x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int b = w + 16 * k;
+        x[k] = (ok && b < P.nblk) ? P.ws[(size_t)b * PSTRIDE + p] : 0.0f;
+    }
+#pragma unroll
+    for (int h = 8; h > 0; h >>= 1)
+#pragma unroll
+        for (int k = 0; k < h; ++k) x[k] += x[k + h];
+    part[w][lane] = x[0];
+    __syncthreads();
+    if (w != 0) return;
+    float a = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a += part[k][lane];
+    float sq = 0.0f;
+    int t = 0;
+    if (ok) {
+        if (p < NP) {
+#pragma unroll
+            for (int k = 1; k < 13; ++k) t += p >= kTensorOff[k] ? 1 : 0;
+            if (t == 6) a += -P.ent_coef;  // d(-ent_coef * mean(entropy)) / d logstd
+            sq = a * a;
+        } else {
+            const int k = p - NP;
+            float v = a * P.inv_n;
+            if (k == 1) v *= 0.5f;  // v_loss = 0.5 * mean(max(...))
+            P.stats[k] = v;
+            if (P.stats_accum) P.stats_accum[k] += v;
+        }
+    }
+    sq = wave_sum(sq);
+    const AdamParams& A = Q.A;
+    if (lane == 0) {
+        __hip_atomic_store(const_cast<float*>(A.norm_part) + blockIdx.x, sq, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(Q.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the arrival wait: lane 0 polls, the wave follows it in program order
+    int arrived = 1;
+    if (lane == 0) {
+        int spins = 0;
+        while (__hip_atomic_load(Q.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < Q.target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1 << 24)) {
+                arrived = 0;
+                break;
+            }
+        }
+    }
+    arrived = __shfl(arrived, 0, 64);
+    float tn = 0.0f;
+    if (A.max_norm > 0.0f)
+        for (int k = lane; k < A.n_part; k += 64)
+            tn += __hip_atomic_load(const_cast<float*>(A.norm_part) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tn = wave_sum(tn);
+    float coef = A.max_norm > 0.0f ? fminf(A.max_norm / (sqrtf(tn) + 1e-6f), 1.0f) : 1.0f;
+    if (!arrived) coef = __int_as_float(0x7fc00000);  // NaN: a lost arrival is never a silent step
+    if (!ok || p >= NP) return;
+    const int64_t i = Q.flat_off[t] + (p - kTensorOff[t]);
+    const float g = a * coef;
+    A.grad[i] = g;
+    float m = A.m[i];
+    m = m + A.lerp_w * (g - m);                   // exp_avg.lerp_(grad, 1 - beta1)
+    float v = A.v[i] * A.beta2;                   // exp_avg_sq.mul_(beta2)
+    v = v + A.one_minus_beta2 * g * g;            //   .addcmul_(grad, grad, 1 - beta2)
+    const float denom = sqrtf(v) / A.bc2_sqrt + A.eps;
+    A.param[i] = A.param[i] + A.step_size * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
+    A.m[i] = m;
+    A.v[i] = v;
+}
+
 // ---- per-epoch shuffle and minibatch advantage statistics ------------------
 // A keyed pseudo-random permutation of [0, n): a 4-round Feistel network on
 // 2h bits (2^(2h) >= n) with cycle-walking, one index per thread -- replaces
@@ -1195,7 +1299,8 @@ ReduceParams reduce_params(float* const* grads_d, int32_t mb, const rt_ppo_hpara
 
 int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* b,
                     const int64_t* idx_d, int32_t mb, const float* adv_stats_d, const rt_ppo_hparams* hp,
-                    float* ws_d, int64_t ws_floats, float* stats_d, float* accum_d, hipStream_t st) {
+                    float* ws_d, int64_t ws_floats, float* stats_d, float* accum_d, hipStream_t st,
+                    bool with_reduce = true) {
     const int nblk = grad_blocks(mb);
     if ((int64_t)nblk * PSTRIDE + kNormSlots > ws_floats)
         return rt_internal_fail(RT_EINVAL, "rt_ppo_grad: workspace too small");
@@ -1222,7 +1327,7 @@ int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const r
     else
         hipLaunchKernelGGL(k_ppo_grad_mfma<kPrecF32>, dim3(nblk), dim3(MT), 0, st, G);
     R = reduce_params(grads_d, mb, hp, ws_d, ws_floats, stats_d, accum_d);
-    hipLaunchKernelGGL(k_ppo_reduce, dim3(kReduceBlocks), dim3(1024), 0, st, R);
+    if (with_reduce) hipLaunchKernelGGL(k_ppo_reduce, dim3(kReduceBlocks), dim3(1024), 0, st, R);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     return RT_OK;
@@ -1333,14 +1438,31 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
         return rt_internal_fail(RT_EINVAL, "rt_ppo_update: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     float* norm_part = workspace_d + (workspace_floats - kNormSlots);
+    // the arrival counter of k_ppo_reduce_adam: the last norm slot (unused by the partials)
+    unsigned* counter = reinterpret_cast<unsigned*>(norm_part + (kNormSlots - 1));
+    if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess)
+        return rt_internal_fail(RT_EDEVICE, "rt_ppo_update: hipMemsetAsync failed");
+    ReduceAdamParams Q{};
+    for (int t = 0; t < 13; ++t) {
+        const int64_t off = params_d[t] - flat_param_d;
+        if (off < 0 || off + (kTensorOff[t + 1] - kTensorOff[t]) > n_flat ||
+            grads_d[t] - flat_grad_d != off)
+            return rt_internal_fail(RT_EINVAL, "rt_ppo_update: params_d / grads_d must be views of the flat buffers");
+        Q.flat_off[t] = (int32_t)off;
+    }
+    Q.counter = counter;
     for (int i = 0; i < n_minibatches; ++i) {
         int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
                                  adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,
-                                 stats_d, stats_accum_d, st);
+                                 stats_d, stats_accum_d, st, false);
         if (rc) return rc;
-        rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part,
-                         true, 1.0f, st);
-        if (rc) return rc;
+        Q.R = reduce_params(grads_d, mb_size, hp, workspace_d, workspace_floats, stats_d, stats_accum_d);
+        Q.A = adam_params(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part,
+                          1.0f);
+        Q.target = (unsigned)((i + 1) * kReduceBlocks);
+        hipLaunchKernelGGL(k_ppo_reduce_adam, dim3(kReduceBlocks), dim3(1024), 0, st, Q);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     }
     return RT_OK;
 }

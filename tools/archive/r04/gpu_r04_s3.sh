@@ -2,7 +2,8 @@
 # r04 session 3: the Winograd conv1 forward (k_conv1_wino) and the cleanup
 # build through the C3D stage tests, the extractor test (argmax-routed f64
 # reference) and the rollout / trainer / DP / RCCL tests, the C3D stage
-# timings, then the first-window probe plain and under a rocprofv3 kernel trace
+# timings, the first-window probe plain and under a rocprofv3 kernel trace,
+# and a short bench (value on staggered phases, fused reduce+Adam update)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
@@ -21,4 +22,6 @@ f=$(find $O/prof -name "*kernel_trace.csv" | head -1); cp "$f" $O/kernel_trace.c
 rm -rf $O/prof
 python3 tools/window_kernels.py $O/kernel_trace.csv > $O/windows.txt
 grep "^window" $O/windows.txt
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-c3d > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('bench', round(d['value']/1e6,3), 'M', round(d['ms_per_step'],4), 'timed', round(r['timed_pass_ms_per_step'],4), 'steady', round(d['steady_state']['ms_per_step'],4), 'upd f32 us', round(d['ppo_update_ms']*1000,1), 'bf16x3 us', round(d['ppo_update_ms_bf16x3']*1000,1), 'march', r.get('march',{}).get('frac'))"
 echo ALLDONE
