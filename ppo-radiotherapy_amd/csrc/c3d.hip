@@ -2772,6 +2772,321 @@ int launch_wgrad_sparse(const rt_conv_layer* L, int32_t B, const float* x, const
     return rc;
 }
 
+// ---------------------------------------------------------------------------
+// Data gradient of the grouped stages (groups 2 and 4) in the Winograd form
+// (the launched f32 data gradient for unpadded pools).  dX is the full
+// correlation of the conv-output gradient dC with the flipped weights: per
+// axis dX[2Q + o] = sum_t W[2 - t] e[o + t] over the 4-wide patch e[i] =
+// dC[2Q - 2 + i], which is exactly the two pooling windows Q - 1 and Q -- so
+// an F(2x2x2, 3x3x3) tile of dX reads the 2x2x2 windows (Q-1 .. Q per axis)
+// and its patch holds at most one non-zero per window: the pooled gradient at
+// the window's argmax when its ReLU was active (argmax byte), zeros elsewhere
+// (the max-pool + ReLU backward, built in registers with one compare + select
+// per patch entry).  Then, as the forward: V = B^T e B per lane (B operand:
+// lane (tile n, co = 4s + l >> 4)), U' = G W' G^T of the flipped weights in LDS
+// (A operand: lane (ci = l & 15, co)), M = U' V on f32 MFMA chained over the
+// group's output-channel quads, dX tile = A^T M A.  The block holds the pooled
+// gradient and the argmax bytes of its group and z chunk (window z rows Qz0 - 1
+// .. Qz1 - 1, every y and x) in LDS, loaded once; items are 16 consecutive
+// tiles of a tile row (row-major over (Qy, Qx)).  MFMAs per 16 tiles (16 input
+// channels): 2 groups x 2 x 64 (groups 2) / 4 x 64 (groups 4) against the
+// direct z-shift kernel's 576 / 432.
+// ---------------------------------------------------------------------------
+struct WinoDgradParams {
+    const float* w;     // [16][CPG][27]
+    const float* dP;    // [B][16][PD][PH][PW]
+    const uint8_t* am;  // same shape
+    float* dx;          // [B][16][D][H][W]
+    Geom g;             // D, H, W = dX dims; PD, PH, PW = pooled dims
+    int32_t G;          // groups (blockIdx.y = sample * G + group)
+    int32_t ZC;         // tile rows per block (z chunk)
+    int32_t QD, QH, QW; // tiles per axis = ceil(dims / 2)
+};
+
+template <int CPG>
+constexpr int wino_dg_u_floats() {
+    return 16 * 64 * 4 * (CPG / 4);
+}
+
+template <int CPG, int NTH>
+__global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
+    extern __shared__ float xs[];
+    constexpr int NW = NTH / 64;
+    constexpr int COG = CPG;     // groups 2 / 4: 8 / 4 output channels per group, as many inputs
+    constexpr int NS = COG / 4;  // output-channel quads (MFMA k-steps) per xi
+    const Geom& g = P.g;
+    const int b = blockIdx.y / P.G, grp = blockIdx.y - b * P.G;
+    const int q0 = blockIdx.x * P.ZC, q1 = min(P.QD, q0 + P.ZC);
+    if (q0 >= q1) return;
+    const int lane = threadIdx.x & 63, n = lane & 15, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // ---- the block's windows: rows wz0 .. wz1 - 1 of its group's channels
+    const int wz0 = max(q0 - 1, 0), wz1 = min(q1, g.PD);
+    const int nz = wz1 - wz0;
+    const int plane = g.PH * g.PW;
+    const int chw = nz * plane;  // LDS floats per channel
+    float* us = xs;
+    float* dps = xs + wino_dg_u_floats<CPG>();
+    uint8_t* ams = reinterpret_cast<uint8_t*>(dps + COG * chw);
+    {
+        const size_t pchan = (size_t)g.PD * plane;
+        const float* src = P.dP + ((size_t)b * CO + grp * COG) * pchan + (size_t)wz0 * plane;
+        const uint8_t* asrc = P.am + ((size_t)b * CO + grp * COG) * pchan + (size_t)wz0 * plane;
+        for (int i = threadIdx.x; i < COG * chw; i += NTH) {
+            const int c = i / chw, rem = i - c * chw;
+            dps[i] = src[c * pchan + rem];
+            ams[i] = asrc[c * pchan + rem];
+        }
+    }
+    // ---- U' = G W' G^T, W' = the flipped filter, for (ci = n, co = 4s + gq)
+    if (wave == 0) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const bool live = n < CPG;
+            const int co = grp * COG + 4 * s + gq;
+            const float* w = P.w + (co * CPG + (live ? n : 0)) * 27;
+            float t[36];  // after the x axis: [kz][ky][xx] of the flipped taps
+#pragma unroll
+            for (int r = 0; r < 9; ++r) {
+                const int fr = 8 - r;  // (kz, ky) flipped
+                const float w0 = live ? w[3 * fr + 2] : 0.0f, w1 = live ? w[3 * fr + 1] : 0.0f;
+                const float w2 = live ? w[3 * fr] : 0.0f;
+                t[4 * r] = w0;
+                t[4 * r + 1] = 0.5f * ((w0 + w1) + w2);
+                t[4 * r + 2] = 0.5f * ((w0 - w1) + w2);
+                t[4 * r + 3] = w2;
+            }
+            float sy[48];
+#pragma unroll
+            for (int kz = 0; kz < 3; ++kz)
+#pragma unroll
+                for (int xx = 0; xx < 4; ++xx) {
+                    const float a0 = t[(kz * 3) * 4 + xx], a1 = t[(kz * 3 + 1) * 4 + xx];
+                    const float a2 = t[(kz * 3 + 2) * 4 + xx];
+                    sy[(kz * 4) * 4 + xx] = a0;
+                    sy[(kz * 4 + 1) * 4 + xx] = 0.5f * ((a0 + a1) + a2);
+                    sy[(kz * 4 + 2) * 4 + xx] = 0.5f * ((a0 - a1) + a2);
+                    sy[(kz * 4 + 3) * 4 + xx] = a2;
+                }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float a0 = sy[j], a1 = sy[16 + j], a2 = sy[32 + j];
+                float* q = us + (j * 64 + lane) * 4 * NS + s;
+                q[0] = a0;
+                q[NS] = 0.5f * ((a0 + a1) + a2);
+                q[2 * NS] = 0.5f * ((a0 - a1) + a2);
+                q[3 * NS] = a2;
+            }
+        }
+    }
+    __syncthreads();
+    const int ntile = P.QH * P.QW;
+    const int items = (ntile + 15) >> 4;
+    const int64_t xchan = (int64_t)g.D * g.H * g.W;
+    const bool lane_ci = 4 * gq < CPG;
+    float* dxb = P.dx + ((int64_t)b * CO + grp * CPG + (lane_ci ? 4 * gq : 0)) * xchan;
+    for (int qz = q0; qz < q1; ++qz) {
+        for (int it = wave; it < items; it += NW) {
+            const int ti = min(16 * it + n, ntile - 1);
+            const int qy = ti / P.QW, qx = ti - qy * P.QW;
+            const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+            f4 Y[2][2][2];
+            f4 Sx[2][2][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float v[NS][32];
+                int base = 0;
+                asm volatile("" : "+v"(base));  // the halves' window reads stay separate (no CSE)
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const int c = 4 * s + gq;  // output channel of the group
+                    // the 8 windows (Qz-1..Qz, Qy-1..Qy, Qx-1..Qx): value, and argmax byte
+                    // with the active bit (0 outside the pooled volume)
+                    float wv[8];
+                    int wa[8];
+#pragma unroll
+                    for (int wq = 0; wq < 8; ++wq) {
+                        const int wz = qz - 1 + (wq >> 2), wy = qy - 1 + ((wq >> 1) & 1), wx = qx - 1 + (wq & 1);
+                        const bool in = (unsigned)wz < (unsigned)g.PD & (unsigned)wy < (unsigned)g.PH &
+                                        (unsigned)wx < (unsigned)g.PW;
+                        const int li = base + c * chw + ((in ? wz : wz0) - wz0) * plane + (in ? wy : 0) * g.PW +
+                                       (in ? wx : 0);
+                        wv[wq] = dps[li];
+                        wa[wq] = in ? (int)ams[li] : 0;
+                    }
+#pragma unroll
+                    for (int dz = 0; dz < 4; ++dz)
+#pragma unroll
+                        for (int dy = 0; dy < 4; ++dy) {
+                            // patch row (dz, dy): x 0, 1 from window x Qx-1, x 2, 3 from Qx
+                            const int w0 = ((dz >> 1) << 2) | ((dy >> 1) << 1), w1 = w0 | 1;
+                            const int kb = 8 | ((dz & 1) << 2) | ((dy & 1) << 1);
+                            const float e0 = (wa[w0] & 15) == kb ? wv[w0] : 0.0f;
+                            const float e1 = (wa[w0] & 15) == (kb | 1) ? wv[w0] : 0.0f;
+                            const float e2 = (wa[w1] & 15) == kb ? wv[w1] : 0.0f;
+                            const float e3 = (wa[w1] & 15) == (kb | 1) ? wv[w1] : 0.0f;
+                            float* q = v[s] + (dz * 4 + dy) * 2;
+                            if (h == 0) {  // B^T along x, rows 0, 1
+                                q[0] = e0 - e2;
+                                q[1] = e1 + e2;
+                            } else {       // rows 2, 3
+                                q[0] = e2 - e1;
+                                q[1] = e1 - e3;
+                            }
+                        }
+#pragma unroll
+                    for (int dz = 0; dz < 4; ++dz)
+#pragma unroll
+                        for (int kx = 0; kx < 2; ++kx) {
+                            float* q = v[s] + dz * 8 + kx;
+                            const float d0 = q[0], d1 = q[2], d2 = q[4], d3 = q[6];
+                            q[0] = d0 - d2;
+                            q[2] = d1 + d2;
+                            q[4] = d2 - d1;
+                            q[6] = d1 - d3;
+                        }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float d0 = v[s][j], d1 = v[s][8 + j], d2 = v[s][16 + j], d3 = v[s][24 + j];
+                        v[s][j] = d0 - d2;
+                        v[s][8 + j] = d1 + d2;
+                        v[s][16 + j] = d2 - d1;
+                        v[s][24 + j] = d1 - d3;
+                    }
+                }
+                f4 pm[4];
+                auto column_sums = [&](const f4 (&m)[4], int xx, int xy) {
+                    const f4 t0 = (m[0] + m[1]) + m[2], t1 = (m[1] - m[2]) - m[3];
+                    f4(&S)[2][2] = Sx[xx & 1];
+                    if (xy == 0) {
+                        S[0][0] = t0;
+                        S[0][1] = t1;
+                    } else if (xy == 1) {
+                        S[0][0] += t0;
+                        S[0][1] += t1;
+                        S[1][0] = t0;
+                        S[1][1] = t1;
+                    } else if (xy == 2) {
+                        S[0][0] += t0;
+                        S[0][1] += t1;
+                        S[1][0] -= t0;
+                        S[1][1] -= t1;
+                    } else {
+                        S[1][0] -= t0;
+                        S[1][1] -= t1;
+                    }
+                    if (xy == 0)
+                        asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]));
+                    else
+                        asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]));
+                    if (xy == 3) {
+#pragma unroll
+                        for (int oy = 0; oy < 2; ++oy)
+#pragma unroll
+                            for (int oz = 0; oz < 2; ++oz) {
+                                if (xx == 0) {
+                                    Y[0][oy][oz] = S[oy][oz];
+                                } else if (xx == 1) {
+                                    Y[0][oy][oz] += S[oy][oz];
+                                    Y[1][oy][oz] = S[oy][oz];
+                                } else if (xx == 2) {
+                                    Y[0][oy][oz] += S[oy][oz];
+                                    Y[1][oy][oz] -= S[oy][oz];
+                                } else {
+                                    Y[1][oy][oz] -= S[oy][oz];
+                                }
+                            }
+                    }
+                };
+#pragma unroll
+                for (int cc = 0; cc <= 8; ++cc) {
+                    f4 m[4];
+                    if (cc < 8) {
+                        const int kx = cc >> 2, xy = cc & 3, xx = 2 * h + kx;
+                        const int j = xy * 4 + xx, jv = xy * 2 + kx;
+                        const float* ub = us + (j * 64 + lane) * 4 * NS;
+                        float uc[4 * NS];
+#pragma unroll
+                        for (int q = 0; q < NS; ++q) {
+                            const float4 u4 = *reinterpret_cast<const float4*>(ub + 4 * q);
+                            uc[4 * q] = u4.x;
+                            uc[4 * q + 1] = u4.y;
+                            uc[4 * q + 2] = u4.z;
+                            uc[4 * q + 3] = u4.w;
+                        }
+#pragma unroll
+                        for (int xz = 0; xz < 4; ++xz) {
+                            m[xz] = mfma4(uc[xz * NS], v[0][xz * 8 + jv], zero);
+#pragma unroll
+                            for (int s = 1; s < NS; ++s) m[xz] = mfma4(uc[xz * NS + s], v[s][xz * 8 + jv], m[xz]);
+                        }
+                    }
+                    if (cc > 0) column_sums(pm, 2 * h + ((cc - 1) >> 2), (cc - 1) & 3);
+                    if (cc < 8)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) pm[i] = m[i];
+                }
+            }
+            // ---- store the tile: dX[ci = 4 gq + r][2Qz + oz][2Qy + oy][2Qx + ox]
+            if (lane_ci && 16 * it + n < ntile) {
+#pragma unroll
+                for (int o = 0; o < 8; ++o) {
+                    const int z = 2 * qz + (o >> 2), y = 2 * qy + ((o >> 1) & 1), x = 2 * qx + (o & 1);
+                    if (z < g.D && y < g.H && x < g.W) {
+                        const int64_t off = ((int64_t)z * g.H + y) * g.W + x;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (4 * gq + r < CPG) dxb[r * xchan + off] = Y[o & 1][(o >> 1) & 1][o >> 2][r];
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int CPG, int NTH>
+int launch_dgrad_wino_k(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am,
+                        float* dx, hipStream_t st) {
+    WinoDgradParams P{};
+    P.g = make_geom<1, 1>(L);
+    P.w = w;
+    P.dP = dP;
+    P.am = am;
+    P.dx = dx;
+    P.G = L->groups;
+    P.QD = (P.g.D + 1) / 2;
+    P.QH = (P.g.H + 1) / 2;
+    P.QW = (P.g.W + 1) / 2;
+    // z chunk: the widest whose window rows fit the LDS beside U'; then split
+    // further while the grid has fewer than ~1024 blocks
+    const size_t per_row = (size_t)CPG * P.g.PH * P.g.PW * 5;
+    const size_t budget = 160 * 1024 - (size_t)wino_dg_u_floats<CPG>() * 4 - 64;
+    int zc = P.QD;
+    while (zc > 1 && (size_t)(zc + 1) * per_row > budget) --zc;
+    if ((size_t)(zc + 1) * per_row > budget) return RT_ELIMIT;
+    while (zc > 1 && (int64_t)B * P.G * ((P.QD + zc - 1) / zc) < 1024) zc = (zc + 1) / 2;
+    P.ZC = zc;
+    const size_t lds = (size_t)wino_dg_u_floats<CPG>() * 4 + (size_t)(zc + 1) * per_row + 16;
+    static bool attr = false;
+    if (!attr) {
+        if (const int rc_lds = allow_big_lds(&k_dgrad_wino<CPG, NTH>)) return rc_lds;
+        attr = true;
+    }
+    dim3 grid((P.QD + zc - 1) / zc, B * P.G);
+    hipLaunchKernelGGL((k_dgrad_wino<CPG, NTH>), grid, dim3(NTH), lds, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+int launch_dgrad_wino(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am,
+                      float* dx, hipStream_t st) {
+    if ((int64_t)B * L->groups > 65535) return RT_ELIMIT;
+    if (L->groups == 2) return launch_dgrad_wino_k<8, 512>(L, B, w, dP, am, dx, st);
+    if (L->groups == 4) return launch_dgrad_wino_k<4, 256>(L, B, w, dP, am, dx, st);
+    return RT_ELIMIT;
+}
+
 bool bad_layer(const rt_conv_layer* L) {
     if (!L) return true;
     if (!((L->cin == 4 && L->groups == 1) || (L->cin == 16 && (L->groups == 1 || L->groups == 2 || L->groups == 4))))
@@ -2886,9 +3201,14 @@ extern "C" int rt_conv_relu_pool_dgrad(const rt_conv_layer* L, int32_t batch, co
     if (bad_layer(L) || L->cin != 16 || batch < 1 || batch > 65535 || !w_d || !dy_d || !argmax_d || !dx_d)
         return rt_internal_fail(RT_EINVAL, "rt_conv_relu_pool_dgrad: bad argument");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // grouped stages: the z-shift ring kernel; then the dense ring kernel; the
-    // tile kernel for padded pools
+    // grouped stages: the Winograd kernel (f32), the z-shift ring kernel
+    // (bf16x3 products, or where the Winograd kernel's LDS does not fit); then
+    // the dense ring kernel; the tile kernel for padded pools
     const bool pad0 = L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0;
+    if (pad0 && L->groups > 1 && g_conv_prec == 0) {
+        const int rc = launch_dgrad_wino(L, batch, w_d, dy_d, argmax_d, dx_d, st);
+        if (rc != RT_ELIMIT) return rc;
+    }
     if (pad0 && L->groups > 1 && (int64_t)batch * L->groups <= 65535) {
         const int rc = L->groups == 2 ? launch_dgrad_ring_zs<2>(L, batch, w_d, dy_d, argmax_d, dx_d, st)
                                       : launch_dgrad_ring_zs<4>(L, batch, w_d, dy_d, argmax_d, dx_d, st);
