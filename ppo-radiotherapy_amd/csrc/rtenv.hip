@@ -576,25 +576,47 @@ __device__ int beam_env(const BeamParams& P, int e, int lane, const float* act) 
         else no_splats(pi);
         if (pairs && k + 1 < niter) march_splats(P.G.g, b, k + 1, yk + b.sgy, zk + b.sgz, ni, nw);
         else no_splats(ni);
+        // the lane's owned voxels (<= 4, distinct): every load of the
+        // iteration is issued before the first store -- written as a
+        // load-modify-store per voxel the compiler kept each store ahead of
+        // the next voxel's loads (it cannot prove the rows do not alias), so
+        // a lane paid 4 (lung-first rows: 8) dependent HBM round trips
+        bool own[4];
+        float wv[4];
+        int32_t pv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int32_t v = ci[i];
-            if (v < 0) continue;
-            bool owned = true;
+            bool owned = v >= 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) owned = owned && (pi[j] != v);
-            if (!owned) continue;
             float w = cw[i];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (ni[j] == v) w = w + nw[j];
-            const int32_t pv = P.lib.dose_pos ? P.lib.dose_pos[v] : v;
-            const float old_d = dose[pv];
-            const float new_d = clip01(old_d + w * bd);
-            dose[pv] = new_d;
-            if (P.incremental && ((lbits[v >> 5] >> (v & 31)) & 1u)) {
-                dcnt += (new_d > thr ? 1 : 0) - (old_d > thr ? 1 : 0);
-                dsum += (double)new_d - (double)old_d;
+            own[i] = owned;
+            wv[i] = w;
+            pv[i] = owned ? v : 0;
+        }
+        if (P.lib.dose_pos) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pv[i] = own[i] ? P.lib.dose_pos[pv[i]] : 0;
+        }
+        float old_d[4];
+        uint32_t lb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            old_d[i] = own[i] ? dose[pv[i]] : 0.0f;
+            lb[i] = (P.incremental && own[i]) ? lbits[ci[i] >> 5] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (!own[i]) continue;
+            const float new_d = clip01(old_d[i] + wv[i] * bd);
+            dose[pv[i]] = new_d;
+            if (P.incremental && ((lb[i] >> (ci[i] & 31)) & 1u)) {
+                dcnt += (new_d > thr ? 1 : 0) - (old_d[i] > thr ? 1 : 0);
+                dsum += (double)new_d - (double)old_d[i];
             }
         }
         // advance (ya, za) to iteration k + 63

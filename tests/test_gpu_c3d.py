@@ -252,16 +252,18 @@ def _check_backward(cin, groups, dims, pad, B, prod_err=0.0):
 
 
 def test_planes_too_wide_fail_cleanly():
-    """Beyond every plane ring and the tile kernel (conv1 planes ~170 wide in
-    f32 LDS) the stage returns RT_ELIMIT with a message; nothing is launched."""
+    """Beyond every plane ring and the tile kernel the stage returns RT_ELIMIT
+    with a message; nothing is launched.  (The Winograd ring takes conv1
+    planes up to ~380 wide in f32 -- one pooled row per band, 6 slots + U in
+    160 KiB; the direct ring ~170, the tile kernel less.)"""
     from ppo_radiotherapy_amd import _lib
 
-    L = _layer(4, 1, (5, 7, 258), (1, 1, 0))
+    L = _layer(4, 1, (5, 7, 402), (1, 1, 0))
     lib = _lib.load()
-    x = torch.zeros((1, 4, 5, 7, 258), device="cuda")
+    x = torch.zeros((1, 4, 5, 7, 402), device="cuda")
     w = torch.zeros((16, 4, 3, 3, 3), device="cuda")
     b = torch.zeros(16, device="cuda")
-    y = torch.zeros((1, 16, 2, 3, 128), device="cuda")
+    y = torch.zeros((1, 16, 2, 3, 200), device="cuda")
     rc = lib.rt_conv_relu_pool_fwd(ctypes.byref(L), 1, x.data_ptr(), None, w.data_ptr(), b.data_ptr(), y.data_ptr(),
                                    None, None)
     assert rc == -5 and b"exceeds LDS" in lib.rt_last_error()
@@ -291,8 +293,10 @@ def test_features_extractor_matches_torch_modules(shape, B, prec):
 
 def _routed_reference(ref, x64, ams, plan):
     """The float64 extractor with each MaxPool3d replaced by a gather at the
-    window position the kernel's argmax byte names (ReLU applied first, so an
-    inactive window gathers 0, as the pool does)."""
+    window position the kernel's argmax byte names, times the byte's ReLU
+    activity bit (a window whose float64 maximum lies within rounding of 0 may
+    be active on one side and not on the other; the kernel passes no gradient
+    through an inactive window, so neither does this reference)."""
     h = x64
     for conv, am, (layer, od) in zip((ref.cnn[0], ref.cnn[3], ref.cnn[6]), ams, plan):
         y = F.relu(conv(h))
@@ -302,7 +306,8 @@ def _routed_reference(ref, x64, ams, plan):
         pz, py, px = torch.meshgrid(*[torch.arange(n) for n in od], indexing="ij")
         flat = (((2 * pz - pad[0] + (k >> 2)) * ch + (2 * py - pad[1] + ((k >> 1) & 1))) * cw
                 + (2 * px - pad[2] + (k & 1)))
-        h = y.reshape(B, C, -1).gather(2, flat.reshape(B, C, -1)).reshape(B, C, *od)
+        active = ((am.long() >> 3) & 1).to(y.dtype)
+        h = y.reshape(B, C, -1).gather(2, flat.reshape(B, C, -1)).reshape(B, C, *od) * active
     return ref.mlp(h.flatten(1))
 
 
