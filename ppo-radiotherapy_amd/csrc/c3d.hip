@@ -2829,13 +2829,31 @@ __global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
     float* dps = xs + wino_dg_u_floats<CPG>();
     uint8_t* ams = reinterpret_cast<uint8_t*>(dps + COG * chw);
     {
+        // 8 loads in flight per thread (a load-then-store loop waited out one
+        // HBM round trip per element)
+        constexpr int U = 8;
         const size_t pchan = (size_t)g.PD * plane;
         const float* src = P.dP + ((size_t)b * CO + grp * COG) * pchan + (size_t)wz0 * plane;
         const uint8_t* asrc = P.am + ((size_t)b * CO + grp * COG) * pchan + (size_t)wz0 * plane;
-        for (int i = threadIdx.x; i < COG * chw; i += NTH) {
-            const int c = i / chw, rem = i - c * chw;
-            dps[i] = src[c * pchan + rem];
-            ams[i] = asrc[c * pchan + rem];
+        const int tot = COG * chw;
+        for (int i0 = threadIdx.x; i0 < tot; i0 += NTH * U) {
+            float v[U];
+            int a[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = min(i0 + u * NTH, tot - 1);
+                const int c = i / chw, rem = i - c * chw;
+                v[u] = src[c * pchan + rem];
+                a[u] = asrc[c * pchan + rem];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NTH;
+                if (i < tot) {
+                    dps[i] = v[u];
+                    ams[i] = (uint8_t)a[u];
+                }
+            }
         }
     }
     // ---- U' = G W' G^T, W' = the flipped filter, for (ci = n, co = 4s + gq)
@@ -3057,14 +3075,19 @@ int launch_dgrad_wino_k(const rt_conv_layer* L, int32_t B, const float* w, const
     P.QD = (P.g.D + 1) / 2;
     P.QH = (P.g.H + 1) / 2;
     P.QW = (P.g.W + 1) / 2;
-    // z chunk: the widest whose window rows fit the LDS beside U'; then split
-    // further while the grid has fewer than ~1024 blocks
+    // z chunk: equal chunks whose window rows fit half the LDS beside U' (two
+    // blocks per CU: one block's load phase runs beside the other's MFMAs),
+    // else the whole LDS; then split further while the grid has fewer than
+    // ~2048 blocks
     const size_t per_row = (size_t)CPG * P.g.PH * P.g.PW * 5;
-    const size_t budget = 160 * 1024 - (size_t)wino_dg_u_floats<CPG>() * 4 - 64;
-    int zc = P.QD;
-    while (zc > 1 && (size_t)(zc + 1) * per_row > budget) --zc;
-    if ((size_t)(zc + 1) * per_row > budget) return RT_ELIMIT;
-    while (zc > 1 && (int64_t)B * P.G * ((P.QD + zc - 1) / zc) < 1024) zc = (zc + 1) / 2;
+    const size_t u_bytes = (size_t)wino_dg_u_floats<CPG>() * 4 + 64;
+    auto rows_fit = [&](size_t lds) { return lds > u_bytes ? (int)((lds - u_bytes) / per_row) - 1 : 0; };
+    int zmax = rows_fit(80 * 1024);
+    if (zmax < 2) zmax = rows_fit(160 * 1024);
+    if (zmax < 1) return RT_ELIMIT;
+    int chunks = (P.QD + zmax - 1) / zmax;
+    while (chunks < P.QD && (int64_t)B * P.G * chunks < 2048) ++chunks;
+    const int zc = (P.QD + chunks - 1) / chunks;
     P.ZC = zc;
     const size_t lds = (size_t)wino_dg_u_floats<CPG>() * 4 + (size_t)(zc + 1) * per_row + 16;
     static bool attr = false;
@@ -3082,7 +3105,7 @@ int launch_dgrad_wino_k(const rt_conv_layer* L, int32_t B, const float* w, const
 int launch_dgrad_wino(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am,
                       float* dx, hipStream_t st) {
     if ((int64_t)B * L->groups > 65535) return RT_ELIMIT;
-    if (L->groups == 2) return launch_dgrad_wino_k<8, 512>(L, B, w, dP, am, dx, st);
+    if (L->groups == 2) return launch_dgrad_wino_k<8, 256>(L, B, w, dP, am, dx, st);
     if (L->groups == 4) return launch_dgrad_wino_k<4, 256>(L, B, w, dP, am, dx, st);
     return RT_ELIMIT;
 }

@@ -292,14 +292,15 @@ def test_features_extractor_matches_torch_modules(shape, B, prec):
 
 
 def _routed_reference(ref, x64, ams, plan):
-    """The float64 extractor with each MaxPool3d replaced by a gather at the
-    window position the kernel's argmax byte names, times the byte's ReLU
-    activity bit (a window whose float64 maximum lies within rounding of 0 may
-    be active on one side and not on the other; the kernel passes no gradient
-    through an inactive window, so neither does this reference)."""
+    """The float64 extractor with each ReLU + MaxPool3d replaced by a gather
+    at the window position the kernel's argmax byte names, times the byte's
+    ReLU activity bit -- the ReLU itself routed through the kernel's decision:
+    a window whose float64 maximum lies within rounding of 0 may be active on
+    one side and not on the other, and the kernel passes the window's whole
+    gradient exactly when its byte says active."""
     h = x64
     for conv, am, (layer, od) in zip((ref.cnn[0], ref.cnn[3], ref.cnn[6]), ams, plan):
-        y = F.relu(conv(h))
+        y = conv(h)
         B, C, cd, ch, cw = y.shape
         pad = tuple(layer.pool_pad)
         k = am.long() & 7

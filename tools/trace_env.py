@@ -7,6 +7,7 @@ each phase's per-env duration (median / p90 / max, us) and each kernel's
 start/end spread relative to the step's first stamp.
 
     python tools/trace_env.py [--mode incremental|dense] [--envs 4096] [--build-only]
+                              [--pipelined [--stagger]]   (dense: the two-group rollout call)
 """
 import argparse
 import ctypes
@@ -44,6 +45,9 @@ def main():
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--two-call", action="store_true", help="rt_policy_sample + rt_env_step instead of the fused step")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="dense mode: the pipelined two-group rollout call (rt_env_rollout_policy); stamps of the last step")
+    ap.add_argument("--stagger", action="store_true", help="staggered episode phases first (bench.stagger_phases)")
     ap.add_argument("--persistent", action="store_true",
                     help="the steps as one persistent k_rollout_policy launch (incremental); stamps of the last step")
     a = ap.parse_args()
@@ -66,7 +70,13 @@ def main():
     lib = assets.synthetic_library((64,) * 3, 1000, 0)
     cfg.fused_env_step = not a.two_call
     tr = ps.make(a.envs, 0, lib, dev, cfg, a.mode)
-    if a.persistent:
+    if a.stagger:
+        bench.stagger_phases(tr, tr.env, dev)
+    if a.pipelined:
+        tr.fused_rollout = True
+        tr.env.set_rollout_groups(2)
+        tr.rollout_steps(0, min(a.steps, tr.T))
+    elif a.persistent:
         tr.fused_rollout = True
         tr.rollout_steps(0, min(a.steps, tr.T))
     else:
@@ -93,9 +103,15 @@ def main():
         d = (us[:, s1] - us[:, s0])[stepped]
         out["phases_us"][name] = {"median": float(np.median(d)), "p90": float(np.percentile(d, 90)),
                                   "max": float(d.max())}
-    for k, (s0, s1) in {"k_policy_sample": (0, 1), "k_beam": (2, 4), "k_finish": (5, 8)}.items():
-        out["kernel_span_us"][k] = {"first_start": float(us[:, s0].min()), "last_start": float(us[:, s0].max()),
-                                    "first_end": float(us[stepped, s1].min()), "last_end": float(us[:, s1].max())}
+    groups = [np.arange(a.envs) < a.envs // 2, np.arange(a.envs) >= a.envs // 2] if a.pipelined else [None]
+    for gi, gm in enumerate(groups):
+        sel = np.ones(a.envs, bool) if gm is None else gm
+        for k, (s0, s1) in {"k_policy_sample": (0, 1), "k_beam": (2, 4), "k_finish": (5, 8)}.items():
+            name = k if gm is None else f"{k}[group {gi}]"
+            out["kernel_span_us"][name] = {"first_start": float(us[sel, s0].min()),
+                                           "last_start": float(us[sel, s0].max()),
+                                           "first_end": float(us[stepped & sel, s1].min()),
+                                           "last_end": float(us[sel, s1].max())}
     if a.persistent:  # slots 13/14: each wave's kernel entry / exit
         blk = np.arange(a.envs) // 16
         ent, ext = us[:, 13], us[:, 14]
