@@ -41,28 +41,54 @@ struct alignas(16) Lds {
     float ab3[NACT], ls[NACT], cb3[4];
 };
 
+// Stage the parameters by LDS DMA (global_load_lds, 4 B per lane, no
+// VGPRs): 160 wave-sized pieces -- the 64-float rows of the two 64x64 layers
+// at their padded stride, then the small tensors in 64-float pieces -- split
+// over the block's waves, every piece in flight at once.  A register copy
+// loop (load, store, next) waited out one dependent L2 round trip per
+// iteration: 36 us of the pipelined rollout's 44 us policy phase beside the
+// dose stream (tools/trace_env.py --pipelined).  Ends with this wave's DMA
+// landed; the caller's barrier then publishes the whole image.
+typedef __attribute__((address_space(3))) void* stage_lds_t;
+typedef __attribute__((address_space(1))) void* stage_glb_t;
+constexpr int kStagePieces = 2 * H + 2 * NOBS + NACT + 5 + 3;
+
 __device__ __forceinline__ void stage(Lds& L, const Weights& w, int tid, int nthreads) {
-    for (int i = tid; i < H * H; i += nthreads) {
-        L.aw2[(i >> 6) * W2S + (i & 63)] = w.p[2][i];
-        L.cw2[(i >> 6) * W2S + (i & 63)] = w.p[9][i];
+    const int lane = tid & 63, nw = nthreads >> 6;
+    for (int p = __builtin_amdgcn_readfirstlane(tid >> 6); p < kStagePieces; p += nw) {
+        const float* src;
+        float* dst;
+        int n = 64;
+        if (p < H) {
+            src = w.p[2] + p * H;
+            dst = L.aw2 + p * W2S;
+        } else if (p < 2 * H) {
+            src = w.p[9] + (p - H) * H;
+            dst = L.cw2 + (p - H) * W2S;
+        } else if (p < 2 * H + NOBS) {
+            src = w.p[0] + (p - 2 * H) * 64;
+            dst = L.aw1 + (p - 2 * H) * 64;
+        } else if (p < 2 * H + 2 * NOBS) {
+            src = w.p[7] + (p - 2 * H - NOBS) * 64;
+            dst = L.cw1 + (p - 2 * H - NOBS) * 64;
+        } else if (p < 2 * H + 2 * NOBS + NACT) {
+            src = w.p[4] + (p - 2 * H - 2 * NOBS) * 64;
+            dst = L.aw3 + (p - 2 * H - 2 * NOBS) * 64;
+        } else {
+            switch (p - (2 * H + 2 * NOBS + NACT)) {
+                case 0: src = w.p[1]; dst = L.ab1; break;
+                case 1: src = w.p[3]; dst = L.ab2; break;
+                case 2: src = w.p[8]; dst = L.cb1; break;
+                case 3: src = w.p[10]; dst = L.cb2; break;
+                case 4: src = w.p[11]; dst = L.cw3; break;
+                case 5: src = w.p[5]; dst = L.ab3; n = NACT; break;
+                case 6: src = w.p[6]; dst = L.ls; n = NACT; break;
+                default: src = w.p[12]; dst = L.cb3; n = 1; break;
+            }
+        }
+        if (lane < n) __builtin_amdgcn_global_load_lds((stage_glb_t)(src + lane), (stage_lds_t)dst, 4, 0, 0);
     }
-    for (int i = tid; i < H * NOBS; i += nthreads) {
-        L.aw1[i] = w.p[0][i];
-        L.cw1[i] = w.p[7][i];
-    }
-    for (int i = tid; i < NACT * H; i += nthreads) L.aw3[i] = w.p[4][i];
-    for (int i = tid; i < H; i += nthreads) {
-        L.ab1[i] = w.p[1][i];
-        L.ab2[i] = w.p[3][i];
-        L.cb1[i] = w.p[8][i];
-        L.cb2[i] = w.p[10][i];
-        L.cw3[i] = w.p[11][i];
-    }
-    if (tid < NACT) {
-        L.ab3[tid] = w.p[5][tid];
-        L.ls[tid] = w.p[6][tid];
-    }
-    if (tid == 0) L.cb3[0] = w.p[12][0];
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's pieces have landed (vmcnt 0)
 }
 
 __device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {

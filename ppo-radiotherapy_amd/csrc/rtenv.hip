@@ -43,7 +43,15 @@
 namespace {
 
 constexpr int kStepThreads = 256;
-constexpr int kUnroll = 8;  // k_dense: float4 loads in flight per thread (4/8 measured equal)
+// variant builds (tools/build_variant.py) override these two for sweeps
+#ifndef RT_DENSE_UNROLL
+#define RT_DENSE_UNROLL 8
+#endif
+#ifndef RT_PIPE_DENSE_BPC
+#define RT_PIPE_DENSE_BPC 5
+#endif
+
+constexpr int kUnroll = RT_DENSE_UNROLL;  // k_dense: float4 loads in flight per thread (4/8 measured equal)
 // Library events order work between the library's own streams on one device
 // (the pipelined rollout's fork / turns / join) or time kernels; neither needs
 // the system-scope release + acquire (L2 writeback and invalidate) a default
@@ -145,7 +153,8 @@ struct Library {
     const int32_t* dose_pos;  // voxel -> position in a dose row (lung-first layout), null = C order
     const int32_t* vox;
     const int32_t* vpos;      // per tumour voxel: its dose-row position (= vox in C order)
-    const uint32_t* coord;   // per tumour voxel: x << 20 | y << 10 | z (no divisions in k_finish)
+    const uint32_t* coord;   // per tumour voxel: lung << 31 | x << 20 | y << 10 | z (no divisions, no
+                             // lung-mask lookup in k_finish)
     const uint32_t* ops;     // packed (a | b << 16); dst = n + op index
     const int32_t* lvl_end;  // per level: op index end (relative to op_base)
     const TumourMeta* meta;
@@ -1102,9 +1111,11 @@ __device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const 
 }
 
 // PF (k_finish): the step's independent scalars (the env's dense partial
-// sums, t, episode return / length) are loaded before the tumour gather and
-// the nearest tumour voxel's index travels with the distance argmin, so the
-// tail issues no dependent load (each one a few us beside the dose stream).
+// sums, t, episode return / length) are loaded before the tumour gather; the
+// nearest tumour voxel's packed coordinates travel with the distance argmin,
+// so the tail issues no dependent load (each one a few us beside the dose
+// stream).
+constexpr int kGatherU = 4;  // tumour voxels per lane in flight in the gather
 template <bool PF = false>
 __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char* wave_lds) {
     float* tvals = reinterpret_cast<float*>(wave_lds);
@@ -1127,11 +1138,9 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     }
     const float* dose = P.st.dose + (size_t)e * P.G.Vpad;
     const int nt = m.n;
-    const int32_t* tv = P.lib.vox + m.vox_base;
     const int32_t* tp = P.lib.vpos + m.vox_base;
     const uint32_t* tc = P.lib.coord + m.vox_base;
     const double px = pose[0], py = pose[1], pz = pose[2];
-    const int W = P.G.g[2], H = P.G.g[1], HW = H * W;
     // plan slots (leaves 0..n-1, op o -> n+o): the wave's LDS, or for a
     // tumour above the LDS capacity a global scratch row (L2)
     const bool in_lds = nt <= P.max_tvox;
@@ -1167,35 +1176,56 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     }
     int ctum = 0;
     double best = INFINITY;
-    int bidx = 0x7fffffff, bvox = 0;
-    auto voxel = [&](int i, int v, uint32_t c, float x, bool lung) {
+    int bidx = 0x7fffffff;
+    uint32_t bc = 0;  // packed coordinates of the nearest voxel
+    auto voxel = [&](int i, uint32_t c, float x) {
         if (in_lds) tvals[i] = x;
         else tg[i] = x;
-        ctum += (lung && x > P.C.lung_thr) ? 1 : 0;
-        const int ix = (int)(c >> 20), iy = (int)((c >> 10) & 1023u), iz = (int)(c & 1023u);
+        ctum += ((c >> 31) && x > P.C.lung_thr) ? 1 : 0;
+        const int ix = (int)((c >> 20) & 1023u), iy = (int)((c >> 10) & 1023u), iz = (int)(c & 1023u);
         const double d0 = (double)ix - px, d1 = (double)iy - py, d2 = (double)iz - pz;
         const double nn = sqrt((d0 * d0 + d1 * d1) + d2 * d2);  // np.linalg.norm(axis=1) order
         if (nn < best) {  // ascending i per lane: the first minimum
             best = nn;
             bidx = i;
-            if constexpr (PF) bvox = v;
+            bc = c;
         }
     };
-    for (int i = lane; i < nt; i += 64) {
-        const int v = tv[i];
-        voxel(i, v, tc[i], dose[tp[i]], (P.lib.lung_bits[v >> 5] >> (v & 31)) & 1u);
+    // two dependent loads per voxel (its row position and packed coordinates,
+    // then its dose): kGatherU voxels per lane in flight (one voxel at a time
+    // paid 2 round trips per 64 voxels: ~40 us for the largest tumours beside
+    // the dose stream)
+    for (int i0 = 0; i0 < nt; i0 += 64 * kGatherU) {
+        int pos[kGatherU];
+        uint32_t cc[kGatherU];
+        float x[kGatherU];
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const int i = i0 + 64 * u + lane;
+            pos[u] = i < nt ? tp[i] : 0;
+            cc[u] = i < nt ? tc[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const int i = i0 + 64 * u + lane;
+            x[u] = i < nt ? dose[pos[u]] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const int i = i0 + 64 * u + lane;
+            if (i < nt) voxel(i, cc[u], x[u]);
+        }
     }
     ctum = wave_sum_i(ctum);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const double ob = __shfl_xor(best, off, 64);
         const int oi = __shfl_xor(bidx, off, 64);
-        int ov = 0;
-        if constexpr (PF) ov = __shfl_xor(bvox, off, 64);
+        const uint32_t oc = (uint32_t)__shfl_xor((int)bc, off, 64);
         if (ob < best || (ob == best && oi < bidx)) {
             best = ob;
             bidx = oi;
-            if constexpr (PF) bvox = ov;
+            bc = oc;
         }
     }
     if (lane == 0) RT_STAMP(e, 6);
@@ -1231,8 +1261,7 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
         const float ratio = S / m.T;
         const float r_tum = ratio * P.C.tum_reward;
         const double r_lung = (double)c / m.lung_total * P.C.lung_reward;
-        const int v = PF ? bvox : tv[bidx];
-        const int ix = v / HW, iy = (v / W) % H, iz = v % W;
+        const int ix = (int)((bc >> 20) & 1023u), iy = (int)((bc >> 10) & 1023u), iz = (int)(bc & 1023u);
         const double dn = ddot_norm3((double)ix - px, (double)iy - py, (double)iz - pz);
         const double r_dist = dn / P.G.normS * P.C.dist_reward;
         const double total = ((double)r_tum + r_lung) + r_dist;
@@ -1806,7 +1835,7 @@ struct rt_env {
     int finish_wpb = 4;      // k_finish envs per block
     int fused_wpb = 16;      // k_step_policy envs (waves) per block
     int pipe_wpb = 8;        // ... in the pipelined dense rollout
-    int pipe_dense_bpc = 6;  // its k_dense: persistent, blocks per CU
+    int pipe_dense_bpc = RT_PIPE_DENSE_BPC;  // its k_dense: persistent, blocks per CU
     int num_cu = 256;        // compute units of the device
     size_t pipe_smem = 0;
     size_t fused_smem = 0;   // k_step_policy dynamic LDS
@@ -2070,7 +2099,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         for (int i = 0; i < n; ++i) vpos.push_back(env->lung_first ? dpos[iv[i]] : iv[i]);
         for (int i = 0; i < n; ++i) {
             const int64_t v = iv[i];
-            coord.push_back((uint32_t)(v / ((int64_t)G.g[1] * G.g[2])) << 20 |
+            coord.push_back((cfg->lungs_h[v] ? 1u << 31 : 0u) | (uint32_t)(v / ((int64_t)G.g[1] * G.g[2])) << 20 |
                             (uint32_t)((v / G.g[2]) % G.g[1]) << 10 | (uint32_t)(v % G.g[2]));
         }
         PlanBuilder pb{iv, n, (int64_t)G.V};
@@ -2316,14 +2345,7 @@ int launch_finish(rt_env* env, float* obs, float* reward, uint8_t* term, float* 
     return RT_OK;
 }
 
-// k_dense / k_dense_vis (skipped in incremental mode) then k_finish
-// envs [e0, e1) (e1 < 0: all).  wait_ev: k_dense starts after it (the other
-// env group's k_dense of the pipelined rollout); done_ev: recorded after k_dense.
-int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, float* info, hipStream_t stream,
-                        hipEvent_t* ev, int e0 = 0, int e1 = -1, hipEvent_t wait_ev = nullptr,
-                        hipEvent_t done_ev = nullptr, int persist_bpc = 0) {
-    if (e1 < 0) e1 = env->N;
-    const int n = e1 - e0;
+DenseParams dense_params(const rt_env* env, int e0) {
     DenseParams dp{};
     dp.G = env->G;
     dp.lung_thr = env->C.lung_thr;
@@ -2335,8 +2357,13 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
     dp.vec_per_slice = env->vec_per_slice;
     dp.lung_n = env->lung_n;
     dp.e_begin = e0;
-    if (wait_ev) RT_HIP(hipStreamWaitEvent(stream, wait_ev, 0));
-    if (ev) (void)hipEventRecord(ev[1], stream);
+    return dp;
+}
+
+// k_dense / k_dense_vis of envs [e0, e0 + n) (nothing in incremental mode);
+// persist_bpc > 0: the persistent k_dense with that many blocks per CU
+int launch_dense(rt_env* env, int e0, int n, float* obs, int persist_bpc, hipStream_t stream) {
+    const DenseParams dp = dense_params(env, e0);
     if (env->incremental) {
         // no dense pass: k_beam maintains the lung count and sum
     } else if (env->visionless) {
@@ -2353,7 +2380,16 @@ int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, f
         hipLaunchKernelGGL(k_dense_vis, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dv);
         RT_LAUNCH_CHECK("k_dense_vis");
     }
-    if (done_ev) RT_HIP(hipEventRecord(done_ev, stream));
+    return RT_OK;
+}
+
+// k_dense / k_dense_vis (skipped in incremental mode) then k_finish of envs
+// [e0, e1) (e1 < 0: all) on one stream
+int launch_dense_finish(rt_env* env, float* obs, float* reward, uint8_t* term, float* info, hipStream_t stream,
+                        hipEvent_t* ev, int e0 = 0, int e1 = -1) {
+    if (e1 < 0) e1 = env->N;
+    if (ev) (void)hipEventRecord(ev[1], stream);
+    if (const int rc = launch_dense(env, e0, e1 - e0, obs, 0, stream)) return rc;
     if (ev) (void)hipEventRecord(ev[2], stream);
     if (const int rc = launch_finish(env, obs, reward, term, info, stream, e0, e1)) return rc;
     if (ev) (void)hipEventRecord(ev[3], stream);
@@ -2502,12 +2538,21 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
             hipLaunchKernelGGL(k_step_policy<false>, dim3((e1 - e0 + wpb - 1) / wpb), dim3(64 * wpb), smem,
                                S[g], bp, fp, Q);
             RT_LAUNCH_CHECK("k_step_policy");
+            if (!piped) {
+                if (const int rc = launch_dense_finish(env, obs_d, rew, terminated_d, info, s, ev, e0, e1)) return rc;
+                continue;
+            }
             // k_dense turns in a ring: group g of step t after group g-1 of step t
-            // (group 0 after group G-1 of step t-1)
-            hipEvent_t wait = (piped && (t > 0 || g > 0)) ? dense_ev[(g + G - 1) % G] : nullptr;
-            int rc = launch_dense_finish(env, obs_d, rew, terminated_d, info, S[g], ev, e0, e1, wait,
-                                         piped ? dense_ev[g] : nullptr, piped ? env->pipe_dense_bpc : 0);
-            if (rc) return rc;
+            // (group 0 after group G-1 of step t-1), each on its group's stream
+            // (one cross-stream wait per turn; a dedicated dose stream, two
+            // waits per turn, measured 18 % slower: DESIGN §10)
+            if (t > 0 || g > 0) RT_HIP(hipStreamWaitEvent(S[g], dense_ev[(g + G - 1) % G], 0));
+            if (ev) (void)hipEventRecord(ev[1], S[g]);
+            if (const int rc = launch_dense(env, e0, e1 - e0, obs_d, env->pipe_dense_bpc, S[g])) return rc;
+            RT_HIP(hipEventRecord(dense_ev[g], S[g]));
+            if (ev) (void)hipEventRecord(ev[2], S[g]);
+            if (const int rc = launch_finish(env, obs_d, rew, terminated_d, info, S[g], e0, e1)) return rc;
+            if (ev) (void)hipEventRecord(ev[3], S[g]);
         }
     }
     if (piped) {

@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--two-call", action="store_true", help="rt_policy_sample + rt_env_step instead of the fused step")
     ap.add_argument("--pipelined", action="store_true",
                     help="dense mode: the pipelined two-group rollout call (rt_env_rollout_policy); stamps of the last step")
+    ap.add_argument("--dump", default=None, help="also save the raw stamp table (us, [envs][16]) to this .npy")
     ap.add_argument("--stagger", action="store_true", help="staggered episode phases first (bench.stagger_phases)")
     ap.add_argument("--persistent", action="store_true",
                     help="the steps as one persistent k_rollout_policy launch (incremental); stamps of the last step")
@@ -98,6 +99,8 @@ def main():
     t0 = t[:, 13].min() if a.persistent else t[:, 0].min()
     us = (t - t0) * 0.01  # 100 MHz
     out = {"mode": a.mode, "envs": a.envs, "phases_us": {}, "kernel_span_us": {}}
+    if a.dump:
+        np.save(a.dump, us)
     stepped = t[:, 8] > t[:, 5]
     for name, (s0, s1) in PHASES.items():
         d = (us[:, s1] - us[:, s0])[stepped]
