@@ -32,6 +32,10 @@
 #include <cstdint>
 #include <cstring>
 #include <algorithm>
+#include <climits>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <type_traits>
 #include <utility>
 
@@ -895,6 +899,15 @@ constexpr int wino_u_floats() {  // U in LDS: 16 columns x 64 lanes x 4 xi_z x C
     return 16 * 64 * 4 * (CPG / 4);
 }
 
+// U element (column j, lane, i = xi_z * NS + s) in LDS: float4 q = i / 4 of
+// the lane's 4 NS values at ((j NS + q) 64 + lane) 4, so the column's NS
+// ds_read_b128 are each 64 lanes x 16 B contiguous (conflict-free; a lane's
+// values contiguous put lanes 8 dwords apart at NS = 2: 2-way conflicts)
+template <int NS>
+__device__ __forceinline__ int wino_u_index(int j, int lane, int i) {
+    return ((j * NS + (i >> 2)) * 64 + lane) * 4 + (i & 3);
+}
+
 struct WinoParams {
     const float* x;
     const int64_t* rows;  // sample b reads x row rows[b] (null: b)
@@ -933,8 +946,8 @@ __global__ __launch_bounds__(NTH) void k_conv_wino(WinoParams P) {
     for (int i = 0; i < 4; ++i) load_plane(2 * k0 + i, i);
 
     // ---- U = G w G^T for (co = n, ci = 4s + gq), by wave 0 into LDS after the
-    // ring: us[(j * 64 + lane) * 4 NS + xz * NS + s], j = xy * 4 + xx (one or
-    // two ds_read_b128 per (xi_x, xi_y) column give its 4 xi_z x NS values)
+    // ring: element (j = xy * 4 + xx, lane, xz * NS + s) at wino_u_index (one
+    // or two ds_read_b128 per (xi_x, xi_y) column give its 4 xi_z x NS values)
     float* us = xs + kRing * SLOT;
     if (wave == 0) {
 #pragma unroll
@@ -966,11 +979,10 @@ __global__ __launch_bounds__(NTH) void k_conv_wino(WinoParams P) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) {  // j = xy * 4 + xx; along z
                 const float a0 = sy[j], a1 = sy[16 + j], a2 = sy[32 + j];
-                float* q = us + (j * 64 + lane) * 4 * NS + s;
-                q[0] = a0;
-                q[NS] = 0.5f * ((a0 + a1) + a2);
-                q[2 * NS] = 0.5f * ((a0 - a1) + a2);
-                q[3 * NS] = a2;
+                us[wino_u_index<NS>(j, lane, s)] = a0;
+                us[wino_u_index<NS>(j, lane, NS + s)] = 0.5f * ((a0 + a1) + a2);
+                us[wino_u_index<NS>(j, lane, 2 * NS + s)] = 0.5f * ((a0 - a1) + a2);
+                us[wino_u_index<NS>(j, lane, 3 * NS + s)] = a2;
             }
         }
     }
@@ -1105,11 +1117,10 @@ __global__ __launch_bounds__(NTH) void k_conv_wino(WinoParams P) {
                     if (c < 8) {
                         const int kx = c >> 2, xy = c & 3, xx = 2 * h + kx;
                         const int j = xy * 4 + xx, jv = xy * 2 + kx;
-                        const float* ub = us + (j * 64 + lane) * 4 * NS;
                         float uc[4 * NS];
 #pragma unroll
                         for (int q = 0; q < NS; ++q) {
-                            const float4 u4 = *reinterpret_cast<const float4*>(ub + 4 * q);
+                            const float4 u4 = *reinterpret_cast<const float4*>(us + wino_u_index<NS>(j, lane, 4 * q));
                             uc[4 * q] = u4.x;
                             uc[4 * q + 1] = u4.y;
                             uc[4 * q + 2] = u4.z;
@@ -1161,9 +1172,66 @@ __global__ __launch_bounds__(NTH) void k_conv_wino(WinoParams P) {
     }
 }
 
+// LDS-bank cycles of one patch read (ds_read_b64: two 32-lane groups, bank =
+// dword mod 64) summed over a band's items: lane (n, gq) reads dwords
+// gq CS + 2 r YS + 2 px + {0, 1} of window 16 it + n = (r, px), lanes past
+// the band repeating its last window (a broadcast).  The read pattern of
+// every (channel quad, dz, dy) of an item is this one shifted by a constant.
+int wino_read_cycles(int PW, int nwin, int YS, int CS) {
+    int total = 0;
+    for (int it = 0; it * 16 < nwin; ++it)
+        for (int half = 0; half < 2; ++half) {
+            int load[64] = {};
+            int seen[32][2];
+            int ns = 0;
+            for (int l = 32 * half; l < 32 * half + 32; ++l) {
+                const int n = l & 15, gq = l >> 4;
+                const int wi = std::min(16 * it + n, nwin - 1);
+                const int a = gq * CS + 2 * (wi / PW) * YS + 2 * (wi % PW);
+                bool dup = false;
+                for (int i = 0; i < ns && !dup; ++i) dup = seen[i][0] == a;
+                if (dup) continue;
+                seen[ns][0] = a;
+                seen[ns++][1] = 0;
+                ++load[a & 63];
+                ++load[(a + 1) & 63];
+            }
+            total += *std::max_element(load, load + 64);
+        }
+    return total;
+}
+
+// Row stride YS and channel stride CS of the Winograd ring (>= XL and YL YS,
+// multiples of the DMA width and of 2 for the float2 patch reads) with the
+// fewest patch-read bank cycles, then the smallest; cached per shape (the
+// launch planner evaluates every band height)
+std::pair<int, int> wino_strides(int PW, int nwin, int XL, int YL, int VEC) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int, int, int>, std::pair<int, int>> cache;
+    const auto key = std::make_tuple(PW, nwin, XL, YL, VEC);
+    std::lock_guard<std::mutex> lock(mu);
+    const auto f = cache.find(key);
+    if (f != cache.end()) return f->second;
+    const int step = std::max(VEC, 2);
+    const int ys0 = (XL + step - 1) / step * step;
+    int best = INT_MAX, bys = ys0, bcs = YL * ys0;
+    for (int ys = ys0; ys < ys0 + 32; ys += step) {
+        const int cs0 = (YL * ys + VEC - 1) / VEC * VEC;
+        for (int cs = cs0; cs < cs0 + 64; cs += VEC) {
+            const int c = wino_read_cycles(PW, nwin, ys, cs);
+            if (c < best || (c == best && cs < bcs)) {
+                best = c;
+                bys = ys;
+                bcs = cs;
+            }
+        }
+    }
+    return cache[key] = {bys, bcs};
+}
+
 // Ring geometry of the Winograd forward: a y band of pyb pooled rows, XL =
-// 2 PW + 2 input columns (the last window's 4-wide patch), rows and channels
-// padded to the DMA width; z chunks until the grid has ~2048 blocks
+// 2 PW + 2 input columns (the last window's 4-wide patch), row / channel
+// strides from wino_strides; z chunks until the grid has ~2048 blocks
 template <int CPG, int VEC>
 RingGeom make_wino_geom(const rt_conv_layer* L, int B, int G, int pyb) {
     RingGeom r{};
@@ -1184,9 +1252,10 @@ RingGeom make_wino_geom(const rt_conv_layer* L, int B, int G, int pyb) {
     g.ZL = 4;
     g.YL = 2 * pyb + 2;
     g.XL = 2 * g.PW + 2;
-    g.YS = (g.XL + 3) / 4 * 4;
+    const std::pair<int, int> st = wino_strides(g.PW, std::min(pyb, g.PH) * g.PW, g.XL, g.YL, VEC);
+    g.YS = st.first;
     g.ZS = 0;
-    g.CS = g.YL * g.YS;
+    g.CS = st.second;
     r.SLOT = CPG * g.CS;
     r.npiece = (r.SLOT + 64 * VEC - 1) / (64 * VEC);
     r.nyb = (g.PH + pyb - 1) / pyb;
@@ -1228,20 +1297,29 @@ int launch_fwd_wino(const rt_conv_layer* L, int32_t B, const float* x, const int
     const bool vec4 = cpg == 4 && G == 1 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     const int nth = G == 4 ? 256 : 512;
+    // the band height with the fewest item rounds per pooled row over all
+    // bands (a band's 16-window items go round-robin to the NW waves, so 9
+    // items on 8 waves cost 2 rounds), plus ~1/4 round per band for its
+    // halo planes and prologue; ties go to the taller band
     auto plan = [&](auto cpg_c, auto vec_c, int& pyb_out) -> RingGeom {
         constexpr int CPG_ = decltype(cpg_c)::value, VEC_ = decltype(vec_c)::value;
         RingGeom best{};
         pyb_out = 0;
+        const int nw = nth / 64;
         const int ph = (L->in_dims[1] - 2 + 2 * L->pool_pad[1] - 2) / 2 + 1;
+        double best_cost = 1e30;
         for (int pyb = 1; pyb <= ph; ++pyb) {
             const RingGeom rg = make_wino_geom<CPG_, VEC_>(L, B, G, pyb);
             const size_t lds = ((size_t)kRing * rg.SLOT + wino_u_floats<CPG_>()) * sizeof(float);
             const int items = (pyb * rg.g.PW + 15) / 16;
-            if (lds > 160 * 1024 || (rg.npiece + nth / 64 - 1) / (nth / 64) > 16 || items > 2 * (nth / 64) ||
-                rg.g.W < VEC_)
-                break;
-            best = rg;
-            pyb_out = pyb;
+            if (lds > 160 * 1024 || (rg.npiece + nw - 1) / nw > 16 || items > 2 * nw || rg.g.W < VEC_) break;
+            double cost = 0.25 * rg.nyb;
+            for (int y = 0; y < ph; y += pyb) cost += ((std::min(pyb, ph - y) * rg.g.PW + 15) / 16 + nw - 1) / nw;
+            if (cost <= best_cost) {
+                best_cost = cost;
+                best = rg;
+                pyb_out = pyb;
+            }
         }
         return best;
     };
@@ -2824,10 +2902,14 @@ __global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
     const int wz0 = max(q0 - 1, 0), wz1 = min(q1, g.PD);
     const int nz = wz1 - wz0;
     const int plane = g.PH * g.PW;
-    const int chw = nz * plane;  // LDS floats per channel
+    const int chw = nz * plane;  // window values per channel
+    // LDS channel stride = 16 (mod 32): the two channels of a 32-lane group
+    // read 16 consecutive windows each on disjoint banks (ds_read_b32: bank =
+    // dword mod 32), the argmax bytes likewise
+    const int chs = chw + ((48 - chw % 32) & 31);
     float* us = xs;
     float* dps = xs + wino_dg_u_floats<CPG>();
-    uint8_t* ams = reinterpret_cast<uint8_t*>(dps + COG * chw);
+    uint8_t* ams = reinterpret_cast<uint8_t*>(dps + COG * chs);
     {
         // 8 loads in flight per thread (a load-then-store loop waited out one
         // HBM round trip per element)
@@ -2850,8 +2932,9 @@ __global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
             for (int u = 0; u < U; ++u) {
                 const int i = i0 + u * NTH;
                 if (i < tot) {
-                    dps[i] = v[u];
-                    ams[i] = (uint8_t)a[u];
+                    const int c = i / chw, li = i + c * (chs - chw);
+                    dps[li] = v[u];
+                    ams[li] = (uint8_t)a[u];
                 }
             }
         }
@@ -2889,11 +2972,10 @@ __global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const float a0 = sy[j], a1 = sy[16 + j], a2 = sy[32 + j];
-                float* q = us + (j * 64 + lane) * 4 * NS + s;
-                q[0] = a0;
-                q[NS] = 0.5f * ((a0 + a1) + a2);
-                q[2 * NS] = 0.5f * ((a0 - a1) + a2);
-                q[3 * NS] = a2;
+                us[wino_u_index<NS>(j, lane, s)] = a0;
+                us[wino_u_index<NS>(j, lane, NS + s)] = 0.5f * ((a0 + a1) + a2);
+                us[wino_u_index<NS>(j, lane, 2 * NS + s)] = 0.5f * ((a0 - a1) + a2);
+                us[wino_u_index<NS>(j, lane, 3 * NS + s)] = a2;
             }
         }
     }
@@ -2927,7 +3009,7 @@ __global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
                         const int wz = qz - 1 + (wq >> 2), wy = qy - 1 + ((wq >> 1) & 1), wx = qx - 1 + (wq & 1);
                         const bool in = (unsigned)wz < (unsigned)g.PD & (unsigned)wy < (unsigned)g.PH &
                                         (unsigned)wx < (unsigned)g.PW;
-                        const int li = base + c * chw + ((in ? wz : wz0) - wz0) * plane + (in ? wy : 0) * g.PW +
+                        const int li = base + c * chs + ((in ? wz : wz0) - wz0) * plane + (in ? wy : 0) * g.PW +
                                        (in ? wx : 0);
                         wv[wq] = dps[li];
                         wa[wq] = in ? (int)ams[li] : 0;
@@ -3022,11 +3104,10 @@ __global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
                     if (cc < 8) {
                         const int kx = cc >> 2, xy = cc & 3, xx = 2 * h + kx;
                         const int j = xy * 4 + xx, jv = xy * 2 + kx;
-                        const float* ub = us + (j * 64 + lane) * 4 * NS;
                         float uc[4 * NS];
 #pragma unroll
                         for (int q = 0; q < NS; ++q) {
-                            const float4 u4 = *reinterpret_cast<const float4*>(ub + 4 * q);
+                            const float4 u4 = *reinterpret_cast<const float4*>(us + wino_u_index<NS>(j, lane, 4 * q));
                             uc[4 * q] = u4.x;
                             uc[4 * q + 1] = u4.y;
                             uc[4 * q + 2] = u4.z;
@@ -3080,7 +3161,7 @@ int launch_dgrad_wino_k(const rt_conv_layer* L, int32_t B, const float* w, const
     // else the whole LDS; then split further while the grid has fewer than
     // ~2048 blocks
     const size_t per_row = (size_t)CPG * P.g.PH * P.g.PW * 5;
-    const size_t u_bytes = (size_t)wino_dg_u_floats<CPG>() * 4 + 64;
+    const size_t u_bytes = (size_t)wino_dg_u_floats<CPG>() * 4 + 64 + (size_t)CPG * 31 * 5;  // + stride padding
     auto rows_fit = [&](size_t lds) { return lds > u_bytes ? (int)((lds - u_bytes) / per_row) - 1 : 0; };
     int zmax = rows_fit(80 * 1024);
     if (zmax < 2) zmax = rows_fit(160 * 1024);
@@ -3089,7 +3170,7 @@ int launch_dgrad_wino_k(const rt_conv_layer* L, int32_t B, const float* w, const
     while (chunks < P.QD && (int64_t)B * P.G * chunks < 2048) ++chunks;
     const int zc = (P.QD + chunks - 1) / chunks;
     P.ZC = zc;
-    const size_t lds = (size_t)wino_dg_u_floats<CPG>() * 4 + (size_t)(zc + 1) * per_row + 16;
+    const size_t lds = (size_t)wino_dg_u_floats<CPG>() * 4 + (size_t)(zc + 1) * per_row + (size_t)CPG * 31 * 5 + 16;
     static bool attr = false;
     if (!attr) {
         if (const int rc_lds = allow_big_lds(&k_dgrad_wino<CPG, NTH>)) return rc_lds;

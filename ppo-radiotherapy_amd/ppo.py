@@ -418,7 +418,7 @@ class PPOTrainer:
         in compact vision mode)."""
         if not self.compact_obs:
             return self._b_obs[mb]
-        return self.env.render(self._b_dose[mb], self._b_pose[mb], self._b_tumour[mb])
+        return self.env.render(self._b_dose, self._b_pose[mb], self._b_tumour[mb], rows=mb)
 
     def _loss_backward(self, mb, adv_mean=None, adv_std=None, weight: float = 1.0, zero: bool = True):
         cfg = self.cfg

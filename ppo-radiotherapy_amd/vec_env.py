@@ -226,15 +226,17 @@ class RadiotherapyVecEnv:
         _lib.check(self._L.rt_env_get_state(self._h, _lib.ptr(pose_out), None, _lib.ptr(tumour_out),
                                             _lib.stream_handle()), "rt_env_get_state")
 
-    def render(self, dose: torch.Tensor, pose: torch.Tensor, tumour: torch.Tensor) -> torch.Tensor:
+    def render(self, dose: torch.Tensor, pose: torch.Tensor, tumour: torch.Tensor, rows=None) -> torch.Tensor:
         """Observations [M, 4, D, H, W] of M stored states, bit-identical to
         what the env emitted in them: a render handle is loaded with the states
         and reset with an all-zero mask, which re-emits every observation (the
         same k_dense_vis / k_finish code).  The returned tensor is the render
-        handle's buffer, valid until the next render call."""
+        handle's buffer, valid until the next render call.  rows: dose is a
+        store [R, V] and the states' doses are its rows `rows`, gathered
+        straight into the render handle (no intermediate [M, V] copy)."""
         if self.visionless:
             raise ValueError("render() is for vision observations")
-        M = int(dose.shape[0])
+        M = int(rows.numel()) if rows is not None else int(dose.shape[0])
         r = getattr(self, "_renderer", None)
         if r is None or r.num_envs < M:
             if r is not None:
@@ -243,7 +245,13 @@ class RadiotherapyVecEnv:
             self._renderer = r
             self._render_mask = torch.zeros(M, dtype=torch.uint8, device=self.device)
         V = int(np.prod(self.grid))
-        r.dose().reshape(r.num_envs, V)[:M].copy_(dose.reshape(M, V))
+        dst = r.dose().reshape(r.num_envs, V)[:M]
+        if rows is not None and dst.is_contiguous():
+            torch.index_select(dose.reshape(-1, V), 0, rows, out=dst)
+        elif rows is not None:
+            dst.copy_(dose.reshape(-1, V)[rows])
+        else:
+            dst.copy_(dose.reshape(M, V))
         p = torch.zeros((r.num_envs, 6), dtype=torch.float64, device=self.device)
         p[:M] = pose
         p[M:, 4] = 1.0

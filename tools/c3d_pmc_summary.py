@@ -18,7 +18,7 @@ for sub in ("a", "b", "c"):
     for f in glob.glob(os.path.join(d, sub, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if "conv" not in k:
+            if "conv" not in k and "dgrad" not in k:
                 continue
             k = re.sub(r"\(anonymous namespace\)::", "", k).split("(")[0]
             vals.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
