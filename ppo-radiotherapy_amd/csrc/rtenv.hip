@@ -1484,6 +1484,18 @@ __global__ __launch_bounds__(1024) void k_rollout_policy(RolloutArgs A) {
     const int n_steps = A.R.n_steps;
     if (lane0 == 0) RT_STAMP(e0, 13);
     for (int t = 0; t < n_steps; ++t) {
+        // Issue priority rotated over the 4 waves each SIMD holds (waves w,
+        // w + 4, w + 8, w + 12 of the block share one): with the hardware's
+        // oldest-first pick the youngest wave of a SIMD fell 27 % behind the
+        // oldest over a rollout, and the launch ended on it with its SIMD
+        // mostly idle (tools/trace_env.py --persistent --dump: life 675 /
+        // 720 / 783 / 859 us by age rank, 24 steps)
+        switch (((w >> 2) + t) & 3) {
+            case 0: __builtin_amdgcn_s_setprio(0); break;
+            case 1: __builtin_amdgcn_s_setprio(1); break;
+            case 2: __builtin_amdgcn_s_setprio(2); break;
+            default: __builtin_amdgcn_s_setprio(3); break;
+        }
         // Re-derive the loop-invariant inputs (kernel arguments through a
         // laundered kernarg pointer, lane, env, LDS bases) every step: hoisted
         // out of the loop they stay live across the whole step body and push
