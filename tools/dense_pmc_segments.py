@@ -13,7 +13,7 @@ import os
 import statistics
 import sys
 
-SEGMENTS = [("warm", 32), ("value_window_20_steps", 40), ("stagger_preroll", 200), ("steady_window_64_steps", 128)]
+SEGMENTS = [("stagger_preroll", 200), ("warm", 10), ("value_window_20_steps", 40), ("steady_window_64_steps", 128)]
 ENVS, LUNG_VOXELS = 2048, 96160  # per launch; lung voxels of the 64^3 resampled reference mask
 
 

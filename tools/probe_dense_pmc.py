@@ -1,10 +1,11 @@
 """PMC companion of bench.py's dense pipelined rollout (4096 envs x 64^3, two
-env groups, k_dense_persist over 2048 envs per launch).  k_dense_persist
-dispatch order: 32 (16 warm steps) + 40 (a 20-step window, bench.py's value
-shape) + 200 (stagger pre-roll: 100 one-step calls) + 128 (a 64-step window
-with staggered episode phases: ~1 % of the envs reset every step, each reset
-zeroing its dose row inside k_dense_persist).  tools/dense_pmc_segments.py
-splits the counter rows by that order."""
+env groups, k_dense_persist over 2048 envs per launch), in bench.py's order:
+200 launches of the stagger pre-roll (100 one-step calls; every env's episode
+clock offset by e % 100), 10 (5 warm steps), 40 (a 20-step window, the
+`value` shape) and 128 (a 64-step window, the steady-state shape).  With the
+phases staggered ~1 % of the envs reset every step in both windows, each
+reset zeroing its dose row inside k_dense_persist.
+tools/dense_pmc_segments.py splits the counter rows by that order."""
 import os
 import sys
 
@@ -26,15 +27,13 @@ env = RadiotherapyVecEnv(N, library=lib, device=dev, seed=1)
 env.set_rollout_groups(2)
 torch.manual_seed(1)
 agent = PPO((9,), (6,), 64).to(dev)
-cfg = bench.trainer_cfg(bench.argparse.Namespace(num_steps=64, num_minibatches=8, update_epochs=10, micro_batch=0))
+cfg = bench.trainer_cfg(bench.argparse.Namespace(num_steps=64, num_minibatches=8, update_epochs=10, micro_batch=0,
+                                                 update_precision="f32", vision=False))
 tr = PPOTrainer(cfg, env, agent, dev, 0, 1, torch.Generator(device=dev).manual_seed(1))
 tr.reset()
-bench.run_steps(tr, 16)
+bench.stagger_phases(tr, env, dev)
+bench.run_steps(tr, 5)
 bench.run_steps(tr, 20)
-e_idx = torch.arange(N, device=dev)
-for k in range(100):
-    env.reset(options={"mask": (e_idx % 100) == k})
-    tr.rollout_steps(k % 64, 1)
 bench.run_steps(tr, 64)
 torch.cuda.synchronize()
 env.close()
