@@ -165,6 +165,14 @@ int rt_env_set_pose(rt_env* env, const double* pose_d /* f64[N,6] */, void* stre
  * (dose, pose, tumour) state -- the vision rollout's compact storage (SURVEY
  * §8 f-3). */
 int rt_env_set_tumours(rt_env* env, const int32_t* tumour_d, void* stream);
+/* Vision handles: the NEXT rt_env_reset re-emits the observation of each env
+ * e < n_rows that the reset leaves unselected (mask 0) from row rows_d[e] of
+ * a dose store (f32, C order, row stride store_stride >= the padded volume,
+ * 16-B aligned) instead of from its own dose row, which stays as it was; the
+ * reset clears the setting.  The re-render of stored states without copying
+ * their doses into the handle first (the trainer's compact vision storage). */
+int rt_env_set_render_source(rt_env* env, const float* dose_store_d, int64_t store_stride,
+                             const int64_t* rows_d /* i64[n_rows] */, int32_t n_rows);
 int rt_env_num_envs(const rt_env* env);
 
 /* Live kernel timing.  rt_env_kernel_timing(env, K) creates HIP events for

@@ -32,7 +32,7 @@ RT_ERRORS = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EDEVICE", -4:
 # every symbol include/rtenv.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "rt_env_config_default", "rt_env_create", "rt_env_destroy", "rt_env_reset", "rt_env_step",
-    "rt_env_set_next_tumours", "rt_env_reseed", "rt_env_dose", "rt_env_dose_index", "rt_env_get_state", "rt_env_set_pose", "rt_env_set_tumours",
+    "rt_env_set_next_tumours", "rt_env_reseed", "rt_env_dose", "rt_env_dose_index", "rt_env_get_state", "rt_env_set_pose", "rt_env_set_tumours", "rt_env_set_render_source",
     "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_env_beam_list", "rt_probe_random_rmw", "rt_probe_stream", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
@@ -156,6 +156,7 @@ def load(build_if_missing: bool = True):
         "rt_env_get_state": ([vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_env_set_pose": ([vp, vp, vp], ctypes.c_int),
         "rt_env_set_tumours": ([vp, vp, vp], ctypes.c_int),
+        "rt_env_set_render_source": ([vp, vp, ctypes.c_int64, vp, ctypes.c_int32], ctypes.c_int),
         "rt_env_num_envs": ([vp], ctypes.c_int),
         "rt_env_kernel_timing": ([vp, i32], ctypes.c_int),
         "rt_env_kernel_timing_read": ([vp, ctypes.POINTER(f64), ctypes.POINTER(i32)], ctypes.c_int),

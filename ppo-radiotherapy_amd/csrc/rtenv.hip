@@ -878,6 +878,13 @@ __device__ __forceinline__ void store4(float* row, int v0, int V, bool aligned4,
 struct DenseVisParams {
     DenseParams d;
     float* obs;   // [N][4][V]
+    // render source (rt_env_set_render_source): a NOOP env e < src_n re-emits
+    // its observation from src + src_rows[e] * src_stride (C order) instead
+    // of its own dose row
+    const float* src;
+    const int64_t* src_rows;
+    int64_t src_stride;
+    int32_t src_n;
 };
 
 // ---------------------------------------------------------------------------
@@ -894,6 +901,8 @@ __global__ __launch_bounds__(256) void k_dense_vis(DenseVisParams PV) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int mode = P.st.setup[e].mode;
     float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
+    if (mode == MODE_NOOP && e < PV.src_n)  // (the source rows are 16-B aligned: checked by the setter)
+        d4 = reinterpret_cast<float4*>(const_cast<float*>(PV.src) + PV.src_rows[e] * PV.src_stride);
     const int nvec = P.G.Vpad >> 2;
     const int V = P.G.V;
     const bool al4 = (V & 3) == 0;
@@ -1869,6 +1878,11 @@ struct rt_env {
     // groups on two library streams; events fork, hand the k_dense turn from
     // one group to the other, join
     int rollout_groups = 2;  // DESIGN.md §3 "Pipelined dense rollout"
+    // rt_env_set_render_source: read by the next reset's k_dense_vis, then cleared
+    const float* render_src = nullptr;
+    const int64_t* render_rows = nullptr;
+    int64_t render_stride = 0;
+    int32_t render_n = 0;
     hipStream_t pipe[kMaxRolloutGroups] = {};
     hipEvent_t pev[1 + 2 * kMaxRolloutGroups] = {};  // fork, dense[G], join[G]
     std::vector<void*> allocs;
@@ -2388,7 +2402,7 @@ int launch_dense(rt_env* env, int e0, int n, float* obs, int persist_bpc, hipStr
         }
         RT_LAUNCH_CHECK("k_dense");
     } else {
-        DenseVisParams dv{dp, obs};
+        DenseVisParams dv{dp, obs, env->render_src, env->render_rows, env->render_stride, env->render_n};
         hipLaunchKernelGGL(k_dense_vis, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dv);
         RT_LAUNCH_CHECK("k_dense_vis");
     }
@@ -2427,8 +2441,27 @@ static int launch_step(rt_env* env, bool reset_call, const float* actions, const
 int rt_env_reset(rt_env* env, const uint8_t* mask_d, const int32_t* tumour_ids_d, float* obs_d,
                  void* stream) {
     if (!env || !obs_d) return fail(RT_EINVAL, "NULL argument");
-    return launch_step(env, true, nullptr, mask_d, tumour_ids_d, obs_d, nullptr, nullptr, nullptr,
-                       as_stream(stream));
+    const int rc = launch_step(env, true, nullptr, mask_d, tumour_ids_d, obs_d, nullptr, nullptr, nullptr,
+                               as_stream(stream));
+    env->render_src = nullptr;  // one reset only
+    env->render_rows = nullptr;
+    env->render_n = 0;
+    return rc;
+}
+
+int rt_env_set_render_source(rt_env* env, const float* dose_store_d, int64_t store_stride, const int64_t* rows_d,
+                             int32_t n_rows) {
+    if (!env) return fail(RT_EINVAL, "NULL argument");
+    if (env->visionless) return fail(RT_EINVAL, "rt_env_set_render_source: vision handles only");
+    if (n_rows < 0 || n_rows > env->N) return fail(RT_EINVAL, "rt_env_set_render_source: n_rows outside [0, N]");
+    if (n_rows > 0 && (!dose_store_d || !rows_d)) return fail(RT_EINVAL, "NULL argument");
+    if (store_stride < env->G.Vpad || store_stride % 4 || (reinterpret_cast<uintptr_t>(dose_store_d) & 15))
+        return fail(RT_EINVAL, "rt_env_set_render_source: rows must be >= the padded volume, 16-B aligned");
+    env->render_src = dose_store_d;
+    env->render_rows = rows_d;
+    env->render_stride = store_stride;
+    env->render_n = n_rows;
+    return RT_OK;
 }
 
 int rt_env_step(rt_env* env, const float* actions_d, float* obs_d, float* reward_d,

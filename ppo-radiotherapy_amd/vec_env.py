@@ -245,13 +245,19 @@ class RadiotherapyVecEnv:
             self._renderer = r
             self._render_mask = torch.zeros(M, dtype=torch.uint8, device=self.device)
         V = int(np.prod(self.grid))
-        dst = r.dose().reshape(r.num_envs, V)[:M]
-        if rows is not None and dst.is_contiguous():
-            torch.index_select(dose.reshape(-1, V), 0, rows, out=dst)
-        elif rows is not None:
-            dst.copy_(dose.reshape(-1, V)[rows])
+        stride = ctypes_int64()
+        self._L.rt_env_dose(r._h, stride)
+        store = dose.reshape(-1, V) if rows is not None else None
+        if (rows is not None and store.is_contiguous() and store.dtype == torch.float32 and V >= stride.value
+                and V % 4 == 0 and store.data_ptr() % 16 == 0):
+            # the reset below reads the states' doses straight from the store
+            ridx = rows.to(torch.int64).contiguous()
+            self._render_rows = ridx  # alive until the reset has run
+            _lib.check(self._L.rt_env_set_render_source(r._h, _lib.ptr(store), V, _lib.ptr(ridx), M),
+                       "rt_env_set_render_source")
         else:
-            dst.copy_(dose.reshape(M, V))
+            dst = r.dose().reshape(r.num_envs, V)[:M]
+            dst.copy_(store[rows] if rows is not None else dose.reshape(M, V))
         p = torch.zeros((r.num_envs, 6), dtype=torch.float64, device=self.device)
         p[:M] = pose
         p[M:, 4] = 1.0
