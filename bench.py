@@ -930,7 +930,10 @@ def main():
                                    f"(BASELINE configs[{1 if world == 1 else 2}])") + (" env-only" if a.env_only else ""),
                       "envs_per_gpu": a.envs, "global_envs": total_envs, "grid": list(grid),
                       "num_steps": T, "num_minibatches": a.num_minibatches, "update_epochs": a.update_epochs,
-                      "parallelism": f"dp{world}"},
+                      "parallelism": f"dp{world}",
+                      "episode_phases": ("lockstep (all envs reset together)" if (a.vision or a.env_only) else
+                                         "staggered: env e's episode clock offset by e mod 100, ~1 % of the envs "
+                                         "autoreset (and zero their dose rows) in every timed step")},
            "env_only_kernel_steps_per_s": total_envs / (env_ms * 1e-3)}
     out.update(upd)
     if steady is not None:
