@@ -168,3 +168,39 @@ def test_compact_trainer_sees_stored_observations():
         env.close()
     assert torch.equal(out[True][0], out[False][0])
     torch.testing.assert_close(out[True][1], out[False][1], rtol=0, atol=0)
+
+
+def test_render_from_store_rows_matches_copied_doses():
+    """The trainer's render path (rt_env_set_render_source: the reset reads
+    each state's dose straight from its row of the dose store) re-emits the
+    same observations bit for bit as rendering from copied doses.  32^3 grid:
+    rows of exactly the padded volume, so the store path is taken."""
+    from ppo_radiotherapy_amd import assets
+    from ppo_radiotherapy_amd.vec_env import RadiotherapyVecEnv
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    lib = assets.synthetic_library((32, 32, 32), 50, 0)
+    N = 8
+    env = RadiotherapyVecEnv(N, visionless=False, library=lib, seed=3)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    V = int(np.prod(env.grid))
+    ds, ps, ks = [], [], []
+    for t in range(6):
+        d = torch.empty((N, V), device="cuda")
+        p = torch.empty((N, 6), dtype=torch.float64, device="cuda")
+        k = torch.empty(N, dtype=torch.int32, device="cuda")
+        env.snapshot(d, p, k)
+        ds.append(d)
+        ps.append(p)
+        ks.append(k)
+        env.step(torch.rand((N, 6), device="cuda", generator=g) * 2 - 1)
+    store, pose, tum = torch.cat(ds), torch.cat(ps), torch.cat(ks)
+    rows = torch.randperm(store.shape[0], device="cuda", generator=g)[:13]
+    via_store = env.render(store, pose[rows], tum[rows], rows=rows).clone()
+    assert getattr(env, "_render_rows", None) is not None  # the store path ran
+    copied = env.render(store[rows], pose[rows], tum[rows])
+    torch.cuda.synchronize()
+    assert torch.equal(via_store, copied)
+    env.close()
