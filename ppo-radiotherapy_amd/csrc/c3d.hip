@@ -1994,15 +1994,18 @@ struct WgradRingParams {
 // patch rows as 8-B pairs from the even x below the patch start -- 2/3 of the
 // LDS cycles, but 27 selects and no packed FMAs -- measured slower: conv1
 // 2.45 -> 2.94 ms)
-// ring geometry of the sparse weight gradient: conv1 keeps the ring's (YS,
-// CS, SLOT) = (4, 8, 2) residues (mod 32 dwords; conflict-free for its lane
-// map), the 16-channel stages take (2, 4, 0) -- a bank model of their
-// half-waves (4 output channels x 8 input channels for groups = 2) over random
-// argmax variants: 1.54 vs 2.0 mean multiplicity (PMC: 48 % conflict cycles)
-template <int CIN, int PYB, int NT>
+// ring geometry of the sparse weight gradient: conv1 and (round 4) the
+// groups = 2 stage keep the ring's (YS, CS, SLOT) = (4, 8, 2) residues (mod
+// 32 dwords): with a half-wave of 8 output channels x 4 input channels (the
+// lane map below) the 4 channels x 8 argmax offsets (dz, dy, dx) of a patch
+// read land on 32 distinct banks whatever the argmax bytes; groups = 4 (8
+// output channels of two groups per half-wave, 8 input channels) cannot be
+// made conflict-free and keeps (2, 4, 0) -- a bank model over random argmax
+// variants: 1.54 vs 2.0 mean multiplicity
+template <int CIN, int G, int PYB, int NT>
 RingGeom make_sparse_geom(const rt_conv_layer* L, int B) {
     RingGeom r = make_ring_geom<CIN, PYB, 1, 2>(L, B, NT);
-    if constexpr (CIN == 16) {
+    if constexpr (CIN == 16 && G != 2) {
         Geom& g = r.g;
         g.YS = round_mod(g.XL, 2);
         g.CS = round_mod(g.YL * g.YS, 4);
@@ -2013,6 +2016,23 @@ RingGeom make_sparse_geom(const rt_conv_layer* L, int B) {
 }
 
 constexpr int kWgSparseMaxG = 4;  // a band row holds <= NT * 4 (channel, window) entries
+
+// thread li of a window's L = 16 x CPG threads -> (output channel, in-group
+// input channel).  groups = 2 (round 4): a 32-lane half-wave holds 8 output
+// channels of one group x 4 input channels (li bits: cig & 3, co & 7,
+// cig >> 2, co >> 3), so its patch reads are conflict-free on the (4, 8, 2)
+// ring (was 4 x 8, 35 % conflict cycles); otherwise co-major
+template <int CIN, int G>
+__device__ __forceinline__ void sparse_lane(int li, int& co, int& cig) {
+    constexpr int CPG = CIN / G;
+    if constexpr (CIN == 16 && G == 2) {
+        co = ((li >> 6) & 1) * 8 + ((li >> 2) & 7);
+        cig = ((li >> 5) & 1) * 4 + (li & 3);
+    } else {
+        co = li / CPG;
+        cig = li - co * CPG;
+    }
+}
 
 template <int CIN, int G, int PYB, int NT>
 __global__ __launch_bounds__(NT) void k_conv_wgrad_sparse(WgradRingParams P) {
@@ -2027,7 +2047,8 @@ __global__ __launch_bounds__(NT) void k_conv_wgrad_sparse(WgradRingParams P) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int sidx = tid / L, li = tid - sidx * L;
-    const int co = li / CPG, cig = li - co * CPG;
+    int co, cig;
+    sparse_lane<CIN, G>(li, co, cig);
     const int ci = (co / (CO / G)) * CPG + cig;
     const int py0 = blockIdx.x * PYB;
     const int y0 = 2 * py0 - g.ph, x0 = -g.pw;
@@ -2167,7 +2188,9 @@ __global__ __launch_bounds__(NT) void k_conv_wgrad_sparse(WgradRingParams P) {
         float v = R[i];
 #pragma unroll
         for (int k = 1; k < NS; ++k) v += R[k * L * 28 + i];
-        const int co2 = l2 / CPG, cig2 = l2 - co2 * CPG, ci2 = (co2 / (CO / G)) * CPG + cig2;
+        int co2, cig2;
+        sparse_lane<CIN, G>(l2, co2, cig2);
+        const int ci2 = (co2 / (CO / G)) * CPG + cig2;
         if (q < 27)
             out[co2 * NCOL + ci2 * 27 + q] = v;
         else if (cig2 == 0)
@@ -2812,7 +2835,7 @@ constexpr int kWgradRingBlocks = 512;  // sparse weight-gradient grid (256 / 102
 template <int CIN, int G, int PYB, int NT>
 int launch_wgrad_sparse_k(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* dP,
                           const uint8_t* am, float* dw, float* db, float* ws, int64_t ws_floats, hipStream_t st) {
-    const RingGeom rg = make_sparse_geom<CIN, PYB, NT>(L, B);
+    const RingGeom rg = make_sparse_geom<CIN, G, PYB, NT>(L, B);
     const int nwin = PYB * rg.g.PW;
     const size_t lds = std::max((size_t)kRing * rg.SLOT * 4 + (size_t)2 * CO * nwin * 5, (size_t)NT * 28 * 4);
     if (lds > 160 * 1024 || CO * nwin > NT * kWgSparseMaxG ||
