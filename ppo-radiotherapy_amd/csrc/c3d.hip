@@ -920,8 +920,12 @@ struct WinoParams {
     int32_t pyb;          // pooled rows per y band
 };
 
+// conv3 (4 channels per group, 4 outputs): 3 waves per SIMD (<= 168 VGPRs,
+// no spills; left free the compiler took 150 VGPRs + 44 AGPRs = 2 waves) --
+// its 256-thread blocks are small enough for 3 per CU
 template <int CPG, int COG, int VEC, int NTH, bool TRAIN>
-__global__ __launch_bounds__(NTH) void k_conv_wino(WinoParams P) {
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(CPG == 4 && COG == 4 ? 3 : 1)))
+void k_conv_wino(WinoParams P) {
     extern __shared__ float xs[];
     constexpr int NW = NTH / 64;
     constexpr int NS = CPG / 4;  // channel quads (MFMA k-steps) per xi
