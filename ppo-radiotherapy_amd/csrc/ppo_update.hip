@@ -740,11 +740,18 @@ __device__ __forceinline__ void mf_wave(MfmaLds& S, const GradParams& P, int pai
     __syncthreads();
     float* out = P.ws + (size_t)blockIdx.x * PSTRIDE;
     const int tid = threadIdx.x;
-    for (int q = tid; q < kW2Region; q += MT) {
-        float v = R[q];
+    // float4 per lane (O_AW2, O_CW2 and PSTRIDE are multiples of 4), stored
+    // write-through: the 32 KB of W2 partials per block leave the XCD's L2
+    // during the kernel instead of as dirty lines the boundary to the
+    // reduction writes back (MI355X_MICROARCH.md, boundary / publish-large)
+    static_assert(O_AW2 % 4 == 0 && O_CW2 % 4 == 0 && PSTRIDE % 4 == 0, "float4 partial rows");
+    const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc(out, 0, PSTRIDE * 4, 0x00020000);
+    for (int q = 4 * tid; q < kW2Region; q += 4 * MT) {
+        f4 v = *reinterpret_cast<const f4*>(R + q);
 #pragma unroll
-        for (int pp = 1; pp < NPAIR; ++pp) v += R[pp * kW2Region + q];
-        out[(q < H * H ? O_AW2 : O_CW2 - H * H) + q] = v;
+        for (int pp = 1; pp < NPAIR; ++pp) v += *reinterpret_cast<const f4*>(R + pp * kW2Region + q);
+        const int o = (q < H * H ? O_AW2 : O_CW2 - H * H) + q;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), wsrd, 4 * o, 0, 16);  // aux 16: sc1
     }
     if (lane == 0) RT_STAMP(tw, 4);
     __syncthreads();
@@ -1098,6 +1105,16 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
     }
     sq = wave_sum(sq);
     const AdamParams& A = Q.A;
+    // the block's own Adam state is loaded before the arrival wait (it does
+    // not depend on the clip coefficient): one dependent load round fewer
+    const bool upd = ok && p < NP;
+    const int64_t i = upd ? Q.flat_off[t] + (p - kTensorOff[t]) : 0;
+    float m0 = 0.0f, v0 = 0.0f, w0 = 0.0f;
+    if (upd) {
+        m0 = A.m[i];
+        v0 = A.v[i];
+        w0 = A.param[i];
+    }
     if (lane == 0) {
         __hip_atomic_store(const_cast<float*>(A.norm_part) + blockIdx.x, sq, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -1118,22 +1135,32 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
     }
     arrived = __shfl(arrived, 0, 64);
     float tn = 0.0f;
-    if (A.max_norm > 0.0f)
-        for (int k = lane; k < A.n_part; k += 64)
-            tn += __hip_atomic_load(const_cast<float*>(A.norm_part) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (A.max_norm > 0.0f) {
+        // all of a lane's partials in flight at once, summed in k_adam's order
+        static_assert(kReduceBlocks <= 4 * 64, "norm partial loads");
+        float np[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = lane + 64 * u;
+            np[u] = k < A.n_part ? __hip_atomic_load(const_cast<float*>(A.norm_part) + k, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tn += np[u];
+    }
     tn = wave_sum(tn);
     float coef = A.max_norm > 0.0f ? fminf(A.max_norm / (sqrtf(tn) + 1e-6f), 1.0f) : 1.0f;
     if (!arrived) coef = __int_as_float(0x7fc00000);  // NaN: a lost arrival is never a silent step
-    if (!ok || p >= NP) return;
-    const int64_t i = Q.flat_off[t] + (p - kTensorOff[t]);
+    if (!upd) return;
     const float g = a * coef;
     A.grad[i] = g;
-    float m = A.m[i];
+    float m = m0;
     m = m + A.lerp_w * (g - m);                   // exp_avg.lerp_(grad, 1 - beta1)
-    float v = A.v[i] * A.beta2;                   // exp_avg_sq.mul_(beta2)
+    float v = v0 * A.beta2;                       // exp_avg_sq.mul_(beta2)
     v = v + A.one_minus_beta2 * g * g;            //   .addcmul_(grad, grad, 1 - beta2)
     const float denom = sqrtf(v) / A.bc2_sqrt + A.eps;
-    A.param[i] = A.param[i] + A.step_size * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
+    A.param[i] = w0 + A.step_size * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
     A.m[i] = m;
     A.v[i] = v;
 }
