@@ -41,8 +41,10 @@
 extern "C" {
 #endif
 
-#define RTENV_ABI_VERSION 3  /* 2: rt_env_config.struct_size (first member); 3: rt_adam_step grad_div,
-                                rt_env_set_dense_handoff removed */
+#define RTENV_ABI_VERSION 4  /* 2: rt_env_config.struct_size (first member); 3: rt_adam_step grad_div,
+                                rt_env_set_dense_handoff removed; 4: arithmetic per call
+                                (rt_ppo_hparams.precision, rt_conv_layer.precision) instead of the
+                                process-wide rt_ppo_/rt_conv_set_precision */
 
 enum {
     RT_OK = 0,
@@ -333,6 +335,7 @@ typedef struct rt_ppo_hparams {
     float max_grad_norm; /* <= 0: no clipping */
     double adam_beta1, adam_beta2;
     float adam_eps;
+    int32_t precision;   /* RT_PPO_PREC_*: the two 64x64 layer products (below); 0 = f32 */
 } rt_ppo_hparams;
 
 /* Floats of workspace rt_ppo_grad / rt_ppo_update need for a minibatch. */
@@ -340,18 +343,15 @@ int64_t rt_ppo_workspace_floats(int32_t minibatch_size);
 /* Parameters of the fused agent (10,061). */
 int32_t rt_ppo_num_params(void);
 
-/* Arithmetic of the two 64x64 layer products in rt_ppo_grad / rt_ppo_update
- * (forward and data gradient; process-wide, initially RT_PPO_PREC=f32|bf16x3
- * from the environment, else f32).  F32: exact f32 MFMA, the reference's
- * arithmetic (torch f32 Linear, TF32 off: train.py:200-238 via networks.py).
- * BF16X3: each f32 operand split into bf16 hi + lo, products hi*hi + hi*lo +
- * lo*hi accumulated in f32 (relative error <= ~2^-15 per product); the same
- * f64-autograd gates hold (tests/test_gpu_trainer.py).  RT_EINVAL on another
- * value. */
+/* rt_ppo_hparams.precision: arithmetic of the two 64x64 layer products in
+ * rt_ppo_grad / rt_ppo_update (forward and data gradient), per call.  F32 (0):
+ * exact f32 MFMA, the reference's arithmetic (torch f32 Linear, TF32 off:
+ * train.py:200-238 via networks.py).  BF16X3: each f32 operand split into bf16
+ * hi + lo, products hi*hi + hi*lo + lo*hi accumulated in f32 (relative error
+ * <= ~2^-15 per product); the same f64-autograd gates hold
+ * (tests/test_gpu_trainer.py).  RT_EINVAL on another value. */
 #define RT_PPO_PREC_F32 0
 #define RT_PPO_PREC_BF16X3 1
-int rt_ppo_set_precision(int32_t prec);
-int32_t rt_ppo_get_precision(void);
 
 /* Gradient of the minibatch PPO loss (train.py:200-238: clipped surrogate,
  * [clipped] value loss * vf_coef, - ent_coef * entropy; advantages normalised
@@ -419,24 +419,21 @@ typedef struct rt_conv_layer {
     int32_t groups;       /* 1 (cin 4); 1, 2 or 4 (cin 16) */
     int32_t in_dims[3];   /* D, H, W of the input */
     int32_t pool_pad[3];  /* 0 or 1 per axis */
+    int32_t precision;    /* RT_CONV_PREC_* of this call's forward products (below); 0 = f32 */
 } rt_conv_layer;
 
-/* Arithmetic of the C3D forward products (process-wide, initially
- * RT_CONV_PREC=f32|bf16x3 from the environment, else f32; PPOTrainer sets it
- * per rollout step and update when its config names conv_precision).  F32:
- * f32 throughout (the reference's torch Conv3d in f32; its cuDNN default
- * allowed TF32) -- conv1's forward in the Winograd form F(2x2x2, 3x3x3) (f32
- * transforms, products on exact f32 MFMA), the other stages direct on f32
- * MFMA.
- * BF16X3: in conv1's forward kernel and the grouped stages' (groups 2 and 4)
- * forward and data-gradient kernels, every operand split into bf16 hi + lo
- * (round to nearest even), products hi*hi + hi*lo + lo*hi accumulated in f32
- * (relative error <= ~2^-15 per product).  The weight gradients stay f32.
+/* rt_conv_layer.precision: arithmetic of the C3D forward products, per call
+ * (the vision trainer's conv_precision config key).  F32 (0): f32 throughout
+ * (the reference's torch Conv3d in f32; its cuDNN default allowed TF32) --
+ * the forward of every stage and the grouped stages' data gradient in the
+ * Winograd form F(2x2x2, 3x3x3) (f32 transforms, products on exact f32 MFMA).
+ * BF16X3: conv1's forward and the grouped stages' (groups 2 and 4) forward and
+ * data gradient as the direct ring kernels, every operand split into bf16 hi
+ * + lo (round to nearest even), products hi*hi + hi*lo + lo*hi accumulated in
+ * f32 (relative error <= ~2^-15 per product).  The weight gradients stay f32.
  * RT_EINVAL on another value. */
 #define RT_CONV_PREC_F32 0
 #define RT_CONV_PREC_BF16X3 1
-int rt_conv_set_precision(int32_t prec);
-int32_t rt_conv_get_precision(void);
 
 /* Pooled output dims of a stage. */
 int rt_conv_out_dims(const rt_conv_layer* layer, int32_t* out_dims);
@@ -454,6 +451,15 @@ int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* layer, int32_t batch
 int rt_conv_relu_pool_wgrad(const rt_conv_layer* layer, int32_t batch, const float* x_d, const int64_t* rows_d,
                             const float* dy_d, const uint8_t* argmax_d, float* dw_d, float* db_d,
                             float* workspace_d, int64_t workspace_floats, void* stream);
+
+/* Measurement hook (bench.py c3d_mfma): the v_mfma_f32_16x16x4_f32
+ * wave-instructions (2,048 FLOP each) the f32 Winograd kernel of a pass
+ * issues for `batch` samples -- pass 0: rt_conv_relu_pool_fwd, 1:
+ * rt_conv_relu_pool_dgrad -- zero-padded rows and channel lanes included, i.e.
+ * what rocprofv3's SQ_INSTS_MFMA counts; 0 when that pass runs no Winograd
+ * kernel (bf16x3, the dense or tile fallbacks), -1 on a bad argument.  Host
+ * only (the launch planner's arithmetic; nothing is launched). */
+int64_t rt_conv_mfma_count(const rt_conv_layer* layer, int32_t batch, int32_t pass);
 
 /* Gradient w.r.t. the stage input (cin 16 stages): dx [B][16][D][H][W]. */
 int rt_conv_relu_pool_dgrad(const rt_conv_layer* layer, int32_t batch, const float* w_d, const float* dy_d,

@@ -23,8 +23,8 @@ INFO_NAMES = {
 }
 INFO_W = 20
 STEP_DENSE, STEP_INCREMENTAL = 0, 1
-PPO_PREC = {"f32": 0, "bf16x3": 1}  # RT_PPO_PREC_* (rt_ppo_set_precision)
-CONV_PREC = {"f32": 0, "bf16x3": 1}  # RT_CONV_PREC_* (rt_conv_set_precision)
+PPO_PREC = {"f32": 0, "bf16x3": 1}  # RT_PPO_PREC_* (rt_ppo_hparams.precision)
+CONV_PREC = {"f32": 0, "bf16x3": 1}  # RT_CONV_PREC_* (rt_conv_layer.precision)
 
 RT_ELIMIT = -5
 RT_ERRORS = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EDEVICE", -4: "RT_ELAUNCH", -5: "RT_ELIMIT"}
@@ -37,9 +37,9 @@ EXPORTS = [
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
     "rt_debug_beam", "rt_debug_pose", "rt_env_beam_list", "rt_probe_random_rmw", "rt_probe_stream", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
     "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups",
-    "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_set_precision", "rt_ppo_get_precision", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
+    "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
     "rt_ppo_shuffle", "rt_ppo_shuffle_epochs", "rt_ppo_adv_stats", "rt_ppo_adv_sums", "rt_ppo_adv_finalize",
-    "rt_conv_set_precision", "rt_conv_get_precision", "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad",
+    "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad", "rt_conv_mfma_count",
     "rt_conv_relu_pool_dgrad",
     "rt_last_error", "rt_abi_version",
 ]
@@ -49,7 +49,7 @@ class RtError(RuntimeError):
     pass
 
 
-ABI_VERSION = 3  # RTENV_ABI_VERSION of include/rtenv.h
+ABI_VERSION = 4  # RTENV_ABI_VERSION of include/rtenv.h
 
 
 class RtEnvConfig(ctypes.Structure):
@@ -101,6 +101,7 @@ class RtPpoHparams(ctypes.Structure):
         ("adam_beta1", ctypes.c_double),
         ("adam_beta2", ctypes.c_double),
         ("adam_eps", ctypes.c_float),
+        ("precision", ctypes.c_int32),
     ]
 
 
@@ -118,7 +119,7 @@ class RtPolicyRollout(ctypes.Structure):
 
 class RtConvLayer(ctypes.Structure):
     _fields_ = [("cin", ctypes.c_int32), ("groups", ctypes.c_int32), ("in_dims", ctypes.c_int32 * 3),
-                ("pool_pad", ctypes.c_int32 * 3)]
+                ("pool_pad", ctypes.c_int32 * 3), ("precision", ctypes.c_int32)]
 
 
 _lib = None
@@ -175,8 +176,6 @@ def load(build_if_missing: bool = True):
         "rt_env_set_rollout_groups": ([vp, i32], ctypes.c_int),
         "rt_ppo_workspace_floats": ([i32], i64),
         "rt_ppo_num_params": ([], i32),
-        "rt_ppo_set_precision": ([i32], ctypes.c_int),
-        "rt_ppo_get_precision": ([], i32),
         "rt_ppo_grad": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, vp,
                          ctypes.POINTER(RtPpoHparams), vp, i64, vp, vp, vp], ctypes.c_int),
         "rt_adam_step": ([i64, vp, vp, vp, vp, i64, f64, ctypes.POINTER(RtPpoHparams), i32, vp, vp], ctypes.c_int),
@@ -188,11 +187,10 @@ def load(build_if_missing: bool = True):
         "rt_ppo_adv_stats": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
         "rt_ppo_adv_sums": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
         "rt_ppo_adv_finalize": ([vp, i64, i32, vp, vp], ctypes.c_int),
-        "rt_conv_set_precision": ([i32], ctypes.c_int),
-        "rt_conv_get_precision": ([], i32),
         "rt_conv_out_dims": ([ctypes.POINTER(RtConvLayer), ctypes.POINTER(i32)], ctypes.c_int),
         "rt_conv_relu_pool_fwd": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "rt_conv_wgrad_workspace_floats": ([ctypes.POINTER(RtConvLayer), i32], i64),
+        "rt_conv_mfma_count": ([ctypes.POINTER(RtConvLayer), i32, i32], i64),
         "rt_conv_relu_pool_wgrad": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp, vp, vp, i64, vp],
                                     ctypes.c_int),
         "rt_conv_relu_pool_dgrad": ([ctypes.POINTER(RtConvLayer), i32, vp, vp, vp, vp, vp], ctypes.c_int),

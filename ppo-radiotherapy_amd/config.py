@@ -34,12 +34,11 @@ DEFAULTS = {
     # resume_from: such a file -> the run continues at its iteration + 1
     "save_checkpoint": True,
     "resume_from": None,
-    # arithmetic (include/rtenv.h): the fused visionless update's 64x64 layer
-    # products, "f32" (the reference's) or "bf16x3"; the C3D forward products,
-    # "f32" / "bf16x3" set per rollout step and update by the trainer, or None:
-    # the library's process-wide setting (RT_CONV_PREC at load, else f32)
+    # arithmetic (include/rtenv.h, passed per call): the fused visionless
+    # update's 64x64 layer products and the C3D forward products, "f32" (the
+    # reference's) or "bf16x3"
     "update_precision": "f32",
-    "conv_precision": None,
+    "conv_precision": "f32",
 }
 
 

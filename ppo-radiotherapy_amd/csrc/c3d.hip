@@ -1220,8 +1220,8 @@ std::pair<int, int> wino_strides(int PW, int nwin, int XL, int YL, int VEC) {
     const int ys0 = (XL + step - 1) / step * step;
     int best = INT_MAX, bys = ys0, bcs = YL * ys0;
     for (int ys = ys0; ys < ys0 + 32; ys += step) {
-        const int cs0 = (YL * ys + VEC - 1) / VEC * VEC;
-        for (int cs = cs0; cs < cs0 + 64; cs += VEC) {
+        const int cs0 = (YL * ys + step - 1) / step * step;  // even: the float2 patch reads stay 8-B aligned
+        for (int cs = cs0; cs < cs0 + 64; cs += step) {
             const int c = wino_read_cycles(PW, nwin, ys, cs);
             if (c < best || (c == best && cs < bcs)) {
                 best = c;
@@ -1294,8 +1294,17 @@ int launch_wino_k(const RingGeom& rg, int pyb, int G, int32_t B, const float* x,
 // widest y band (up to 2 item rounds per pooled row) whose ring + U fit the
 // 160 KiB of one block per CU; RT_ELIMIT when none does or the stage is not
 // one of those (groups 1 with 16 channels: the direct ring kernel)
+// MFMA wave-instructions of a Winograd forward launch: every pooled z row of
+// every (sample, group) runs each band's 16-window items, 64 NS MFMAs each
+int64_t wino_fwd_mfma(const RingGeom& rg, int pyb, int B, int G, int NS) {
+    int64_t items = 0;
+    for (int y = 0; y < rg.g.PH; y += pyb) items += (std::min(pyb, rg.g.PH - y) * rg.g.PW + 15) / 16;
+    return (int64_t)B * G * rg.g.PD * items * 64 * NS;
+}
+
+// mfma_count (measurement hook): set to the launch's MFMA count, nothing launched
 int launch_fwd_wino(const rt_conv_layer* L, int32_t B, const float* x, const int64_t* rows, const float* w,
-                    const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+                    const float* bias, float* y, uint8_t* amax, hipStream_t st, int64_t* mfma_count = nullptr) {
     const int G = L->groups, cpg = L->cin / G;
     if (!(L->cin == 4 || G == 2 || G == 4) || (int64_t)B * G > 65535) return RT_ELIMIT;
     const bool vec4 = cpg == 4 && G == 1 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
@@ -1328,18 +1337,26 @@ int launch_fwd_wino(const rt_conv_layer* L, int32_t B, const float* x, const int
         return best;
     };
     int pyb = 0;
+    auto counted = [&](const RingGeom& rg, int ns) {
+        *mfma_count = wino_fwd_mfma(rg, pyb, B, G, ns);
+        return RT_OK;
+    };
     if (cpg == 4 && G == 1) {
         if (vec4) {
             const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{}, pyb);
+            if (pyb && mfma_count) return counted(rg, 1);
             if (pyb) return launch_wino_k<4, 16, 4, 512>(rg, pyb, 1, B, x, rows, w, bias, y, amax, st);
         }
         const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, pyb);
+        if (pyb && mfma_count) return counted(rg, 1);
         if (pyb) return launch_wino_k<4, 16, 1, 512>(rg, pyb, 1, B, x, rows, w, bias, y, amax, st);
     } else if (G == 2) {
         const RingGeom rg = plan(std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{}, pyb);
+        if (pyb && mfma_count) return counted(rg, 2);
         if (pyb) return launch_wino_k<8, 8, 1, 512>(rg, pyb, 2, B, x, rows, w, bias, y, amax, st);
     } else {
         const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, pyb);
+        if (pyb && mfma_count) return counted(rg, 1);
         if (pyb) return launch_wino_k<4, 4, 1, 256>(rg, pyb, 4, B, x, rows, w, bias, y, amax, st);
     }
     return RT_ELIMIT;
@@ -1395,13 +1412,9 @@ RingGeom make_ring_geom_zs(const rt_conv_layer* L, int B) {
     return r;
 }
 
-// Arithmetic of the C3D forward products (rt_conv_set_precision; initial
-// value from RT_CONV_PREC=f32|bf16x3, default f32): bf16x3 in conv1's ring
-// kernel and the grouped stages' z-shift kernels
-int g_conv_prec = [] {
-    const char* e = std::getenv("RT_CONV_PREC");
-    return (e && std::strcmp(e, "bf16x3") == 0) ? 1 : 0;
-}();
+// Arithmetic of the C3D forward products: per call, rt_conv_layer.precision
+// (bf16x3 in conv1's ring kernel and the grouped stages' z-shift kernels)
+bool layer_bf16x3(const rt_conv_layer* L) { return L->precision == RT_CONV_PREC_BF16X3; }
 
 // ring slots of the z-shift kernel: the G + 2 planes of a tile + the next G
 template <int G>
@@ -1655,8 +1668,8 @@ int launch_ring_zs_kp(const RingGeom& rg, int32_t B, const float* x, const int64
 
 template <int G, int PYB>
 int launch_ring_zs_k(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
-                     const float* bias, float* y, uint8_t* amax, hipStream_t st) {
-    if (g_conv_prec == 1) return launch_ring_zs_kp<G, PYB, true>(rg, B, x, rows, w, bias, y, amax, st);
+                     const float* bias, float* y, uint8_t* amax, bool bf, hipStream_t st) {
+    if (bf) return launch_ring_zs_kp<G, PYB, true>(rg, B, x, rows, w, bias, y, amax, st);
     return launch_ring_zs_kp<G, PYB, false>(rg, B, x, rows, w, bias, y, amax, st);
 }
 
@@ -1669,20 +1682,20 @@ int launch_ring_zs(const rt_conv_layer* L, int32_t B, const float* x, const int6
                (rg.npiece + 7) / 8 <= ring_max_pieces<CO / G, 1>();
     };
     RingGeom rg = make_ring_geom_zs<G, 8>(L, B);
-    if (fits(rg)) return launch_ring_zs_k<G, 8>(rg, B, x, rows, w, bias, y, amax, st);
+    if (fits(rg)) return launch_ring_zs_k<G, 8>(rg, B, x, rows, w, bias, y, amax, layer_bf16x3(L), st);
     rg = make_ring_geom_zs<G, 4>(L, B);
-    if (fits(rg)) return launch_ring_zs_k<G, 4>(rg, B, x, rows, w, bias, y, amax, st);
+    if (fits(rg)) return launch_ring_zs_k<G, 4>(rg, B, x, rows, w, bias, y, amax, layer_bf16x3(L), st);
     rg = make_ring_geom_zs<G, 2>(L, B);
-    if (fits(rg)) return launch_ring_zs_k<G, 2>(rg, B, x, rows, w, bias, y, amax, st);
+    if (fits(rg)) return launch_ring_zs_k<G, 2>(rg, B, x, rows, w, bias, y, amax, layer_bf16x3(L), st);
     return RT_ELIMIT;
 }
 
 
 template <int CIN, int G, int PYB, int VEC, int NTH>
 int launch_ring_p(const RingGeom& rg, int32_t B, const float* x, const int64_t* rows, const float* w,
-                  const float* bias, float* y, uint8_t* amax, hipStream_t st) {
+                  const float* bias, float* y, uint8_t* amax, bool bf, hipStream_t st) {
     if constexpr (CIN == 4 && G == 1)
-        if (g_conv_prec == 1) return launch_ring<CIN, G, PYB, VEC, NTH, true>(rg, B, x, rows, w, bias, y, amax, st);
+        if (bf) return launch_ring<CIN, G, PYB, VEC, NTH, true>(rg, B, x, rows, w, bias, y, amax, st);
     return launch_ring<CIN, G, PYB, VEC, NTH, false>(rg, B, x, rows, w, bias, y, amax, st);
 }
 
@@ -1708,20 +1721,20 @@ int launch_fwd_ring(const rt_conv_layer* L, int32_t B, const float* x, const int
         if constexpr (CIN == 4) {
             if (vec4) {
                 RingGeom rg = make_ring_geom<CIN, PY_BIG, 4>(L, B, NTH);
-                if (fits(rg, 4, budget)) return launch_ring_p<CIN, G, PY_BIG, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+                if (fits(rg, 4, budget)) return launch_ring_p<CIN, G, PY_BIG, 4, NTH>(rg, B, x, rows, w, bias, y, amax, layer_bf16x3(L), st);
                 rg = make_ring_geom<CIN, PY_BIG / 2, 4>(L, B, NTH);
                 if (fits(rg, 4, budget))
-                    return launch_ring_p<CIN, G, PY_BIG / 2, 4, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+                    return launch_ring_p<CIN, G, PY_BIG / 2, 4, NTH>(rg, B, x, rows, w, bias, y, amax, layer_bf16x3(L), st);
             }
         }
         RingGeom rg = make_ring_geom<CIN, PY_BIG, 1>(L, B, NTH);
-        if (fits(rg, 1, budget)) return launch_ring_p<CIN, G, PY_BIG, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+        if (fits(rg, 1, budget)) return launch_ring_p<CIN, G, PY_BIG, 1, NTH>(rg, B, x, rows, w, bias, y, amax, layer_bf16x3(L), st);
         rg = make_ring_geom<CIN, PY_BIG / 2, 1>(L, B, NTH);
-        if (fits(rg, 1, budget)) return launch_ring_p<CIN, G, PY_BIG / 2, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+        if (fits(rg, 1, budget)) return launch_ring_p<CIN, G, PY_BIG / 2, 1, NTH>(rg, B, x, rows, w, bias, y, amax, layer_bf16x3(L), st);
         if constexpr (PY_BIG / 4 >= 1) {
             rg = make_ring_geom<CIN, PY_BIG / 4, 1>(L, B, NTH);
             if (fits(rg, 1, budget))
-                return launch_ring_p<CIN, G, PY_BIG / 4, 1, NTH>(rg, B, x, rows, w, bias, y, amax, st);
+                return launch_ring_p<CIN, G, PY_BIG / 4, 1, NTH>(rg, B, x, rows, w, bias, y, amax, layer_bf16x3(L), st);
         }
         if (CIN != 4) break;  // the 16-channel stages already tried the whole 160 KiB
     }
@@ -2769,8 +2782,8 @@ int launch_dgrad_ring_zs_kp(const RingGeom& rg, int32_t B, const float* w, const
 
 template <int G, int PYB>
 int launch_dgrad_ring_zs_k(const RingGeom& rg, int32_t B, const float* w, const float* dP, const uint8_t* am,
-                           float* dx, hipStream_t st) {
-    if (g_conv_prec == 1) return launch_dgrad_ring_zs_kp<G, PYB, true>(rg, B, w, dP, am, dx, st);
+                           float* dx, bool bf, hipStream_t st) {
+    if (bf) return launch_dgrad_ring_zs_kp<G, PYB, true>(rg, B, w, dP, am, dx, st);
     return launch_dgrad_ring_zs_kp<G, PYB, false>(rg, B, w, dP, am, dx, st);
 }
 
@@ -2782,11 +2795,11 @@ int launch_dgrad_ring_zs(const rt_conv_layer* L, int32_t B, const float* w, cons
                CO / G * (pyb + 1) * (2 * rg.g.XT + 1) <= kDgMaxWin * 512;
     };
     RingGeom rg = make_dgrad_ring_geom_zs<G, 8>(L, B);
-    if (fits(rg, 8)) return launch_dgrad_ring_zs_k<G, 8>(rg, B, w, dP, am, dx, st);
+    if (fits(rg, 8)) return launch_dgrad_ring_zs_k<G, 8>(rg, B, w, dP, am, dx, layer_bf16x3(L), st);
     rg = make_dgrad_ring_geom_zs<G, 4>(L, B);
-    if (fits(rg, 4)) return launch_dgrad_ring_zs_k<G, 4>(rg, B, w, dP, am, dx, st);
+    if (fits(rg, 4)) return launch_dgrad_ring_zs_k<G, 4>(rg, B, w, dP, am, dx, layer_bf16x3(L), st);
     rg = make_dgrad_ring_geom_zs<G, 2>(L, B);
-    if (fits(rg, 2)) return launch_dgrad_ring_zs_k<G, 2>(rg, B, w, dP, am, dx, st);
+    if (fits(rg, 2)) return launch_dgrad_ring_zs_k<G, 2>(rg, B, w, dP, am, dx, layer_bf16x3(L), st);
     return RT_ELIMIT;
 }
 
@@ -3172,7 +3185,7 @@ __global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
 
 template <int CPG, int NTH>
 int launch_dgrad_wino_k(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am,
-                        float* dx, hipStream_t st) {
+                        float* dx, hipStream_t st, int64_t* mfma_count) {
     WinoDgradParams P{};
     P.g = make_geom<1, 1>(L);
     P.w = w;
@@ -3197,6 +3210,10 @@ int launch_dgrad_wino_k(const rt_conv_layer* L, int32_t B, const float* w, const
     while (chunks < P.QD && (int64_t)B * P.G * chunks < 2048) ++chunks;
     const int zc = (P.QD + chunks - 1) / chunks;
     P.ZC = zc;
+    if (mfma_count) {  // every tile row of every (sample, group): its 16-tile items, 64 NS MFMAs each
+        *mfma_count = (int64_t)B * P.G * P.QD * ((P.QH * P.QW + 15) / 16) * 64 * (CPG / 4);
+        return RT_OK;
+    }
     const size_t lds = (size_t)wino_dg_u_floats<CPG>() * 4 + (size_t)(zc + 1) * per_row + (size_t)CPG * 31 * 5 + 16;
     static bool attr = false;
     if (!attr) {
@@ -3211,10 +3228,10 @@ int launch_dgrad_wino_k(const rt_conv_layer* L, int32_t B, const float* w, const
 }
 
 int launch_dgrad_wino(const rt_conv_layer* L, int32_t B, const float* w, const float* dP, const uint8_t* am,
-                      float* dx, hipStream_t st) {
+                      float* dx, hipStream_t st, int64_t* mfma_count = nullptr) {
     if ((int64_t)B * L->groups > 65535) return RT_ELIMIT;
-    if (L->groups == 2) return launch_dgrad_wino_k<8, 256>(L, B, w, dP, am, dx, st);
-    if (L->groups == 4) return launch_dgrad_wino_k<4, 256>(L, B, w, dP, am, dx, st);
+    if (L->groups == 2) return launch_dgrad_wino_k<8, 256>(L, B, w, dP, am, dx, st, mfma_count);
+    if (L->groups == 4) return launch_dgrad_wino_k<4, 256>(L, B, w, dP, am, dx, st, mfma_count);
     return RT_ELIMIT;
 }
 
@@ -3224,7 +3241,7 @@ bool bad_layer(const rt_conv_layer* L) {
         return true;
     for (int a = 0; a < 3; ++a)
         if (L->in_dims[a] < 4 || L->pool_pad[a] < 0 || L->pool_pad[a] > 1) return true;
-    return false;
+    return L->precision != RT_CONV_PREC_F32 && L->precision != RT_CONV_PREC_BF16X3;
 }
 
 // the one-region-per-block tile kernels (before the plane rings; kept as the
@@ -3259,15 +3276,6 @@ extern "C" int rt_conv_out_dims(const rt_conv_layer* L, int32_t* out_dims) {
     return RT_OK;
 }
 
-extern "C" int rt_conv_set_precision(int32_t prec) {
-    if (prec != RT_CONV_PREC_F32 && prec != RT_CONV_PREC_BF16X3)
-        return rt_internal_fail(RT_EINVAL, "rt_conv_set_precision: unknown precision");
-    g_conv_prec = prec == RT_CONV_PREC_BF16X3 ? 1 : 0;
-    return RT_OK;
-}
-
-extern "C" int32_t rt_conv_get_precision(void) { return g_conv_prec ? RT_CONV_PREC_BF16X3 : RT_CONV_PREC_F32; }
-
 extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, const float* x_d, const int64_t* rows_d,
                                      const float* w_d, const float* b_d, float* y_d, uint8_t* argmax_d,
                                      void* stream) {
@@ -3277,7 +3285,7 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     int rc = RT_ELIMIT;
     // f32: the Winograd kernel (conv1 and the grouped stages); bf16x3, groups 1
     // with 16 channels and planes too wide for its ring: the direct kernels
-    if (g_conv_prec == 0) rc = launch_fwd_wino(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+    if (!layer_bf16x3(L)) rc = launch_fwd_wino(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
     if (rc != RT_ELIMIT) return rc;
     if (L->cin == 4) {
         rc = launch_fwd_ring<4, 1>(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
@@ -3297,6 +3305,23 @@ extern "C" int rt_conv_relu_pool_fwd(const rt_conv_layer* L, int32_t batch, cons
     // (its region is 2 pooled z rows x 4 or 2 pooled y rows, so it fits where
     // the 6-plane ring does not)
     return fwd_tile(L, batch, x_d, rows_d, w_d, b_d, y_d, argmax_d, st);
+}
+
+extern "C" int64_t rt_conv_mfma_count(const rt_conv_layer* L, int32_t batch, int32_t pass) {
+    if (bad_layer(L) || batch < 1 || batch > 65535 || (pass != 0 && pass != 1)) return -1;
+    if (layer_bf16x3(L)) return 0;
+    int64_t n = 0;
+    int rc;
+    if (pass == 0) {
+        // the forward's input alignment decides conv1's DMA width (same count either way)
+        rc = launch_fwd_wino(L, batch, reinterpret_cast<const float*>(16), nullptr, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, &n);
+    } else {
+        const bool pad0 = L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0;
+        if (!pad0 || L->groups == 1 || L->cin != 16) return 0;
+        rc = launch_dgrad_wino(L, batch, nullptr, nullptr, nullptr, nullptr, nullptr, &n);
+    }
+    return rc == RT_OK ? n : 0;
 }
 
 extern "C" int64_t rt_conv_wgrad_workspace_floats(const rt_conv_layer* L, int32_t batch) {
@@ -3336,7 +3361,7 @@ extern "C" int rt_conv_relu_pool_dgrad(const rt_conv_layer* L, int32_t batch, co
     // (bf16x3 products, or where the Winograd kernel's LDS does not fit); then
     // the dense ring kernel; the tile kernel for padded pools
     const bool pad0 = L->pool_pad[0] == 0 && L->pool_pad[1] == 0 && L->pool_pad[2] == 0;
-    if (pad0 && L->groups > 1 && g_conv_prec == 0) {
+    if (pad0 && L->groups > 1 && !layer_bf16x3(L)) {
         const int rc = launch_dgrad_wino(L, batch, w_d, dy_d, argmax_d, dx_d, st);
         if (rc != RT_ELIMIT) return rc;
     }

@@ -26,6 +26,8 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "rtenv.h"
@@ -1054,7 +1056,10 @@ __global__ __launch_bounds__(256) void k_adam(AdamParams P) {
 // updates in the last block and lost to the two kernels).  The
 // kReduceBlocks blocks (16 waves, 4 KiB LDS each: >= 2 fit a CU) are all
 // resident at once on an otherwise idle stream, so the wait completes; a
-// bounded poll that runs out (hardware fault) poisons the step with NaN.
+// bounded poll that runs out leaves the state untouched and raises a sticky
+// host-visible flag (every later rt_ppo_* call returns RT_EDEVICE).
+// rt_ppo_update checks once per device that the occupancy query admits the
+// whole grid at once and otherwise runs k_ppo_reduce + k_adam instead.
 // The counter (the workspace's last norm slot) is zeroed by rt_ppo_update
 // before its first launch; launch i waits for (i + 1) * kReduceBlocks.
 struct ReduceAdamParams {
@@ -1063,6 +1068,7 @@ struct ReduceAdamParams {
     int32_t flat_off[13];  // flat index of each tensor's first element (params_d[t] - flat_param_d)
     unsigned* counter;
     unsigned target;
+    int* fault;  // host-mapped sticky flag (reduce_adam_fault)
 };
 
 __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
@@ -1134,6 +1140,9 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
         }
     }
     arrived = __shfl(arrived, 0, 64);
+    // the partial loads below stay behind the poll (sc1 loads of sc1-stored
+    // bytes behind a matched poll: MI355X_MICROARCH.md hand-off table, row 1)
+    asm volatile("" ::: "memory");
     float tn = 0.0f;
     if (A.max_norm > 0.0f) {
         // all of a lane's partials in flight at once, summed in k_adam's order
@@ -1150,8 +1159,13 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
         for (int u = 0; u < 4; ++u) tn += np[u];
     }
     tn = wave_sum(tn);
-    float coef = A.max_norm > 0.0f ? fminf(A.max_norm / (sqrtf(tn) + 1e-6f), 1.0f) : 1.0f;
-    if (!arrived) coef = __int_as_float(0x7fc00000);  // NaN: a lost arrival is never a silent step
+    const float coef = A.max_norm > 0.0f ? fminf(A.max_norm / (sqrtf(tn) + 1e-6f), 1.0f) : 1.0f;
+    if (!arrived) {
+        // a lost arrival (the grid was not co-resident): no parameter, moment or
+        // gradient is written, and the host sees RT_EDEVICE on its next call
+        if (lane == 0) __hip_atomic_store(Q.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     if (!upd) return;
     const float g = a * coef;
     A.grad[i] = g;
@@ -1303,13 +1317,6 @@ __global__ __launch_bounds__(256) void k_adv_finalize(const double* sums, int64_
     stats[2 * i + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
 }
 
-// Arithmetic of k_ppo_grad_mfma's two 64x64 products (rt_ppo_set_precision;
-// the initial value from RT_PPO_PREC=f32|bf16x3, default f32)
-int g_ppo_prec = [] {
-    const char* e = std::getenv("RT_PPO_PREC");
-    return (e && std::strcmp(e, "bf16x3") == 0) ? kPrecBf16x3 : kPrecF32;
-}();
-
 ReduceParams reduce_params(float* const* grads_d, int32_t mb, const rt_ppo_hparams* hp, float* ws_d,
                            int64_t ws_floats, float* stats_d, float* accum_d) {
     ReduceParams R{};
@@ -1349,7 +1356,8 @@ int ppo_grad_launch(const float* const* params_d, float* const* grads_d, const r
     G.clip_vloss = hp->clip_vloss;
     G.vf_coef = hp->vf_coef;
     G.ws = ws_d;
-    if (g_ppo_prec == kPrecBf16x3)
+    // arithmetic of the two 64x64 products: per call (rt_ppo_hparams.precision)
+    if (hp->precision == RT_PPO_PREC_BF16X3)
         hipLaunchKernelGGL(k_ppo_grad_mfma<kPrecBf16x3>, dim3(nblk), dim3(MT), 0, st, G);
     else
         hipLaunchKernelGGL(k_ppo_grad_mfma<kPrecF32>, dim3(nblk), dim3(MT), 0, st, G);
@@ -1398,6 +1406,45 @@ int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step,
     return RT_OK;
 }
 
+// The sticky fault flag of k_ppo_reduce_adam: one host-mapped int per
+// process (a lost grid arrival on any device sets it); nullptr when the host
+// allocation failed (rt_ppo_update then runs the two-kernel form)
+int* reduce_adam_fault() {
+    static int* flag = [] {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return (int*)nullptr;
+        *static_cast<volatile int*>(p) = 0;
+        return static_cast<int*>(p);
+    }();
+    return flag;
+}
+
+bool reduce_adam_faulted() {
+    int* f = reduce_adam_fault();
+    return f && *static_cast<volatile int*>(f) != 0;
+}
+
+// k_ppo_reduce_adam's grid arrival needs all kReduceBlocks blocks resident at
+// once: checked per device against the occupancy query (cached)
+bool reduce_adam_coresident() {
+    static std::mutex mu;
+    static std::map<int, bool> ok;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    std::lock_guard<std::mutex> lock(mu);
+    const auto f = ok.find(dev);
+    if (f != ok.end()) return f->second;
+    int per_cu = 0, cus = 0;
+    const bool good = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ppo_reduce_adam, 1024, 0) == hipSuccess &&
+                      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                      (int64_t)per_cu * cus >= kReduceBlocks;
+    return ok[dev] = good;
+}
+
+bool bad_prec(const rt_ppo_hparams* hp) {
+    return hp->precision != RT_PPO_PREC_F32 && hp->precision != RT_PPO_PREC_BF16X3;
+}
+
 bool bad13(const void* const* p) {
     if (!p) return true;
     for (int i = 0; i < 13; ++i)
@@ -1419,25 +1466,16 @@ extern "C" int64_t rt_ppo_workspace_floats(int32_t minibatch_size) {
 
 extern "C" int32_t rt_ppo_num_params(void) { return NP; }
 
-extern "C" int rt_ppo_set_precision(int32_t prec) {
-    if (prec != RT_PPO_PREC_F32 && prec != RT_PPO_PREC_BF16X3)
-        return rt_internal_fail(RT_EINVAL, "rt_ppo_set_precision: unknown precision");
-    g_ppo_prec = prec == RT_PPO_PREC_BF16X3 ? kPrecBf16x3 : kPrecF32;
-    return RT_OK;
-}
-
-extern "C" int32_t rt_ppo_get_precision(void) {
-    return g_ppo_prec == kPrecBf16x3 ? RT_PPO_PREC_BF16X3 : RT_PPO_PREC_F32;
-}
-
 extern "C" int rt_ppo_grad(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
                            const int64_t* mb_idx_d, int32_t mb_size, const float* adv_stats_d,
                            const rt_ppo_hparams* hp, float* workspace_d, int64_t workspace_floats, float* stats_d,
                            float* stats_accum_d, void* stream) {
     if (bad13(reinterpret_cast<const void* const*>(params_d)) || bad13(reinterpret_cast<const void* const*>(grads_d)) ||
-        bad_batch(batch) || !mb_idx_d || mb_size < 1 || !hp || !workspace_d || !stats_d ||
+        bad_batch(batch) || !mb_idx_d || mb_size < 1 || !hp || bad_prec(hp) || !workspace_d || !stats_d ||
         (hp->norm_adv && !adv_stats_d))
         return rt_internal_fail(RT_EINVAL, "rt_ppo_grad: bad argument");
+    if (reduce_adam_faulted())
+        return rt_internal_fail(RT_EDEVICE, "rt_ppo_grad: an earlier rt_ppo_update lost its grid arrival");
     return ppo_grad_launch(params_d, grads_d, batch, mb_idx_d, mb_size, adv_stats_d, hp, workspace_d,
                            workspace_floats, stats_d, stats_accum_d, reinterpret_cast<hipStream_t>(stream));
 }
@@ -1448,6 +1486,8 @@ extern "C" int rt_adam_step(int64_t n, float* param_d, float* grad_d, float* exp
     if (n < 1 || !param_d || !grad_d || !exp_avg_d || !exp_avg_sq_d || step < 1 || !hp || !workspace_d ||
         grad_div < 1 || grad_div > (1 << 24))
         return rt_internal_fail(RT_EINVAL, "rt_adam_step: bad argument");
+    if (reduce_adam_faulted())
+        return rt_internal_fail(RT_EDEVICE, "rt_adam_step: an earlier rt_ppo_update lost its grid arrival");
     return adam_launch(n, param_d, grad_d, exp_avg_d, exp_avg_sq_d, step, lr, hp, workspace_d, false,
                        (float)grad_div, reinterpret_cast<hipStream_t>(stream));
 }
@@ -1461,10 +1501,29 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
     if (bad13(reinterpret_cast<const void* const*>(params_d)) || bad13(reinterpret_cast<const void* const*>(grads_d)) ||
         bad_batch(batch) || !perm_d || mb_size < 1 || n_minibatches < 1 || !hp || !flat_param_d || !flat_grad_d ||
         !exp_avg_d || !exp_avg_sq_d || n_flat != NP || step0 < 1 || !workspace_d || !stats_d ||
-        (hp->norm_adv && !adv_stats_d) || mb_size > batch->batch_size)
+        (hp->norm_adv && !adv_stats_d) || mb_size > batch->batch_size || bad_prec(hp))
         return rt_internal_fail(RT_EINVAL, "rt_ppo_update: bad argument");
+    if (reduce_adam_faulted())
+        return rt_internal_fail(RT_EDEVICE, "rt_ppo_update: an earlier call lost its grid arrival");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     float* norm_part = workspace_d + (workspace_floats - kNormSlots);
+    int* fault_h = reduce_adam_fault();
+    int* fault_d = nullptr;
+    if (fault_h && hipHostGetDevicePointer(reinterpret_cast<void**>(&fault_d), fault_h, 0) != hipSuccess)
+        fault_d = nullptr;
+    if (!fault_d || !reduce_adam_coresident()) {
+        // the two-kernel form: k_ppo_grad_mfma + k_ppo_reduce, then k_adam
+        for (int i = 0; i < n_minibatches; ++i) {
+            int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
+                                     adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,
+                                     stats_d, stats_accum_d, st, true);
+            if (rc) return rc;
+            rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part,
+                             true, 1.0f, st);
+            if (rc) return rc;
+        }
+        return RT_OK;
+    }
     // the arrival counter of k_ppo_reduce_adam: the last norm slot (unused by the partials)
     unsigned* counter = reinterpret_cast<unsigned*>(norm_part + (kNormSlots - 1));
     if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess)
@@ -1478,6 +1537,7 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
         Q.flat_off[t] = (int32_t)off;
     }
     Q.counter = counter;
+    Q.fault = fault_d;
     for (int i = 0; i < n_minibatches; ++i) {
         int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
                                  adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,

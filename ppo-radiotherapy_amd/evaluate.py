@@ -1,7 +1,6 @@
 """Policy evaluation (reference: ppo_eval.py:5-37), on the vectorised env."""
 from __future__ import annotations
 
-import numpy as np
 import torch
 
 

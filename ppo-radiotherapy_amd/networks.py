@@ -121,10 +121,11 @@ class PPO(GaussianHeadMixin, nn.Module):
         self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
 
 
-def _conv_layer(cin, groups, dims, pad):
+def _conv_layer(cin, groups, dims, pad, precision: str = "f32"):
     from . import _lib
 
-    return _lib.RtConvLayer(cin, groups, (ctypes.c_int32 * 3)(*dims), (ctypes.c_int32 * 3)(*pad))
+    return _lib.RtConvLayer(cin, groups, (ctypes.c_int32 * 3)(*dims), (ctypes.c_int32 * 3)(*pad),
+                            _lib.CONV_PREC[precision])
 
 
 def _stage_fwd(layer, out_dims, x, w, b, train: bool):
@@ -195,10 +196,14 @@ class FeaturesExtractor3D(nn.Module):
     The first pool pads each axis by (S_i - 2) % 2 (networks.py:18-20).
     On the GPU the three stages run as the fused f32-MFMA kernels of
     csrc/c3d.hip (forward + backward); the Conv3d modules hold the parameters
-    (same state-dict keys)."""
+    (same state-dict keys).  `conv_precision` ("f32", the reference's, or
+    "bf16x3") is the arithmetic of the forward products, passed per call in
+    each stage's rt_conv_layer (set_conv_precision)."""
 
-    def __init__(self, observation_shape, features_dim: int):
+    def __init__(self, observation_shape, features_dim: int, conv_precision: str = "f32"):
         super().__init__()
+        self.conv_precision = "f32"
+        self.set_conv_precision(conv_precision)
         self.observation_shape = tuple(observation_shape)
         c_in, *spatial = self.observation_shape
         pad1 = tuple((s - 2) % 2 for s in spatial)
@@ -220,6 +225,14 @@ class FeaturesExtractor3D(nn.Module):
         s = [(x - 2 - 2) // 2 + 1 for x in s]                  # conv3 + pool3
         return 16 * int(np.prod(s))
 
+    def set_conv_precision(self, precision: str):
+        """Arithmetic of the stages' forward products ("f32" or "bf16x3")."""
+        if precision not in ("f32", "bf16x3"):
+            raise ValueError(f"conv_precision {precision!r}: expected 'f32' or 'bf16x3'")
+        if precision != self.conv_precision:
+            self.conv_precision = precision
+            self._plan_cache = None
+
     def _plan(self):
         """rt_conv_layer descriptors + pooled dims of the three stages."""
         if getattr(self, "_plan_cache", None) is None:
@@ -230,7 +243,7 @@ class FeaturesExtractor3D(nn.Module):
             pads = [tuple((s - 2) % 2 for s in spatial), (0, 0, 0), (0, 0, 0)]
             dims, plan = tuple(spatial), []
             for (cin, groups), pad in zip([(c_in, 1), (16, 2), (16, 4)], pads):
-                layer = _conv_layer(cin, groups, dims, pad)
+                layer = _conv_layer(cin, groups, dims, pad, self.conv_precision)
                 od = (ctypes.c_int32 * 3)()
                 _lib.check(L.rt_conv_out_dims(ctypes.byref(layer), od), "rt_conv_out_dims")
                 plan.append((layer, tuple(od)))

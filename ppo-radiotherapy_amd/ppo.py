@@ -132,21 +132,21 @@ class PPOTrainer:
             self._ppo_stats = torch.zeros(6, **kw)
             self._ppo_accum = torch.zeros(6, **kw)
             # arithmetic of the fused grad kernel's 64x64 products: "f32" (the
-            # reference's) or "bf16x3" (rt_ppo_set_precision, include/rtenv.h)
+            # reference's) or "bf16x3" (rt_ppo_hparams.precision, per call)
             prec = str(getattr(cfg, "update_precision", "f32"))
             if prec not in _lib.PPO_PREC:
                 raise ValueError(f"update_precision {prec!r}: expected one of {sorted(_lib.PPO_PREC)}")
             self._update_prec = _lib.PPO_PREC[prec]
         # arithmetic of the C3D forward products (vision agent): "f32" (the
-        # reference's) or "bf16x3".  rt_conv_set_precision is process-wide, so
-        # the trainer sets it at the start of every rollout step and update of
-        # its own (_apply_conv_precision); None (the default) leaves the
-        # library's setting (RT_CONV_PREC at load, else f32) alone
-        cprec = getattr(cfg, "conv_precision", None)
-        if cprec is not None and str(cprec) not in _lib.CONV_PREC:
+        # reference's, the default) or "bf16x3"; the extractor passes it per
+        # call in each stage's rt_conv_layer
+        cprec = str(getattr(cfg, "conv_precision", None) or "f32")
+        if cprec not in _lib.CONV_PREC:
             raise ValueError(f"conv_precision {cprec!r}: expected one of {sorted(_lib.CONV_PREC)}")
-        self._conv_prec = None if cprec is None else _lib.CONV_PREC[str(cprec)]
-        self._apply_conv_precision()
+        self.conv_precision = cprec
+        fe = getattr(agent, "features_extractor", None)
+        if fe is not None and hasattr(fe, "set_conv_precision"):
+            fe.set_conv_precision(cprec)
         # one flat gradient bucket; every param.grad is a view of it
         self.flat_grad = torch.zeros(n, dtype=self.params[0].dtype, **kw)
         off = 0
@@ -201,10 +201,6 @@ class PPOTrainer:
         self.next_done = torch.zeros(N, **kw)
         self.global_step = 0
         self.iteration = 0
-
-    def _apply_conv_precision(self):
-        if self._conv_prec is not None and self.device.type == "cuda":
-            _lib.check(_lib.load().rt_conv_set_precision(self._conv_prec), "rt_conv_set_precision")
 
     # parameter order of the fused kernels (include/rtenv.h rt_policy_sample)
     POLICY_ORDER = ["actor_mean.0.weight", "actor_mean.0.bias", "actor_mean.2.weight", "actor_mean.2.bias",
@@ -279,7 +275,6 @@ class PPOTrainer:
         """One vectorised step of train.py:138-161 (policy sample + env step)."""
         if self.fused_policy:
             return self._rollout_step_fused(step, env_events)
-        self._apply_conv_precision()
         if self.compact_obs:
             self.env.snapshot(self.dose_snap[step], self.pose_snap[step], self.tumour_snap[step])
         else:
@@ -453,8 +448,19 @@ class PPOTrainer:
         return torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,
                             approx_kl, clipfrac])
 
-    def _optimizer_step(self):
-        nn.utils.clip_grad_norm_(self.params, float(self.cfg.max_grad_norm))
+    def _optimizer_step(self, grad_div: int = 1):
+        """clip_grad_norm_ + Adam (train.py:244-246).  grad_div > 1: the flat
+        bucket holds the ranks' SUM (all-reduced, not yet averaged); the
+        average and the clip are one multiply by min(1, max_norm / (||g|| /
+        world + 1e-6)) / world -- torch's clip coefficient of the averaged
+        gradient, without a division pass over the bucket of its own."""
+        max_norm = float(self.cfg.max_grad_norm)
+        if grad_div == 1:
+            nn.utils.clip_grad_norm_(self.params, max_norm)
+        else:
+            norm = torch.linalg.vector_norm(self.flat_grad) / grad_div
+            coef = (max_norm / (norm + 1e-6)).clamp(max=1.0)
+            self.flat_grad.mul_(coef / grad_div)
         self.optimizer.step()
 
     def _bind_batch(self):
@@ -518,7 +524,7 @@ class PPOTrainer:
         bucket between rt_ppo_grad and rt_adam_step)."""
         self._bind_batch()
         L = _lib.load()
-        _lib.check(L.rt_ppo_set_precision(self._update_prec), "rt_ppo_set_precision")  # process-wide: set per call
+        self._hp.precision = self._update_prec  # per call (rt_ppo_hparams.precision)
         stream = _lib.stream_handle()
         batch = self._batch_struct()
         hp = ctypes.byref(self._hp)
@@ -564,7 +570,6 @@ class PPOTrainer:
         """train.py:183-248: update_epochs x num_minibatches optimizer steps."""
         if self.fused_update:
             return self._update_fused()
-        self._apply_conv_precision()
         self._bind_batch()
         dev = self.device
         stats_sum = torch.zeros(6, device=dev)
@@ -577,8 +582,8 @@ class PPOTrainer:
                 mb = perm[start:start + self.minibatch_size]
                 st = self._minibatch_loss_backward(mb)
                 stats_sum[5] += st[5]
-                self._allreduce_(self.flat_grad)
-                self._optimizer_step()
+                self._allreduce_(self.flat_grad, average=False)  # SUM; averaged inside the clip multiply
+                self._optimizer_step(self.world if self.collective else 1)
                 n_mb += 1
                 if self.max_minibatches and n_mb >= self.max_minibatches:
                     break

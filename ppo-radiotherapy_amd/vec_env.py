@@ -118,7 +118,11 @@ class RadiotherapyVecEnv:
         mask_t = None if mask is None else _device_array(mask, torch.uint8, self.device)
         _lib.check(self._L.rt_env_reset(self._h, _lib.ptr(mask_t), _lib.ptr(ids_t), _lib.ptr(self.obs),
                                         _lib.stream_handle()), "rt_env_reset")
-        self._episode_start.fill_(time.perf_counter())
+        now = time.perf_counter()
+        if mask_t is None:
+            self._episode_start.fill_(now)
+        else:  # RecordEpisodeStatistics' clock restarts for the reset envs only
+            self._episode_start = torch.where(mask_t.bool(), now, self._episode_start)
         return self.obs, {}
 
     def step(self, actions: torch.Tensor, info_out: torch.Tensor | None = None,
@@ -142,7 +146,18 @@ class RadiotherapyVecEnv:
         _lib.check(self._L.rt_env_step(self._h, _lib.ptr(a), _lib.ptr(self.obs), _lib.ptr(rew),
                                        _lib.ptr(self.terminated), _lib.ptr(info), _lib.stream_handle()),
                    "rt_env_step")
-        return self.obs, rew, self.terminated.view(torch.bool), self.truncated, LazyInfos(self._infos, info)
+        return self.obs, rew, self.terminated.view(torch.bool), self.truncated, self._lazy_infos(info)
+
+    def _lazy_infos(self, info: torch.Tensor) -> "LazyInfos":
+        """RecordEpisodeStatistics' wall-clock `t` (gymnasium 1.0: seconds
+        since the env's own reset, rounded to 6 decimals): the host time of
+        this step minus each env's episode start, which an autoreset on this
+        step (info[RT_INFO_STEPPED] = 0) moves to now -- two small device ops
+        per facade step, no host sync."""
+        now = time.perf_counter()
+        ep_t = now - self._episode_start
+        self._episode_start = torch.where(info[:, 16] < 0.5, now, self._episode_start)
+        return LazyInfos(lambda I: self._infos(I, ep_t), info)
 
     def step_policy(self, step, info_out: torch.Tensor | None = None, reward_out: torch.Tensor | None = None):
         """Fused rollout step (rt_env_step_policy): the visionless MLP policy
@@ -157,7 +172,7 @@ class RadiotherapyVecEnv:
         _lib.check(self._L.rt_env_step_policy(self._h, ctypes.byref(step), _lib.ptr(self.obs), _lib.ptr(rew),
                                               _lib.ptr(self.terminated), _lib.ptr(info), _lib.stream_handle()),
                    "rt_env_step_policy")
-        return self.obs, rew, self.terminated.view(torch.bool), self.truncated, LazyInfos(self._infos, info)
+        return self.obs, rew, self.terminated.view(torch.bool), self.truncated, self._lazy_infos(info)
 
     def rollout_policy(self, rollout) -> int:
         """`rollout.n_steps` fused rollout steps (rt_env_rollout_policy): one
@@ -325,7 +340,7 @@ class RadiotherapyVecEnv:
             pass
 
     # ------------------------------------------------------------------ infos
-    def _infos(self, I=None):
+    def _infos(self, I=None, ep_t=None):
         I = self.info if I is None else I
         stepped = I[:, 16] > 0.5
         ep_done = I[:, 17] > 0.5
@@ -333,7 +348,10 @@ class RadiotherapyVecEnv:
             "total": I[:, 0], "tumour": I[:, 1], "lung": I[:, 2], "distance_to_tumour": I[:, 3],
             "_total": stepped, "_tumour": stepped, "_lung": stepped, "_distance_to_tumour": stepped,
         }
-        ep = {"r": I[:, 18], "l": I[:, 19], "_r": ep_done, "_l": ep_done, "_t": ep_done}
+        if ep_t is None:
+            ep_t = time.perf_counter() - self._episode_start
+        ep = {"r": I[:, 18], "l": I[:, 19], "t": torch.where(ep_done, ep_t.round(decimals=6), 0.0),
+              "_r": ep_done, "_l": ep_done, "_t": ep_done}
         return {
             "reward_components": rc, "_reward_components": stepped,
             "beam_position": {"translation": I[:, 10:13], "rotation": I[:, 13:16]}, "_beam_position": stepped,

@@ -71,7 +71,7 @@ def test_config_defaults_are_reference_constants():
     assert c.tumour_dose_threshold == np.float32(0.9) and c.min_angle_z == math.pi / 4
     assert c.movement_speed == 0.2 and c.rotation_speed == 0.5
     assert (c.lung_dose_reward, c.tumour_dose_reward, c.distance_reward) == (-1.0, 10.0, -1.0)
-    assert L.rt_abi_version() == 3
+    assert L.rt_abi_version() == 4
     assert c.struct_size == ctypes.sizeof(_lib.RtEnvConfig)
 
 
@@ -175,17 +175,40 @@ def test_fast_sincos_matches_plain_double_double(tmp_path):
     assert out.returncode == 0, out.stdout
 
 
-def test_ppo_precision_switch():
-    """rt_ppo_set_precision: the two RT_PPO_PREC_* values round-trip, anything
-    else is RT_EINVAL and leaves the setting alone (host-only, no launch)."""
+def test_ppo_precision_is_per_call():
+    """rt_ppo_hparams.precision (ABI 4: per call, no process-wide setting):
+    a value other than the two RT_PPO_PREC_* is RT_EINVAL before anything is
+    launched (host-only; the dummy pointers are never dereferenced)."""
     L = _lib.load()
-    before = L.rt_ppo_get_precision()
-    try:
-        for name, v in _lib.PPO_PREC.items():
-            assert L.rt_ppo_set_precision(v) == 0, name
-            assert L.rt_ppo_get_precision() == v
-        assert L.rt_ppo_set_precision(7) == -1
-        assert b"precision" in L.rt_last_error()
-        assert L.rt_ppo_get_precision() == _lib.PPO_PREC["bf16x3"]
-    finally:
-        L.rt_ppo_set_precision(before)
+    assert not hasattr(L, "rt_ppo_set_precision") and not hasattr(L, "rt_conv_set_precision")
+    fake = (ctypes.c_void_p * 13)(*[16 * (i + 1) for i in range(13)])
+    batch = _lib.RtPpoBatch(16, 32, 48, 64, 80, 96, 1024)
+    hp = _lib.RtPpoHparams(clip_coef=0.1, clip_vloss=1, norm_adv=0, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
+                           adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5, precision=7)
+    rc = L.rt_ppo_grad(fake, fake, ctypes.byref(batch), 128, 256, None, ctypes.byref(hp), 256, 1 << 20, 512,
+                       None, None)
+    assert rc == -1
+    assert b"bad argument" in L.rt_last_error()
+
+def test_conv_mfma_count_hook():
+    """rt_conv_mfma_count (host only): the MFMA wave-instructions of the f32
+    Winograd launches bench.py's c3d_mfma counts as executed work -- linear in
+    the batch, 0 for bf16x3 (direct kernels), -1 for a bad pass; the data
+    gradient of conv2 at 64^3 (31^3 input, 16^3 tiles) is 2 groups x 16 tile
+    rows x 16 items x 64 xi x 2 channel quads per sample."""
+    L = _lib.load()
+
+    def lay(cin, groups, dims, pad, prec="f32"):
+        return _lib.RtConvLayer(cin, groups, (ctypes.c_int32 * 3)(*dims), (ctypes.c_int32 * 3)(*pad),
+                                _lib.CONV_PREC[prec])
+
+    c1 = lay(4, 1, (64, 64, 64), (0, 0, 0))
+    c2 = lay(16, 2, (31, 31, 31), (0, 0, 0))
+    n1 = L.rt_conv_mfma_count(ctypes.byref(c1), 1, 0)
+    assert n1 > 0 and L.rt_conv_mfma_count(ctypes.byref(c1), 512, 0) == 512 * n1
+    # conv1 forward: 31^3 pooled windows in 16-window items of pooled rows, 64 xi, one channel quad
+    assert n1 >= 31 * 31 * 31 // 16 * 64
+    assert L.rt_conv_mfma_count(ctypes.byref(c2), 3, 1) == 3 * 2 * 16 * 16 * 64 * 2
+    assert L.rt_conv_mfma_count(ctypes.byref(c1), 1, 1) == 0  # conv1 has no data gradient
+    assert L.rt_conv_mfma_count(ctypes.byref(lay(4, 1, (64, 64, 64), (0, 0, 0), "bf16x3")), 1, 0) == 0
+    assert L.rt_conv_mfma_count(ctypes.byref(c1), 1, 2) == -1

@@ -29,10 +29,14 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
+_PREC = ["f32"]  # the arithmetic _layer / _check_extractor pass per call (_conv_precision)
+
+
 def _layer(cin, groups, dims, pad):
     from ppo_radiotherapy_amd import _lib
 
-    return _lib.RtConvLayer(cin, groups, (ctypes.c_int32 * 3)(*dims), (ctypes.c_int32 * 3)(*pad))
+    return _lib.RtConvLayer(cin, groups, (ctypes.c_int32 * 3)(*dims), (ctypes.c_int32 * 3)(*pad),
+                            _lib.CONV_PREC[_PREC[0]])
 
 
 def _ref(x, w, b, groups, pad):
@@ -46,25 +50,23 @@ def test_conv_relu_pool_forward(cin, groups, dims, pad, B):
 
 
 class _conv_precision:
-    """rt_conv_set_precision for the duration of a block (process-wide setting)."""
+    """rt_conv_layer.precision of the layers this module builds, for the
+    duration of a block (the arithmetic is per call)."""
 
     def __init__(self, name):
         self.name = name
 
     def __enter__(self):
-        from ppo_radiotherapy_amd import _lib
-
-        self.L = _lib.load()
-        self.prev = int(self.L.rt_conv_get_precision())
-        _lib.check(self.L.rt_conv_set_precision(_lib.CONV_PREC[self.name]), "rt_conv_set_precision")
+        self.prev = _PREC[0]
+        _PREC[0] = self.name
 
     def __exit__(self, *exc):
-        self.L.rt_conv_set_precision(self.prev)
+        _PREC[0] = self.prev
 
 
 @pytest.mark.parametrize("cin,groups,dims,pad,B", STAGES)
 def test_forward_bf16x3(cin, groups, dims, pad, B):
-    """bf16x3 products (rt_conv_set_precision: conv1's ring kernel and the
+    """bf16x3 products (rt_conv_layer.precision: conv1's ring kernel and the
     grouped stages' z-shift kernels; other stage kernels stay f32): the f32 forward's
     value and activity gates at unchanged tolerances (within 2e-5 of float64
     torch), and torch's argmax on every window whose top-2 gap exceeds the
@@ -75,7 +77,7 @@ def test_forward_bf16x3(cin, groups, dims, pad, B):
     from ppo_radiotherapy_amd import _lib
 
     with _conv_precision("bf16x3"):
-        assert int(_lib.load().rt_conv_get_precision()) == _lib.CONV_PREC["bf16x3"]
+        assert _layer(cin, groups, dims, pad).precision == _lib.CONV_PREC["bf16x3"]
         _check_forward(cin, groups, dims, pad, B, prod_err=2.0 ** -15)
 
 
@@ -83,8 +85,14 @@ def test_conv_precision_rejects_unknown():
     from ppo_radiotherapy_amd import _lib
 
     L = _lib.load()
-    assert L.rt_conv_set_precision(7) == -1  # RT_EINVAL
-    assert int(L.rt_conv_get_precision()) in _lib.CONV_PREC.values()
+    lay = _layer(4, 1, (8, 8, 8), (0, 0, 0))
+    lay.precision = 7
+    x = torch.zeros((1, 4, 8, 8, 8), device="cuda")
+    w = torch.zeros((16, 4, 3, 3, 3), device="cuda")
+    b = torch.zeros(16, device="cuda")
+    y = torch.empty((1, 16, 3, 3, 3), device="cuda")
+    assert L.rt_conv_relu_pool_fwd(ctypes.byref(lay), 1, x.data_ptr(), None, w.data_ptr(), b.data_ptr(),
+                                   y.data_ptr(), None, None) == -1  # RT_EINVAL
 
 
 def _check_forward(cin, groups, dims, pad, B, prod_err=0.0):
@@ -316,7 +324,7 @@ def _check_extractor(shape, B, gtol):
     from ppo_radiotherapy_amd.networks import FeaturesExtractor3D, _stage_fwd
 
     torch.manual_seed(0)
-    fe = FeaturesExtractor3D(shape, 64)
+    fe = FeaturesExtractor3D(shape, 64, conv_precision=_PREC[0])
     ref = FeaturesExtractor3D(shape, 64).double()
     ref.load_state_dict({k: v.double() for k, v in fe.state_dict().items()})
     fe = fe.cuda()

@@ -212,7 +212,7 @@ def test_train_cli_vision_reference_grid(tmp_path, capsys, conv_precision):
     configs/vision.yaml.template keys), run through the CLI at the reference
     grid 67x43x70 -- odd dims, so the first pool pads (networks.py:18-20) --
     on the C3D kernels, with the micro-batched update; and with the config key
-    conv_precision: bf16x3 (conv1's forward products, rt_conv_set_precision)."""
+    conv_precision: bf16x3 (the forward products, rt_conv_layer.precision)."""
     import yaml
 
     import train as train_mod
@@ -223,16 +223,12 @@ def test_train_cli_vision_reference_grid(tmp_path, capsys, conv_precision):
                     update_epochs=2, num_saves=1, micro_batch=6))
     if conv_precision:
         cfg["conv_precision"] = conv_precision
-    L = _lib.load()
-    prev = int(L.rt_conv_get_precision())
     p = tmp_path / "vision.yaml"
     yaml.safe_dump(cfg, open(p, "w"))
     out = tmp_path / "out"
-    try:
-        agent = train_mod.main(["--config-file", str(p), "--output-dir", str(out)])
-        assert int(L.rt_conv_get_precision()) == _lib.CONV_PREC[conv_precision or "f32"] if conv_precision else True
-    finally:
-        L.rt_conv_set_precision(prev)
+    agent = train_mod.main(["--config-file", str(p), "--output-dir", str(out)])
+    want = _lib.CONV_PREC[conv_precision or "f32"]
+    assert all(layer.precision == want for layer, _ in agent.features_extractor._plan())
     printed = capsys.readouterr().out
     assert "Observation shape:  (4, 67, 43, 70)" in printed  # agent.summary()
     from ppo_radiotherapy_amd.networks import PPO_3DCNN

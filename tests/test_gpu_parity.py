@@ -7,6 +7,8 @@ accumulated dose volumes bit-exact.
 """
 import ctypes
 
+import time
+
 import numpy as np
 import pytest
 
@@ -188,9 +190,11 @@ def test_termination_and_autoreset(golden, dev, mode):
     acts = torch.tensor(z["actions"], dtype=torch.float32, device=env.device)
     ret = np.zeros(E)
     finished = np.zeros(E, bool)
+    t_start = time.perf_counter()
     for t in range(101):
         a = acts[:, min(t, 99)].contiguous()
         obs, rew, term, trunc, infos = env.step(a)
+        t_now = time.perf_counter()
         r = rew.cpu().numpy()
         term = term.cpu().numpy()
         stepped = infos["_reward_components"].cpu().numpy()
@@ -206,6 +210,11 @@ def test_termination_and_autoreset(golden, dev, mode):
                     assert epd[e]
                     assert abs(infos["episode"]["r"][e].item() - ret[e]) <= 1e-4
                     assert infos["episode"]["l"][e].item() == L
+                    # episode["t"] (gymnasium 1.0 RecordEpisodeStatistics): wall
+                    # seconds since the env's reset, rounded to 6 decimals
+                    ep_t = infos["episode"]["t"][e].item()
+                    assert infos["episode"]["_t"][e].item()
+                    assert 0.0 < ep_t <= t_now - t_start + 1e-6 and abs(ep_t - round(ep_t, 6)) < 1e-9
                     finished[e] = True
             elif t == L:  # autoreset step: action ignored, reward 0, reset obs
                 assert not stepped[e] and r[e] == 0.0 and not term[e] and not epd[e]

@@ -134,22 +134,18 @@ def test_fused_grad_matches_autograd(mb, clip_vloss, norm_adv, ent, prec):
     pp, _ = _policy_ptrs(agent)
     gp, grads = _policy_ptrs(agent, grads=True)
     hp = _lib.RtPpoHparams(clip_coef=0.1, clip_vloss=clip_vloss, norm_adv=norm_adv, ent_coef=ent, vf_coef=0.5,
-                           max_grad_norm=0.5, adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
+                           max_grad_norm=0.5, adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5,
+                           precision=_lib.PPO_PREC[prec])
     batch = _lib.RtPpoBatch(obs.data_ptr(), act.data_ptr(), logp.data_ptr(), adv.data_ptr(), ret.data_ptr(),
                             val.data_ptr(), B)
     L = _lib.load()
     ws = torch.empty(int(L.rt_ppo_workspace_floats(mb)), device=dev)
     st = torch.zeros(6, device=dev)
     acc = torch.ones(6, device=dev)
-    _lib.check(L.rt_ppo_set_precision(_lib.PPO_PREC[prec]), "rt_ppo_set_precision")
-    assert L.rt_ppo_get_precision() == _lib.PPO_PREC[prec]
-    try:
-        _lib.check(L.rt_ppo_grad(pp, gp, ctypes.byref(batch), idx.data_ptr(), mb, stats2.data_ptr(),
-                                 ctypes.byref(hp), ws.data_ptr(), ws.numel(), st.data_ptr(), acc.data_ptr(), None),
-                   "rt_ppo_grad")
-        torch.cuda.synchronize()
-    finally:
-        _lib.check(L.rt_ppo_set_precision(_lib.PPO_PREC["f32"]), "rt_ppo_set_precision")
+    _lib.check(L.rt_ppo_grad(pp, gp, ctypes.byref(batch), idx.data_ptr(), mb, stats2.data_ptr(),
+                             ctypes.byref(hp), ws.data_ptr(), ws.numel(), st.data_ptr(), acc.data_ptr(), None),
+               "rt_ppo_grad")
+    torch.cuda.synchronize()
     # float64 autograd reference (ppo.PPOTrainer._loss_backward, the reference's formulas)
     ref = PPO((9,), (6,), 64).double()
     ref.load_state_dict({k: v.double().cpu() for k, v in agent.state_dict().items()})
@@ -347,3 +343,64 @@ def test_fused_checkpoint_resume_is_bitwise():
     torch.cuda.synchronize()
     assert torch.equal(a.flat_param, b.flat_param)
     assert torch.equal(a._exp_avg_sq, b._exp_avg_sq)
+
+
+@pytest.mark.parametrize("max_norm", [0.0, 0.5])
+def test_update_call_equals_grad_plus_adam(max_norm):
+    """rt_ppo_update (k_ppo_grad_mfma -> k_ppo_reduce_adam per minibatch, the
+    reduce + clip + Adam in one launch behind a grid arrival) vs the same
+    minibatches through the separate entry points rt_ppo_grad + rt_adam_step
+    (grad_div 1), from the same state, permutation and advantage statistics
+    (ADVICE r4).  Without clipping the two are bitwise equal (params, Adam
+    moments, the last gradient, the loss statistics); with clipping
+    rt_adam_step takes ||g|| from its own partial sums (k_gnorm, another
+    summation order), so the clip coefficient agrees to f32 rounding."""
+    import ctypes
+
+    from ppo_radiotherapy_amd import _lib
+
+    tr = _make(fused=True)
+    dev = tr.device
+    tr._bind_batch()
+    batch = tr._batch_struct()
+    L = _lib.load()
+    mbs, n_mb = tr.minibatch_size, tr.batch_size // tr.minibatch_size
+    perm = torch.randperm(tr.batch_size, generator=torch.Generator().manual_seed(9)).to(dev)
+    adv = torch.empty((n_mb, 2), device=dev)
+    _lib.check(L.rt_ppo_adv_stats(tr._b_adv.data_ptr(), perm.data_ptr(), mbs, n_mb, adv.data_ptr(),
+                                  tr._ws.data_ptr(), tr._ws.numel(), None), "rt_ppo_adv_stats")
+    hp = _lib.RtPpoHparams(clip_coef=0.1, clip_vloss=1, norm_adv=1, ent_coef=0.01, vf_coef=0.5,
+                           max_grad_norm=max_norm, adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
+    state = [tr.flat_param, tr._exp_avg, tr._exp_avg_sq]
+    with torch.no_grad():
+        tr._exp_avg.normal_(0, 1e-3)
+        tr._exp_avg_sq.uniform_(0, 1e-5)
+    start = [t.clone() for t in state]
+    n, lr, step0 = tr.flat_param.numel(), 2.5e-4, 7
+    stats_a, acc_a = torch.zeros(6, device=dev), torch.zeros(6, device=dev)
+    _lib.check(L.rt_ppo_update(tr._policy_ptrs, tr._grad_ptrs, ctypes.byref(batch), perm.data_ptr(), mbs, n_mb,
+                               adv.data_ptr(), ctypes.byref(hp), tr.flat_param.data_ptr(), tr.flat_grad.data_ptr(),
+                               tr._exp_avg.data_ptr(), tr._exp_avg_sq.data_ptr(), n, step0, lr, tr._ws.data_ptr(),
+                               tr._ws.numel(), stats_a.data_ptr(), acc_a.data_ptr(), None), "rt_ppo_update")
+    torch.cuda.synchronize()
+    got = [t.clone() for t in state] + [tr.flat_grad.clone()]
+    with torch.no_grad():
+        for t, s in zip(state, start):
+            t.copy_(s)
+    stats_b, acc_b = torch.zeros(6, device=dev), torch.zeros(6, device=dev)
+    for i in range(n_mb):
+        _lib.check(L.rt_ppo_grad(tr._policy_ptrs, tr._grad_ptrs, ctypes.byref(batch), perm.data_ptr() + 8 * i * mbs,
+                                 mbs, adv.data_ptr() + 8 * i, ctypes.byref(hp), tr._ws.data_ptr(), tr._ws.numel(),
+                                 stats_b.data_ptr(), acc_b.data_ptr(), None), "rt_ppo_grad")
+        _lib.check(L.rt_adam_step(n, tr.flat_param.data_ptr(), tr.flat_grad.data_ptr(), tr._exp_avg.data_ptr(),
+                                  tr._exp_avg_sq.data_ptr(), step0 + i, lr, ctypes.byref(hp), 1,
+                                  tr._norm_ws.data_ptr(), None), "rt_adam_step")
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in state] + [tr.flat_grad.clone()]
+    assert torch.equal(stats_a, stats_b) and torch.equal(acc_a, acc_b)
+    for name, a, b in zip(("param", "exp_avg", "exp_avg_sq", "grad"), got, ref):
+        if max_norm == 0.0:
+            assert torch.equal(a, b), name
+        else:
+            torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-9, msg=name)
+    assert not torch.equal(got[0], start[0])  # the update moved the parameters
