@@ -215,6 +215,24 @@ def stagger_phases(tr, env, dev):
         tr.rollout_steps(k % tr.T, 1)
 
 
+_MARK_BUF = {}
+
+
+def window_marker(dev):
+    """A one-block rt_probe_stream launch on the current stream, issued just
+    before a timed window's opening synchronise: it marks the window in a
+    rocprofv3 kernel trace (tools/window_kernels.py, tools/call_cost_trace.py)
+    and costs the window nothing."""
+    import torch
+
+    from ppo_radiotherapy_amd import _lib
+
+    buf = _MARK_BUF.get(dev)
+    if buf is None:
+        buf = _MARK_BUF[dev] = torch.zeros(4, device=dev)
+    _lib.check(_lib.load().rt_probe_stream(buf.data_ptr(), buf.data_ptr(), 4, 0, 1, _lib.stream_handle()), "marker")
+
+
 def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int = 2):
     """Env steps/s over three back-to-back windows of calls x T (>= 101)
     rollout steps each, on the staggered episode phases stagger_phases set up
@@ -225,14 +243,8 @@ def steady_state(tr, env, dev, barrier, max_over_ranks, total_envs, calls: int =
     a rocprofv3 kernel trace (tools/window_kernels.py)."""
     import torch
 
-    from ppo_radiotherapy_amd import _lib
-
-    L = _lib.load()
-    mark_buf = torch.zeros(4, device=dev)
-
     def mark():
-        _lib.check(L.rt_probe_stream(mark_buf.data_ptr(), mark_buf.data_ptr(), 4, 0, 1, _lib.stream_handle()),
-                   "marker")
+        window_marker(dev)
 
     T = tr.T
     K = calls * T
@@ -722,6 +734,7 @@ def main():
 
     # `value`: the uninstrumented pass (the library's timing events, recorded
     # between kernels, cost ~4 % of the pipelined step)
+    window_marker(dev)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

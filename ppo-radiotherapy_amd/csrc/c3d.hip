@@ -894,6 +894,11 @@ int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* ro
 // item is 16 consecutive windows of the block's y band (row-major over
 // (py, px)), one per lane group column n.
 // ---------------------------------------------------------------------------
+#ifndef RT_WINO_C1_NTH
+#define RT_WINO_C1_NTH 512
+#endif
+constexpr int kWinoC1Nth = RT_WINO_C1_NTH;  // threads per block of conv1's Winograd forward
+
 template <int CPG>
 constexpr int wino_u_floats() {  // U in LDS: 16 columns x 64 lanes x 4 xi_z x CPG / 4 quads
     return 16 * 64 * 4 * (CPG / 4);
@@ -924,7 +929,7 @@ struct WinoParams {
 // no spills; left free the compiler took 150 VGPRs + 44 AGPRs = 2 waves) --
 // its 256-thread blocks are small enough for 3 per CU
 template <int CPG, int COG, int VEC, int NTH, bool TRAIN>
-__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(CPG == 4 && COG == 4 ? 3 : 1)))
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(CPG == 4 && NTH == 256 ? 3 : 1)))
 void k_conv_wino(WinoParams P) {
     extern __shared__ float xs[];
     constexpr int NW = NTH / 64;
@@ -1206,13 +1211,14 @@ int wino_read_cycles(int PW, int nwin, int YS, int CS) {
 }
 
 // Row stride YS and channel stride CS of the Winograd ring (>= XL and YL YS,
-// multiples of the DMA width and of 2 for the float2 patch reads) with the
-// fewest patch-read bank cycles, then the smallest; cached per shape (the
-// launch planner evaluates every band height)
-std::pair<int, int> wino_strides(int PW, int nwin, int XL, int YL, int VEC) {
+// multiples of the DMA width and of 2 for the float2 patch reads, CS <=
+// cs_max: the block's LDS budget) with the fewest patch-read bank cycles,
+// then the smallest; cached per shape (the launch planner evaluates every
+// band height)
+std::pair<int, int> wino_strides(int PW, int nwin, int XL, int YL, int VEC, int cs_max) {
     static std::mutex mu;
-    static std::map<std::tuple<int, int, int, int, int>, std::pair<int, int>> cache;
-    const auto key = std::make_tuple(PW, nwin, XL, YL, VEC);
+    static std::map<std::tuple<int, int, int, int, int, int>, std::pair<int, int>> cache;
+    const auto key = std::make_tuple(PW, nwin, XL, YL, VEC, cs_max);
     std::lock_guard<std::mutex> lock(mu);
     const auto f = cache.find(key);
     if (f != cache.end()) return f->second;
@@ -1221,7 +1227,7 @@ std::pair<int, int> wino_strides(int PW, int nwin, int XL, int YL, int VEC) {
     int best = INT_MAX, bys = ys0, bcs = YL * ys0;
     for (int ys = ys0; ys < ys0 + 32; ys += step) {
         const int cs0 = (YL * ys + step - 1) / step * step;  // even: the float2 patch reads stay 8-B aligned
-        for (int cs = cs0; cs < cs0 + 64; cs += step) {
+        for (int cs = cs0; cs < cs0 + 64 && cs <= cs_max; cs += step) {
             const int c = wino_read_cycles(PW, nwin, ys, cs);
             if (c < best || (c == best && cs < bcs)) {
                 best = c;
@@ -1237,7 +1243,7 @@ std::pair<int, int> wino_strides(int PW, int nwin, int XL, int YL, int VEC) {
 // 2 PW + 2 input columns (the last window's 4-wide patch), row / channel
 // strides from wino_strides; z chunks until the grid has ~2048 blocks
 template <int CPG, int VEC>
-RingGeom make_wino_geom(const rt_conv_layer* L, int B, int G, int pyb) {
+RingGeom make_wino_geom(const rt_conv_layer* L, int B, int G, int pyb, size_t lds_budget = 160 * 1024) {
     RingGeom r{};
     Geom& g = r.g;
     g.D = L->in_dims[0];
@@ -1256,7 +1262,8 @@ RingGeom make_wino_geom(const rt_conv_layer* L, int B, int G, int pyb) {
     g.ZL = 4;
     g.YL = 2 * pyb + 2;
     g.XL = 2 * g.PW + 2;
-    const std::pair<int, int> st = wino_strides(g.PW, std::min(pyb, g.PH) * g.PW, g.XL, g.YL, VEC);
+    const int cs_max = (int)((lds_budget / sizeof(float) - wino_u_floats<CPG>()) / (kRing * CPG));
+    const std::pair<int, int> st = wino_strides(g.PW, std::min(pyb, g.PH) * g.PW, g.XL, g.YL, VEC, cs_max);
     g.YS = st.first;
     g.ZS = 0;
     g.CS = st.second;
@@ -1309,7 +1316,11 @@ int launch_fwd_wino(const rt_conv_layer* L, int32_t B, const float* x, const int
     if (!(L->cin == 4 || G == 2 || G == 4) || (int64_t)B * G > 65535) return RT_ELIMIT;
     const bool vec4 = cpg == 4 && G == 1 && L->in_dims[2] % 4 == 0 && L->pool_pad[2] == 0 &&
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    const int nth = G == 4 ? 256 : 512;
+    // conv1 (and conv3): 256-thread blocks in a third of the LDS, three per
+    // CU = 3 waves per SIMD (<= 168 VGPRs), against 2 for one 512-thread
+    // block holding the whole LDS
+    int nth = (G == 4 || (G == 1 && kWinoC1Nth == 256)) ? 256 : 512;
+    size_t lds_budget = nth == 256 ? 160 * 1024 / 3 : 160 * 1024;
     // the band height with the fewest item rounds per pooled row over all
     // bands (a band's 16-window items go round-robin to the NW waves, so 9
     // items on 8 waves cost 2 rounds), plus ~1/4 round per band for its
@@ -1322,10 +1333,10 @@ int launch_fwd_wino(const rt_conv_layer* L, int32_t B, const float* x, const int
         const int ph = (L->in_dims[1] - 2 + 2 * L->pool_pad[1] - 2) / 2 + 1;
         double best_cost = 1e30;
         for (int pyb = 1; pyb <= ph; ++pyb) {
-            const RingGeom rg = make_wino_geom<CPG_, VEC_>(L, B, G, pyb);
+            const RingGeom rg = make_wino_geom<CPG_, VEC_>(L, B, G, pyb, lds_budget);
             const size_t lds = ((size_t)kRing * rg.SLOT + wino_u_floats<CPG_>()) * sizeof(float);
             const int items = (pyb * rg.g.PW + 15) / 16;
-            if (lds > 160 * 1024 || (rg.npiece + nw - 1) / nw > 16 || items > 2 * nw || rg.g.W < VEC_) break;
+            if (lds > lds_budget || (rg.npiece + nw - 1) / nw > 16 || items > 2 * nw || rg.g.W < VEC_) break;
             double cost = 0.25 * rg.nyb;
             for (int y = 0; y < ph; y += pyb) cost += ((std::min(pyb, ph - y) * rg.g.PW + 15) / 16 + nw - 1) / nw;
             if (cost <= best_cost) {
@@ -1342,14 +1353,32 @@ int launch_fwd_wino(const rt_conv_layer* L, int32_t B, const float* x, const int
         return RT_OK;
     };
     if (cpg == 4 && G == 1) {
-        if (vec4) {
-            const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{}, pyb);
-            if (pyb && mfma_count) return counted(rg, 1);
-            if (pyb) return launch_wino_k<4, 16, 4, 512>(rg, pyb, 1, B, x, rows, w, bias, y, amax, st);
+        // the small blocks when a band fits a third of the LDS, else one
+        // 512-thread block per CU (wide planes: 128^3)
+        auto conv1 = [&](auto nth_c, int64_t* cnt) -> int {
+            constexpr int NT = decltype(nth_c)::value;
+            nth = NT;
+            lds_budget = NT == 256 ? 160 * 1024 / 3 : 160 * 1024;
+            if (vec4) {
+                const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{}, pyb);
+                if (pyb && cnt) return *cnt = wino_fwd_mfma(rg, pyb, B, G, 1), RT_OK;
+                if (pyb) return launch_wino_k<4, 16, 4, NT>(rg, pyb, 1, B, x, rows, w, bias, y, amax, st);
+            }
+            const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, pyb);
+            if (pyb && cnt) return *cnt = wino_fwd_mfma(rg, pyb, B, G, 1), RT_OK;
+            if (pyb) return launch_wino_k<4, 16, 1, NT>(rg, pyb, 1, B, x, rows, w, bias, y, amax, st);
+            return RT_ELIMIT;
+        };
+        if constexpr (kWinoC1Nth == 256) {
+            // the small blocks unless their narrow bands pad the 16-window
+            // items by > 10 % more MFMAs than the big block's bands
+            int64_t c256 = 0, c512 = 0;
+            const int r256 = conv1(std::integral_constant<int, 256>{}, &c256);
+            const int r512 = conv1(std::integral_constant<int, 512>{}, &c512);
+            if (r256 == RT_OK && (r512 != RT_OK || c256 * 10 <= c512 * 11))
+                return conv1(std::integral_constant<int, 256>{}, mfma_count);
         }
-        const RingGeom rg = plan(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, pyb);
-        if (pyb && mfma_count) return counted(rg, 1);
-        if (pyb) return launch_wino_k<4, 16, 1, 512>(rg, pyb, 1, B, x, rows, w, bias, y, amax, st);
+        return conv1(std::integral_constant<int, 512>{}, mfma_count);
     } else if (G == 2) {
         const RingGeom rg = plan(std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{}, pyb);
         if (pyb && mfma_count) return counted(rg, 2);

@@ -186,11 +186,11 @@ def test_termination_and_autoreset(golden, dev, mode):
     lib = _custom_library(ref.shape, ref.lungs, tumours)
     E = len(tumours)
     env = _vec_env(E, lib, step_mode=mode)
+    t_start = time.perf_counter()  # the envs' RecordEpisodeStatistics clocks start inside reset()
     env.reset(options={"tumour_ids": np.arange(E, dtype=np.int32)})
     acts = torch.tensor(z["actions"], dtype=torch.float32, device=env.device)
     ret = np.zeros(E)
     finished = np.zeros(E, bool)
-    t_start = time.perf_counter()
     for t in range(101):
         a = acts[:, min(t, 99)].contiguous()
         obs, rew, term, trunc, infos = env.step(a)
