@@ -589,13 +589,17 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
     y32 = [t.clone() for t in y32]
     # PMC per stage kernel (committed run of the same kernels at this batch)
     if pmc is not None:
-        kern = {"conv1": ("k_conv_wino<4,16,4,512,true>", None), "conv2": ("k_conv_wino<8,8,1,512,true>",
-                "k_dgrad_wino<8,256>"), "conv3": ("k_conv_wino<4,4,1,256,true>", "k_dgrad_wino<4,256>")}
+        # kernel-name prefixes (the training forward, whose argmax bytes the PMC driver requests)
+        kern = {"conv1": ("k_conv_wino<4,16,", None), "conv2": ("k_conv_wino<8,8,", "k_dgrad_wino<8,"),
+                "conv3": ("k_conv_wino<4,4,", "k_dgrad_wino<4,")}
         for nm, (kf, kd) in kern.items():
-            for key, kname, count_key in (("forward", kf, "forward_mfma_insts"), ("dgrad", kd, "dgrad_mfma_insts")):
-                v = pmc["kernels"].get(kname) if kname else None
-                if v is None:
+            for key, prefix, count_key in (("forward", kf, "forward_mfma_insts"), ("dgrad", kd, "dgrad_mfma_insts")):
+                hits = [k for k in pmc["kernels"] if prefix and k.startswith(prefix)
+                        and (key == "dgrad" or k.endswith(",true>"))]
+                if not hits:
                     continue
+                kname = hits[0]
+                v = pmc["kernels"][kname]
                 stages[nm][f"{key}_pmc"] = {
                     "kernel": kname, "mfma_busy": v.get("mfma_busy_frac"), "clock_GHz": v.get("clock_GHz"),
                     "valu_per_mfma": v.get("valu_per_mfma"), "kernel_ms": v.get("kernel_ms"),

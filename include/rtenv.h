@@ -400,6 +400,16 @@ int rt_ppo_shuffle(int64_t n, uint64_t key, int64_t* perm_d, void* stream);
 int rt_ppo_shuffle_epochs(int64_t n, int32_t n_epochs, const uint64_t* keys_h, int64_t* perm_d, void* stream);
 int rt_ppo_adv_stats(const float* adv_d, const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
                      float* stats_d, float* workspace_d, int64_t workspace_floats, void* stream);
+/* rt_ppo_shuffle_epochs + the advantage statistics of all their minibatches
+ * (mb_size divides n) in one pass: perm_d[e*n .. (e+1)*n) as rt_ppo_shuffle_epochs,
+ * and either stats_d[n_epochs * n/mb_size][2] = rt_ppo_adv_stats of those
+ * minibatches (single process) or sums_d[..][2] = rt_ppo_adv_sums (data
+ * parallel: the caller all-reduces, then rt_ppo_adv_finalize) -- exactly one
+ * of the two non-NULL; bitwise the separate calls' results.  workspace_d:
+ * >= 128 * min(n_epochs, 32) * n/mb_size floats. */
+int rt_ppo_shuffle_adv(int64_t n, int32_t n_epochs, const uint64_t* keys_h, int64_t* perm_d, const float* adv_d,
+                       int32_t mb_size, double* sums_d, float* stats_d, float* workspace_d,
+                       int64_t workspace_floats, void* stream);
 /* Data-parallel form of rt_ppo_adv_stats (train.py:215-218 over the union
  * of the ranks' minibatches): rt_ppo_adv_sums writes this rank's per-minibatch
  * (sum, sum of squares) of adv, f64 sums_d[n_mb][2] (same workspace rule);

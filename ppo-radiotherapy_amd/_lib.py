@@ -38,7 +38,7 @@ EXPORTS = [
     "rt_debug_beam", "rt_debug_pose", "rt_env_beam_list", "rt_probe_random_rmw", "rt_probe_stream", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
     "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update",
-    "rt_ppo_shuffle", "rt_ppo_shuffle_epochs", "rt_ppo_adv_stats", "rt_ppo_adv_sums", "rt_ppo_adv_finalize",
+    "rt_ppo_shuffle", "rt_ppo_shuffle_epochs", "rt_ppo_shuffle_adv", "rt_ppo_adv_stats", "rt_ppo_adv_sums", "rt_ppo_adv_finalize",
     "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad", "rt_conv_mfma_count",
     "rt_conv_relu_pool_dgrad",
     "rt_last_error", "rt_abi_version",
@@ -184,6 +184,7 @@ def load(build_if_missing: bool = True):
                           ctypes.c_int),
         "rt_ppo_shuffle": ([i64, ctypes.c_uint64, vp, vp], ctypes.c_int),
         "rt_ppo_shuffle_epochs": ([i64, i32, vp, vp, vp], ctypes.c_int),
+        "rt_ppo_shuffle_adv": ([i64, i32, vp, vp, vp, i32, vp, vp, vp, i64, vp], ctypes.c_int),
         "rt_ppo_adv_stats": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
         "rt_ppo_adv_sums": ([vp, vp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
         "rt_ppo_adv_finalize": ([vp, i64, i32, vp, vp], ctypes.c_int),

@@ -895,7 +895,7 @@ int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* ro
 // (py, px)), one per lane group column n.
 // ---------------------------------------------------------------------------
 #ifndef RT_WINO_C1_NTH
-#define RT_WINO_C1_NTH 512
+#define RT_WINO_C1_NTH 256
 #endif
 constexpr int kWinoC1Nth = RT_WINO_C1_NTH;  // threads per block of conv1's Winograd forward
 

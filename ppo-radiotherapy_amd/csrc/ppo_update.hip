@@ -22,6 +22,7 @@
 #include "rt_trace.h"
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -1278,6 +1279,65 @@ __global__ __launch_bounds__(kAdvThreads) void k_adv_partial(const float* adv, c
     }
 }
 
+// rt_ppo_shuffle_adv: the epochs' permutations AND the minibatch advantage
+// partial sums in one launch -- k_adv_partial's grid and summation order, each
+// position's permuted index computed in place (feistel_index, the k_shuffle
+// arithmetic) and stored to perm as it is used, instead of a k_shuffle_epochs
+// pass whose output k_adv_partial then re-reads.  blockIdx.y = minibatch k of
+// the launch (epoch e0 + k / n_mb); the sums are bitwise k_adv_partial's.
+__global__ __launch_bounds__(kAdvThreads) void k_shuffle_adv_partial(const float* adv, int64_t n, int h,
+                                                                     ShuffleKeys K, int mb, int n_mb,
+                                                                     int64_t* perm, double* part) {
+    __shared__ double ps[kAdvThreads / 64], pq[kAdvThreads / 64];
+    const int chunk = (mb + kAdvParts - 1) / kAdvParts;
+    const int j0 = blockIdx.x * chunk, j1 = min(j0 + chunk, mb);
+    const int e = blockIdx.y / n_mb, m = blockIdx.y - e * n_mb;
+    const int64_t pos0 = (int64_t)m * mb;
+    int64_t* pe = perm + (int64_t)e * n;
+    const uint64_t key = K.k[e];
+    double s = 0.0, q = 0.0;
+    for (int jb = j0; jb < j1; jb += kAdvThreads * kAdvBatch) {
+        int64_t ix[kAdvBatch];
+        float a[kAdvBatch];
+#pragma unroll
+        for (int u = 0; u < kAdvBatch; ++u) {
+            const int j = jb + u * kAdvThreads + (int)threadIdx.x;
+            ix[u] = -1;
+            if (j < j1) {
+                ix[u] = feistel_index((uint32_t)(pos0 + j), n, h, key);
+                pe[pos0 + j] = ix[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kAdvBatch; ++u) a[u] = ix[u] >= 0 ? adv[ix[u]] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < kAdvBatch; ++u) {
+            s += (double)a[u];
+            q += (double)a[u] * (double)a[u];
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off, 64);
+        q += __shfl_xor(q, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ps[threadIdx.x >> 6] = s;
+        pq[threadIdx.x >> 6] = q;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double S = 0.0, Q = 0.0;
+        for (int w = 0; w < kAdvThreads / 64; ++w) {
+            S += ps[w];
+            Q += pq[w];
+        }
+        double* o = part + ((size_t)blockIdx.y * kAdvParts + blockIdx.x) * 2;
+        o[0] = S;
+        o[1] = Q;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_adv_stats(const double* part, int mb, int n_mb, float* stats) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n_mb) return;
@@ -1580,6 +1640,40 @@ extern "C" int rt_ppo_shuffle_epochs(int64_t n, int32_t n_epochs, const uint64_t
         for (int j = 0; j < ne; ++j) K.k[j] = keys_h[e0 + j];
         hipLaunchKernelGGL(k_shuffle_epochs, dim3((unsigned)((n + 255) / 256), (unsigned)ne), dim3(256), 0, st, n, h,
                            K, perm_d + (int64_t)e0 * n);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_ppo_shuffle_adv(int64_t n, int32_t n_epochs, const uint64_t* keys_h, int64_t* perm_d,
+                                  const float* adv_d, int32_t mb_size, double* sums_d, float* stats_d,
+                                  float* workspace_d, int64_t workspace_floats, void* stream) {
+    if (n < 1 || n > ((int64_t)1 << 31) || n_epochs < 1 || !keys_h || !perm_d || !adv_d || mb_size < 1 ||
+        n % mb_size != 0 || n / mb_size > 65535 || (sums_d == nullptr) == (stats_d == nullptr) || !workspace_d)
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_shuffle_adv: bad argument");
+    const int n_mb = (int)(n / mb_size);
+    if (workspace_floats < (int64_t)std::min(n_epochs, kShuffleKeys) * n_mb * kAdvParts * 4 ||
+        (int64_t)std::min(n_epochs, kShuffleKeys) * n_mb > 65535)
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_shuffle_adv: workspace too small");
+    int b = 1;
+    while (((int64_t)1 << b) < n) ++b;
+    const int h = (b + 1) / 2;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    double* part = reinterpret_cast<double*>(workspace_d);
+    for (int e0 = 0; e0 < n_epochs; e0 += kShuffleKeys) {
+        const int ne = n_epochs - e0 < kShuffleKeys ? n_epochs - e0 : kShuffleKeys;
+        ShuffleKeys K{};
+        for (int j = 0; j < ne; ++j) K.k[j] = keys_h[e0 + j];
+        const int k = ne * n_mb;  // minibatches of these epochs
+        hipLaunchKernelGGL(k_shuffle_adv_partial, dim3(kAdvParts, k), dim3(kAdvThreads), 0, st, adv_d, n, h, K,
+                           mb_size, n_mb, perm_d + (int64_t)e0 * n, part);
+        if (stats_d)
+            hipLaunchKernelGGL(k_adv_stats, dim3((k + 255) / 256), dim3(256), 0, st, part, mb_size, k,
+                               stats_d + (int64_t)e0 * n_mb * 2);
+        else
+            hipLaunchKernelGGL(k_adv_sums, dim3((k + 255) / 256), dim3(256), 0, st, part, k,
+                               sums_d + (int64_t)e0 * n_mb * 2);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));

@@ -1756,15 +1756,35 @@ __global__ void k_gae(int T, int N, const float* __restrict__ rew, const float* 
     float last = 0.0f;
     float nv = next_value[n];
     float nnt = 1.0f - next_done[n];
-    for (int t = T - 1; t >= 0; --t) {
-        size_t i = (size_t)t * N + n;
-        float v = val[i];
-        float delta = (rew[i] + (gamma * nv) * nnt) - v;
-        last = delta + ((gl * nnt) * last);
-        adv[i] = last;
-        ret[i] = last + v;
-        nv = v;
-        nnt = 1.0f - dones[i];
+    // the scan is serial in t, its loads are not: each chunk of kGaeChunk
+    // steps loads all its rewards / values / dones before the dependent chain
+    // (one memory round trip per chunk instead of per step: 35 -> ~8 us for
+    // T = 64, N = 4096)
+    constexpr int kGaeChunk = 16;
+    for (int hi = T; hi > 0; hi -= kGaeChunk) {
+        const int lo = hi - kGaeChunk > 0 ? hi - kGaeChunk : 0;
+        float r[kGaeChunk], v[kGaeChunk], d[kGaeChunk];
+#pragma unroll
+        for (int k = 0; k < kGaeChunk; ++k) {
+            const int t = hi - 1 - k;
+            const size_t i = (size_t)(t >= lo ? t : lo) * N + n;
+            r[k] = rew[i];
+            v[k] = val[i];
+            d[k] = dones[i];
+        }
+#pragma unroll
+        for (int k = 0; k < kGaeChunk; ++k) {
+            const int t = hi - 1 - k;
+            if (t >= lo) {  // (no break: the loop stays unrolled, r / v / d in registers)
+                const size_t i = (size_t)t * N + n;
+                const float delta = (r[k] + (gamma * nv) * nnt) - v[k];
+                last = delta + ((gl * nnt) * last);
+                adv[i] = last;
+                ret[i] = last + v[k];
+                nv = v[k];
+                nnt = 1.0f - d[k];
+            }
+        }
     }
 }
 

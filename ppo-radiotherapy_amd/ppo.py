@@ -315,26 +315,38 @@ class PPOTrainer:
         self._policy_counter += count
         self._done_valid = True
 
+    @staticmethod
+    def _row_ptr(t: torch.Tensor, row: int) -> int:
+        """Device address of t[row] without building the view (a CUDA view op
+        runs a device guard: two HIP calls each, on the host's critical path
+        between a synchronise and the rollout call's first launch)."""
+        return t.data_ptr() + row * t.stride(0) * t.element_size()
+
     def _rollout_struct(self, first: int, count: int):
-        """rt_policy_rollout for storage rows first .. first+count-1."""
+        """rt_policy_rollout for storage rows first .. first+count-1 (one
+        cached struct, refilled: the call's host time before its first launch
+        is part of every timed window)."""
         env = self.env
-        ro = _lib.RtPolicyRollout()
+        ro = getattr(self, "_ro_cache", None)
+        if ro is None:
+            ro = self._ro_cache = _lib.RtPolicyRollout()
+            ro.step.params = ctypes.cast(self._policy_ptrs, ctypes.POINTER(ctypes.c_void_p))
+            ro.step.n_params = 13
         st = ro.step
-        st.params = ctypes.cast(self._policy_ptrs, ctypes.POINTER(ctypes.c_void_p))
-        st.n_params = 13
+        rp = self._row_ptr
         st.obs_in = env.obs.data_ptr()
         st.done_in = env.terminated.data_ptr() if self._done_valid else None
-        st.obs_store = self.obs[first].data_ptr()
-        st.done_store = self.dones[first].data_ptr()
-        st.act_store = self.actions[first].data_ptr()
-        st.logp_store = self.logprobs[first].data_ptr()
-        st.value_store = self.values[first].data_ptr()
+        st.obs_store = rp(self.obs, first)
+        st.done_store = rp(self.dones, first)
+        st.act_store = rp(self.actions, first)
+        st.logp_store = rp(self.logprobs, first)
+        st.value_store = rp(self.values, first)
         st.seed = self._policy_seed
         st.counter = self._policy_counter
         st.env_id_base = self.rank * self.N
         ro.n_steps = count
-        ro.reward_store = self.rewards[first].data_ptr()
-        ro.info_store = self.infos[first].data_ptr()
+        ro.reward_store = rp(self.rewards, first)
+        ro.info_store = rp(self.infos, first)
         return ro
 
     def _sync_next(self):
@@ -492,28 +504,27 @@ class PPOTrainer:
         keys = (ctypes.c_uint64 * epochs)(*[int(torch.randint(0, 2 ** 62, (1,), generator=self._host_gen).item())
                                             for _ in range(epochs)])
         perm = self._perm_buf[:epochs]
-        _lib.check(L.rt_ppo_shuffle_epochs(self.batch_size, epochs, keys, perm.data_ptr(), stream),
-                   "rt_ppo_shuffle_epochs")
+        if not self.cfg.norm_adv:
+            _lib.check(L.rt_ppo_shuffle_epochs(self.batch_size, epochs, keys, perm.data_ptr(), stream),
+                       "rt_ppo_shuffle_epochs")
+            stats = None
+        else:
+            # the shuffles and the minibatch statistics in one pass (rt_ppo_shuffle_adv)
+            k = epochs * n_mb
+            stats = self._adv_stats_buf[:k]
+            sums = self._adv_sums[:k] if self.collective else None
+            _lib.check(L.rt_ppo_shuffle_adv(self.batch_size, epochs, keys, perm.data_ptr(), self._b_adv.data_ptr(),
+                                            self.minibatch_size, _lib.ptr(sums),
+                                            None if self.collective else stats.data_ptr(), self._ws.data_ptr(),
+                                            self._ws.numel(), stream), "rt_ppo_shuffle_adv")
+            if self.collective:
+                # this rank's (sum, sum of squares) per minibatch -> ONE all-reduce
+                # of [k, 2] f64 -> global (mean, std) over mbs x world rows
+                dist.all_reduce(sums)
+                _lib.check(L.rt_ppo_adv_finalize(sums.data_ptr(), self.minibatch_size * self.world, k,
+                                                 stats.data_ptr(), stream), "rt_ppo_adv_finalize")
         if self.record_perms is not None:  # test hook: the epochs' minibatch rows
             self.record_perms.extend(p.clone() for p in perm)
-        if not self.cfg.norm_adv:
-            return perm, None
-        k = epochs * n_mb
-        stats = self._adv_stats_buf[:k]
-        if self.collective:
-            # this rank's (sum, sum of squares) per minibatch -> ONE all-reduce
-            # of [k, 2] f64 -> global (mean, std) over mbs x world rows
-            sums = self._adv_sums[:k]
-            _lib.check(L.rt_ppo_adv_sums(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, k,
-                                         sums.data_ptr(), self._ws.data_ptr(), self._ws.numel(), stream),
-                       "rt_ppo_adv_sums")
-            dist.all_reduce(sums)
-            _lib.check(L.rt_ppo_adv_finalize(sums.data_ptr(), self.minibatch_size * self.world, k,
-                                             stats.data_ptr(), stream), "rt_ppo_adv_finalize")
-            return perm, stats
-        _lib.check(L.rt_ppo_adv_stats(self._b_adv.data_ptr(), perm.data_ptr(), self.minibatch_size, k,
-                                      stats.data_ptr(), self._ws.data_ptr(), self._ws.numel(), stream),
-                   "rt_ppo_adv_stats")
         return perm, stats
 
     def _update_fused(self):

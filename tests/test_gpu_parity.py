@@ -254,8 +254,10 @@ def test_large_batch_vs_oracle(dev):
 
 
 # ----------------------------------------------------------------- GAE
-def test_gae_matches_torch_loop(dev):
-    T, N = 37, 513
+@pytest.mark.parametrize("T,N", [(37, 513), (64, 4096), (1, 3), (2048, 16)])
+def test_gae_matches_torch_loop(dev, T, N):
+    """rt_gae (the reverse scan loading kGaeChunk steps ahead, ragged last
+    chunk) vs train.py:163-181's loop."""
     g = torch.Generator(device="cpu").manual_seed(0)
     rew = torch.randn(T, N, generator=g).to(dev)
     val = torch.randn(T, N, generator=g).to(dev)

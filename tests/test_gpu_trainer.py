@@ -404,3 +404,43 @@ def test_update_call_equals_grad_plus_adam(max_norm):
         else:
             torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-9, msg=name)
     assert not torch.equal(got[0], start[0])  # the update moved the parameters
+
+
+@pytest.mark.parametrize("n,mb,epochs", [(262144, 32768, 10), (8192, 2048, 3), (3000, 1000, 33)])
+def test_shuffle_adv_equals_separate_calls(n, mb, epochs):
+    """rt_ppo_shuffle_adv (the epochs' permutations and the minibatch
+    advantage statistics in one pass) is bitwise rt_ppo_shuffle_epochs +
+    rt_ppo_adv_stats, and its sums form is bitwise rt_ppo_adv_sums (33
+    epochs: two key batches)."""
+    import ctypes
+
+    from ppo_radiotherapy_amd import _lib
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = torch.device("cuda")
+    L = _lib.load()
+    adv = (torch.randn(n, generator=torch.Generator().manual_seed(3)) * 2 + 0.3).to(dev)
+    keys = (ctypes.c_uint64 * epochs)(*[(0x9E3779B97F4A7C15 * (e + 1)) & (2 ** 62 - 1) for e in range(epochs)])
+    k = epochs * (n // mb)
+    ws = torch.empty(128 * k, device=dev)
+    p1, p2 = torch.empty((epochs, n), dtype=torch.int64, device=dev), torch.empty((epochs, n), dtype=torch.int64, device=dev)
+    s1, s2 = torch.empty((k, 2), device=dev), torch.empty((k, 2), device=dev)
+    q1, q2 = torch.empty((k, 2), dtype=torch.float64, device=dev), torch.empty((k, 2), dtype=torch.float64, device=dev)
+    _lib.check(L.rt_ppo_shuffle_epochs(n, epochs, keys, p1.data_ptr(), None), "shuffle_epochs")
+    _lib.check(L.rt_ppo_adv_stats(adv.data_ptr(), p1.data_ptr(), mb, k, s1.data_ptr(), ws.data_ptr(), ws.numel(),
+                                  None), "adv_stats")
+    _lib.check(L.rt_ppo_adv_sums(adv.data_ptr(), p1.data_ptr(), mb, k, q1.data_ptr(), ws.data_ptr(), ws.numel(),
+                                 None), "adv_sums")
+    _lib.check(L.rt_ppo_shuffle_adv(n, epochs, keys, p2.data_ptr(), adv.data_ptr(), mb, None, s2.data_ptr(),
+                                    ws.data_ptr(), ws.numel(), None), "shuffle_adv stats")
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2) and torch.equal(s1, s2)
+    p2.zero_()
+    _lib.check(L.rt_ppo_shuffle_adv(n, epochs, keys, p2.data_ptr(), adv.data_ptr(), mb, q2.data_ptr(), None,
+                                    ws.data_ptr(), ws.numel(), None), "shuffle_adv sums")
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2) and torch.equal(q1, q2)
+    assert torch.equal(p1[0].sort().values, torch.arange(n, device=dev))  # a permutation
+    assert L.rt_ppo_shuffle_adv(n, epochs, keys, p2.data_ptr(), adv.data_ptr(), mb, q2.data_ptr(), s2.data_ptr(),
+                                ws.data_ptr(), ws.numel(), None) == -1  # exactly one output form

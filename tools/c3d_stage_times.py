@@ -19,9 +19,13 @@ lib = assets.synthetic_library((S, S, S), 1000, 0)
 r = bench.c3d_roofline(dev, lib, (S, S, S))
 for prec, st in (("f32", r["stages"]), ("bf16x3", r["bf16x3"]["stages"])):
     for k, v in st.items():
-        print(f"{prec:7s} {k}: fwd {v['forward_ms']:.3f} ms {v['forward_tflops']:.1f} TF | train fwd "
-              f"{v['train_forward_ms']:.3f} | wgrad {v['wgrad_ms']:.3f} ({v['wgrad_tflops']:.1f})"
-              + (f" | dgrad {v['dgrad_ms']:.3f} ({v['dgrad_tflops']:.1f})" if "dgrad_ms" in v else ""))
-print(f"f32 forward {r['forward']['ms']:.3f} ms = {r['forward']['achieved']:.1f} TF ({r['forward']['frac']:.3f}); "
-      f"train pass {r['train_pass']['ms']:.3f} ms = {r['train_pass']['achieved']:.1f} TF")
+        print(f"{prec:7s} {k}: fwd {v['forward_ms']:.3f} ms"
+              + (f" ({v['forward_frac']:.3f} of f32 peak executed)" if "forward_frac" in v else "")
+              + f" | train fwd {v['train_forward_ms']:.3f} | wgrad {v['wgrad_ms']:.3f}"
+              + (f" (VALU {v['wgrad_valu_frac']:.3f})" if "wgrad_valu_frac" in v else "")
+              + (f" | dgrad {v['dgrad_ms']:.3f}" if "dgrad_ms" in v else "")
+              + (f" ({v['dgrad_frac']:.3f})" if "dgrad_frac" in v else ""))
+print(f"f32 forward {r['forward']['ms']:.3f} ms = {r['forward']['achieved']:.1f} TF executed ({r['forward']['frac']:.3f}); "
+      f"train pass {r['train_pass']['ms']:.3f} ms ({r['train_pass']['frac']:.3f} executed); "
+      f"bf16x3 train pass {r['bf16x3']['train_pass_ms']:.3f} ms")
 print(json.dumps(r))

@@ -52,3 +52,15 @@ out = {"window_us": us(t0, t1), "per_step_us": us(t0, t1) / K,
        "handoff_gap_us_max": max(gaps), "steps_per_step_us": us(d0, d1) / K}
 for k, v in out.items():
     print(f"{k:24s} {v:10.2f}" if isinstance(v, float) else f"{k:24s} {v}")
+# the host side of the window's head and tail: every HIP API call between the
+# opening synchronise and the first kernel, and after the last launch
+print("-- HIP calls from t0 (us: start, end, function); first kernel at", round(us(t0, first), 2))
+for h in hs:
+    s0, e0 = int(h["Start_Timestamp"]), int(h["End_Timestamp"])
+    if t0 - 50_000 <= s0 <= first + 20_000:
+        print(f"  {us(t0, s0):9.2f} {us(t0, e0):9.2f}  {h['Function']}")
+print("-- HIP calls around the last kernel end (", round(us(t0, last_end), 2), ") and t1 (", round(us(t0, t1), 2), ")")
+for h in hs:
+    s0, e0 = int(h["Start_Timestamp"]), int(h["End_Timestamp"])
+    if last_end - 60_000 <= e0 <= t1 + 1_000:
+        print(f"  {us(t0, s0):9.2f} {us(t0, e0):9.2f}  {h['Function']}")

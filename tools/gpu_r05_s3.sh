@@ -8,6 +8,8 @@ cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 O=gpurun_out/r05_s3
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_trainer.py tests/test_gpu_parity.py -k "gae or shuffle or update_call or termination" > $O/pytest_upd.log 2>&1 || { tail -40 $O/pytest_upd.log; exit 1; }
+tail -1 $O/pytest_upd.log
 RT_LIB_PATH=_variants/librtenv_w256.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_c3d.py > $O/pytest_c3d_w256.log 2>&1 || { tail -40 $O/pytest_c3d_w256.log; exit 1; }
 tail -1 $O/pytest_c3d_w256.log
 for v in base w256; do
