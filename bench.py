@@ -120,9 +120,10 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=0)
     ap.add_argument("--step-mode", choices=["dense", "incremental"], default="dense",
                     help="env step formulation measured as `value` (the other is reported beside it)")
-    ap.add_argument("--rollout-groups", type=int, default=2, choices=[0, 1, 2, 3, 4],
+    ap.add_argument("--rollout-groups", type=int, default=2, choices=[0, 1, 2, 3, 4, 16],
                     help="dense mode: env groups of the rollout call (2 = two pipelined streams, "
-                         "0 = one persistent launch with a per-env dense pass)")
+                         "0 = one persistent launch with a per-env dense pass, 16 = RT_ROLLOUT_FLOW: the "
+                         "dataflow rollout)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
     ap.add_argument("--conv-precision", choices=["f32", "bf16x3"], default="f32",

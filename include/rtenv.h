@@ -306,6 +306,15 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* 
  * returns RT_ELIMIT only when the per-wave LDS region cannot hold even the
  * policy's activations. */
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
+/* rt_env_set_rollout_groups value of the dataflow rollout (dense visionless
+ * handles): the call runs as two concurrent persistent launches -- a chain
+ * kernel (finish, policy, pose, march; the parameters staged once per call)
+ * and the dose stream -- handing each env's step over through per-env device
+ * counters instead of kernel boundaries (no per-turn hand-off, no per-step
+ * parameter staging).  Same bits as the stepwise launches.  A hand-off wait
+ * that runs out (~1 s: hardware fault) makes the next rollout call return
+ * RT_EDEVICE. */
+#define RT_ROLLOUT_FLOW 16
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */

@@ -23,6 +23,7 @@ INFO_NAMES = {
 }
 INFO_W = 20
 STEP_DENSE, STEP_INCREMENTAL = 0, 1
+ROLLOUT_FLOW = 16  # RT_ROLLOUT_FLOW: rt_env_set_rollout_groups value of the dataflow rollout
 PPO_PREC = {"f32": 0, "bf16x3": 1}  # RT_PPO_PREC_* (rt_ppo_hparams.precision)
 CONV_PREC = {"f32": 0, "bf16x3": 1}  # RT_CONV_PREC_* (rt_conv_layer.precision)
 

@@ -8,7 +8,9 @@ back to back; plan slots in the global scratch row for 1000 and 12000 voxel
 tumours).  Dense step mode: the stepwise launches of two env groups
 pipelined over two library streams (and the one-group variant), and the
 persistent dense rollout (groups 0: one launch, each wave streaming its own
-env's lung segment every step)."""
+env's lung segment every step), and the dataflow rollout (groups 16 =
+RT_ROLLOUT_FLOW: a persistent chain kernel and a persistent dose kernel
+handing every env's step over through device counters)."""
 import os
 import sys
 from types import SimpleNamespace
@@ -64,7 +66,7 @@ def _compare(a, b, it, loose_dose_lung=False):
     for name in ("obs", "dones", "actions", "logprobs", "values", "rewards", "infos"):
         x, y = getattr(a, name), getattr(b, name)
         if name == "infos" and loose_dose_lung:
-            # the persistent dense rollout sums doses.lung in another order
+            # the persistent dense and the dataflow rollouts sum doses.lung in another order
             # than k_dense's slices (f64, then f32): within f32 rounding
             c = 5  # RT_INFO_DOSE_LUNG
             torch.testing.assert_close(x[..., c], y[..., c], rtol=2e-6, atol=1e-6)
@@ -82,7 +84,8 @@ def _compare(a, b, it, loose_dose_lung=False):
                                                    ("incremental", 12000, 0), ("dense", 0, 2),
                                                    ("dense", 1000, 2), ("dense", 0, 3),
                                                    ("dense", 1000, 4), ("dense", 0, 1),
-                                                   ("dense", 0, 0), ("dense", 12000, 0)])
+                                                   ("dense", 0, 0), ("dense", 12000, 0),
+                                                   ("dense", 0, 16), ("dense", 1000, 16), ("dense", 12000, 16)])
 def test_rollout_call_is_bitwise_the_stepwise_rollout(step_mode, big, groups):
     from ppo_radiotherapy_amd import assets
 
@@ -106,7 +109,7 @@ def test_rollout_call_is_bitwise_the_stepwise_rollout(step_mode, big, groups):
             a.rollout_steps(first, count)
             b.rollout_steps(first, count)
         torch.cuda.synchronize()
-        _compare(a, b, it, loose_dose_lung=step_mode == "dense" and groups == 0)
+        _compare(a, b, it, loose_dose_lung=step_mode == "dense" and groups in (0, 16))
         ended += int(a.dones.sum().item())
         seen_big += int(a.env.get_state()[2].eq(lib.n_tumours - 1).sum().item())
     assert ended >= n  # every env's first episode ended inside the compared steps
