@@ -2955,8 +2955,12 @@ constexpr int wino_dg_u_floats() {
     return 16 * 64 * 4 * (CPG / 4);
 }
 
+// groups 4 (conv3): 4 waves per SIMD (<= 128 VGPRs, no spills; left free the
+// compiler took 130 and 3 waves); groups 2 stays at 2 (167 VGPRs, two
+// 4-wave blocks per CU by LDS: 6-wave blocks for 3 per SIMD ran slower, §10)
 template <int CPG, int NTH>
-__global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(CPG == 4 ? 4 : 1))) void k_dgrad_wino(
+    WinoDgradParams P) {
     extern __shared__ float xs[];
     constexpr int NW = NTH / 64;
     constexpr int COG = CPG;     // groups 2 / 4: 8 / 4 output channels per group, as many inputs
@@ -3054,8 +3058,13 @@ __global__ __launch_bounds__(NTH) void k_dgrad_wino(WinoDgradParams P) {
     const int64_t xchan = (int64_t)g.D * g.H * g.W;
     const bool lane_ci = 4 * gq < CPG;
     float* dxb = P.dx + ((int64_t)b * CO + grp * CPG + (lane_ci ? 4 * gq : 0)) * xchan;
-    for (int qz = q0; qz < q1; ++qz) {
-        for (int it = wave; it < items; it += NW) {
+    // the chunk's (tile row, item) pairs flattened over the waves: no wave
+    // takes more than one item beyond any other (conv3: 4 items per row on 4
+    // waves is even either way; the flat loop also lets it run 4 waves per SIMD)
+    const int nwork = (q1 - q0) * items;
+    for (int k = wave; k < nwork; k += NW) {
+        {
+            const int qz = q0 + k / items, it = k - (qz - q0) * items;
             const int ti = min(16 * it + n, ntile - 1);
             const int qy = ti / P.QW, qx = ti - qy * P.QW;
             const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
