@@ -2869,8 +2869,8 @@ int rt_env_step_policy(rt_env* env, const rt_policy_step* ps, float* obs_d, floa
 // per env.  The groups take turns on k_dense (each group's k_dense waits for
 // the other's previous one), so while one group streams its dose rows the
 // other runs its latency-bound kernels beside it; only the first policy
-// kernel and the last finish are not hidden.  Fork and join with the
-// caller's stream are events; nothing synchronises the host.
+// kernel and the last finish are not hidden.  Group 0 runs on the caller's
+// stream, the others fork and join by events; nothing synchronises the host.
 // ---------------------------------------------------------------------------
 static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
                          hipStream_t s) {
@@ -2887,10 +2887,13 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
     hipStream_t S[kMaxRolloutGroups];
     hipEvent_t* dense_ev = env->pev + 1;
     hipEvent_t* join_ev = env->pev + 1 + kMaxRolloutGroups;
+    // group 0 runs on the caller's stream itself (ordered after the caller's
+    // work without a fork, so the call's first kernel is its first packet);
+    // the other groups fork from it onto library streams and join back
     for (int g = 0; g < G; ++g) S[g] = s;
     if (piped) {
         RT_HIP(hipEventRecord(env->pev[0], s));
-        for (int g = 0; g < G; ++g) {
+        for (int g = 1; g < G; ++g) {
             S[g] = env->pipe[g];
             RT_HIP(hipStreamWaitEvent(S[g], env->pev[0], 0));
         }
@@ -2946,7 +2949,7 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
         }
     }
     if (piped) {
-        for (int g = 0; g < G; ++g) {
+        for (int g = 1; g < G; ++g) {
             RT_HIP(hipEventRecord(join_ev[g], S[g]));
             RT_HIP(hipStreamWaitEvent(s, join_ev[g], 0));
         }
