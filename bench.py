@@ -127,7 +127,7 @@ def parse():
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
     ap.add_argument("--conv-precision", choices=["f32", "bf16x3"], default="f32",
-                    help="vision: conv1's forward products (rt_conv_set_precision) in the rollout and the update")
+                    help="vision: conv1's forward products (rt_conv_layer.precision) in the rollout and the update")
     ap.add_argument("--update-precision", choices=["f32", "bf16x3"], default="f32",
                     help="the fused update's 64x64 layer products (ppo_update_ms); the other is timed beside it")
     ap.add_argument("--rocprof-stats", default=None,

@@ -71,7 +71,7 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// bf16x3 products (rt_conv_set_precision(RT_CONV_PREC_BF16X3), conv1 forward):
+// bf16x3 products (rt_conv_layer.precision = RT_CONV_PREC_BF16X3: the forward and grouped data-gradient ring kernels):
 // x = hi + lo + e, hi = bf16(x), lo = bf16(x - hi), both round to nearest even
 // (|e| <= 2^-17 |x|); a product is hi*hi + hi*lo + lo*hi in three
 // v_mfma_f32_16x16x32_bf16 (16 cycles each, f32 accumulate) against one
