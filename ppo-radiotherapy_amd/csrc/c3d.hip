@@ -897,7 +897,8 @@ int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* ro
 #ifndef RT_WINO_C1_NTH
 #define RT_WINO_C1_NTH 256
 #endif
-constexpr int kWinoC1Nth = RT_WINO_C1_NTH;  // threads per block of conv1's Winograd forward
+constexpr int kWinoC1Nth = RT_WINO_C1_NTH;
+  // threads per block of conv1's Winograd forward
 
 template <int CPG>
 constexpr int wino_u_floats() {  // U in LDS: 16 columns x 64 lanes x 4 xi_z x CPG / 4 quads
@@ -934,6 +935,7 @@ void k_conv_wino(WinoParams P) {
     extern __shared__ float xs[];
     constexpr int NW = NTH / 64;
     constexpr int NS = CPG / 4;  // channel quads (MFMA k-steps) per xi
+    constexpr bool kWinoPrio = CPG == 4 && COG == 16;  // conv1
     const Geom& g = P.rg.g;
     const int SLOT = P.rg.SLOT;
     const int b = blockIdx.z / P.G, grp = blockIdx.z - b * P.G;
@@ -1030,6 +1032,12 @@ void k_conv_wino(WinoParams P) {
                 float v[NS][32];  // [s][dz][dy][kx] -> [s][xz][xy][kx], xi_x = 2h + kx
                 int xo = xoff;
                 asm volatile("" : "+v"(xo));  // the halves' patch reads stay separate (no CSE)
+                // conv1: the input transform at base issue priority, the MFMA
+                // columns raised, so waves in their column phase keep the MFMA
+                // pipe fed (conv1 forward 2.32 -> 2.29 ms per 512 samples,
+                // training forward 2.32 -> 2.28; conv2's training forward lost
+                // 3 % with it: r05_s17)
+                if constexpr (kWinoPrio) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
 #pragma unroll
@@ -1120,6 +1128,7 @@ void k_conv_wino(WinoParams P) {
                             }
                     }
                 };
+                if constexpr (kWinoPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int c = 0; c <= 8; ++c) {  // column c = kx * 4 + xy of this half
                     f4 m[4];
@@ -3074,6 +3083,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(CPG == 4 ? 
             for (int h = 0; h < 2; ++h) {
                 float v[NS][32];
                 int base = 0;
+                __builtin_amdgcn_s_setprio(0);  // patch + input transform (conv2 1.357 -> 1.335, conv3 0.150 -> 0.144 ms: r05_s18)
                 asm volatile("" : "+v"(base));  // the halves' window reads stay separate (no CSE)
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
@@ -3132,6 +3142,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(CPG == 4 ? 
                         v[s][24 + j] = d1 - d3;
                     }
                 }
+                __builtin_amdgcn_s_setprio(1);  // the MFMA columns at raised issue priority (as conv1's forward)
                 f4 pm[4];
                 auto column_sums = [&](const f4 (&m)[4], int xx, int xy) {
                     const f4 t0 = (m[0] + m[1]) + m[2], t1 = (m[1] - m[2]) - m[3];

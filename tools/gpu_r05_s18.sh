@@ -1,0 +1,18 @@
+#!/bin/bash
+# r05 session 18: conv1's forward with MFMA-phase issue priority (in-tree) --
+# C3D gates; the data gradient with the same (dgp variant build) vs without
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+O=gpurun_out/r05_s18
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_c3d.py tests/test_gpu_configs.py > $O/pytest_c3d.log 2>&1 || { tail -40 $O/pytest_c3d.log; exit 1; }
+tail -1 $O/pytest_c3d.log
+for i in 1 2; do
+for v in base dgp; do
+  L=ppo-radiotherapy_amd/librtenv.so; [ $v != base ] && L=_variants/librtenv_$v.so
+  RT_LIB_PATH=$L timeout -k 10 300 python3 tools/c3d_stage_times.py > $O/stages_${v}_$i.txt 2> $O/stages_${v}_$i.err || { tail -20 $O/stages_${v}_$i.err; exit 1; }
+  echo "== $v $i"; grep -v "^{" $O/stages_${v}_$i.txt | grep "f32" | grep -v bf16
+done
+done
+echo ALLDONE
