@@ -2,7 +2,7 @@
 one source recompiled with extra flags, the other objects from the in-tree
 build.
 
-    python tools/build_variant.py NAME c3d.hip -DRT_C3D_EXP=1 [...]
+    python tools/build_variant.py NAME rtenv.hip -DRT_PIPE_DENSE_BPC=4 [...]
     -> _variants/librtenv_NAME.so
     python tools/build_variant.py NAME c3d.hip --rev HEAD [...]
     (the source as of a git revision: before/after A/B of an edit)
