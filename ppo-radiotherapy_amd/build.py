@@ -29,8 +29,12 @@ HIPCC_FLAGS = [
 # constants of the pose update out of k_rollout_policy's step loop and spills
 # them to scratch (reloaded serially inside the sincos chain); without it the
 # kernel fits 128 VGPRs with no spill, and the other kernels' loops are unchanged
-# (register renaming only).
-EXTRA_FLAGS = {SRC: ["-mllvm", "-disable-machine-licm"]}
+# (register renaming only).  c3d.hip: no SLP vectorizer -- it packs f32 adds
+# and FMAs into v_pk_add_f32 / v_pk_fma_f32, which beside MFMAs cost more issue
+# than the scalar pairs (MI355X_MICROARCH.md); without it the conv1 sparse
+# weight gradient runs 3.5 % and the groups-2 data gradient 2 % faster
+# (profiles/r05/r05_s19_c3d_slp.txt).
+EXTRA_FLAGS = {SRC: ["-mllvm", "-disable-machine-licm"], SRCS[3]: ["-fno-slp-vectorize"]}
 OBJ_DIR = os.path.join(PKG, "_obj")
 
 

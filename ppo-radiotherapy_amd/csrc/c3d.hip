@@ -71,6 +71,27 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// f4 sums of MFMA results as four scalar v_add / v_sub: the f4 operators
+// lower to v_pk_add_f32, which beside MFMAs costs ~4x a scalar add's issue
+// (MI355X_MICROARCH.md, 'price of one filler beside MFMAs'); built with
+// -fno-slp-vectorize so the SLP pass does not re-pack them
+__device__ __forceinline__ f4 add4s(f4 a, f4 b) {
+    f4 r;
+    r.x = a.x + b.x;
+    r.y = a.y + b.y;
+    r.z = a.z + b.z;
+    r.w = a.w + b.w;
+    return r;
+}
+__device__ __forceinline__ f4 sub4s(f4 a, f4 b) {
+    f4 r;
+    r.x = a.x - b.x;
+    r.y = a.y - b.y;
+    r.z = a.z - b.z;
+    r.w = a.w - b.w;
+    return r;
+}
+
 // bf16x3 products (rt_conv_layer.precision = RT_CONV_PREC_BF16X3: the forward and grouped data-gradient ring kernels):
 // x = hi + lo + e, hi = bf16(x), lo = bf16(x - hi), both round to nearest even
 // (|e| <= 2^-17 |x|); a product is hi*hi + hi*lo + lo*hi in three
@@ -1086,24 +1107,24 @@ void k_conv_wino(WinoParams P) {
                 // their accumulator registers spill)
                 f4 pm[4];
                 auto column_sums = [&](const f4 (&m)[4], int xx, int xy) {
-                    const f4 t0 = (m[0] + m[1]) + m[2], t1 = (m[1] - m[2]) - m[3];  // A^T along z
+                    const f4 t0 = add4s(add4s(m[0], m[1]), m[2]), t1 = sub4s(sub4s(m[1], m[2]), m[3]);  // A^T along z
                     f4(&S)[2][2] = Sx[xx & 1];
                     if (xy == 0) {  // A^T along y: rows (1 1 1 0), (0 1 -1 -1)
                         S[0][0] = t0;
                         S[0][1] = t1;
                     } else if (xy == 1) {
-                        S[0][0] += t0;
-                        S[0][1] += t1;
+                        S[0][0] = add4s(S[0][0], t0);
+                        S[0][1] = add4s(S[0][1], t1);
                         S[1][0] = t0;
                         S[1][1] = t1;
                     } else if (xy == 2) {
-                        S[0][0] += t0;
-                        S[0][1] += t1;
-                        S[1][0] -= t0;
-                        S[1][1] -= t1;
+                        S[0][0] = add4s(S[0][0], t0);
+                        S[0][1] = add4s(S[0][1], t1);
+                        S[1][0] = sub4s(S[1][0], t0);
+                        S[1][1] = sub4s(S[1][1], t1);
                     } else {
-                        S[1][0] -= t0;
-                        S[1][1] -= t1;
+                        S[1][0] = sub4s(S[1][0], t0);
+                        S[1][1] = sub4s(S[1][1], t1);
                     }
                     if (xy == 0)
                         asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]));
@@ -1117,13 +1138,13 @@ void k_conv_wino(WinoParams P) {
                                 if (xx == 0) {
                                     Y[0][oy][oz] = S[oy][oz];
                                 } else if (xx == 1) {
-                                    Y[0][oy][oz] += S[oy][oz];
+                                    Y[0][oy][oz] = add4s(Y[0][oy][oz], S[oy][oz]);
                                     Y[1][oy][oz] = S[oy][oz];
                                 } else if (xx == 2) {
-                                    Y[0][oy][oz] += S[oy][oz];
-                                    Y[1][oy][oz] -= S[oy][oz];
+                                    Y[0][oy][oz] = add4s(Y[0][oy][oz], S[oy][oz]);
+                                    Y[1][oy][oz] = sub4s(Y[1][oy][oz], S[oy][oz]);
                                 } else {
-                                    Y[1][oy][oz] -= S[oy][oz];
+                                    Y[1][oy][oz] = sub4s(Y[1][oy][oz], S[oy][oz]);
                                 }
                             }
                     }
@@ -3145,24 +3166,24 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(CPG == 4 ? 
                 __builtin_amdgcn_s_setprio(1);  // the MFMA columns at raised issue priority (as conv1's forward)
                 f4 pm[4];
                 auto column_sums = [&](const f4 (&m)[4], int xx, int xy) {
-                    const f4 t0 = (m[0] + m[1]) + m[2], t1 = (m[1] - m[2]) - m[3];
+                    const f4 t0 = add4s(add4s(m[0], m[1]), m[2]), t1 = sub4s(sub4s(m[1], m[2]), m[3]);
                     f4(&S)[2][2] = Sx[xx & 1];
                     if (xy == 0) {
                         S[0][0] = t0;
                         S[0][1] = t1;
                     } else if (xy == 1) {
-                        S[0][0] += t0;
-                        S[0][1] += t1;
+                        S[0][0] = add4s(S[0][0], t0);
+                        S[0][1] = add4s(S[0][1], t1);
                         S[1][0] = t0;
                         S[1][1] = t1;
                     } else if (xy == 2) {
-                        S[0][0] += t0;
-                        S[0][1] += t1;
-                        S[1][0] -= t0;
-                        S[1][1] -= t1;
+                        S[0][0] = add4s(S[0][0], t0);
+                        S[0][1] = add4s(S[0][1], t1);
+                        S[1][0] = sub4s(S[1][0], t0);
+                        S[1][1] = sub4s(S[1][1], t1);
                     } else {
-                        S[1][0] -= t0;
-                        S[1][1] -= t1;
+                        S[1][0] = sub4s(S[1][0], t0);
+                        S[1][1] = sub4s(S[1][1], t1);
                     }
                     if (xy == 0)
                         asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]));
@@ -3176,13 +3197,13 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(CPG == 4 ? 
                                 if (xx == 0) {
                                     Y[0][oy][oz] = S[oy][oz];
                                 } else if (xx == 1) {
-                                    Y[0][oy][oz] += S[oy][oz];
+                                    Y[0][oy][oz] = add4s(Y[0][oy][oz], S[oy][oz]);
                                     Y[1][oy][oz] = S[oy][oz];
                                 } else if (xx == 2) {
-                                    Y[0][oy][oz] += S[oy][oz];
-                                    Y[1][oy][oz] -= S[oy][oz];
+                                    Y[0][oy][oz] = add4s(Y[0][oy][oz], S[oy][oz]);
+                                    Y[1][oy][oz] = sub4s(Y[1][oy][oz], S[oy][oz]);
                                 } else {
-                                    Y[1][oy][oz] -= S[oy][oz];
+                                    Y[1][oy][oz] = sub4s(Y[1][oy][oz], S[oy][oz]);
                                 }
                             }
                     }
