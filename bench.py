@@ -377,12 +377,12 @@ def stream_ceilings(dev, lib_obj, gib: float = 4.0, reps: int = 8) -> dict:
     return out
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r05", "r05_s11_k_dense_persist_pmc.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r05", "r05_s23_k_dense_persist_pmc.json")
 # rocprofv3 --kernel-trace --stats of this bench's default command, committed
 # with a sidecar <csv>.meta.json naming the commit of the tree it was measured
 # on; used (labelled "historical") when --rocprof-stats does not name the
 # stats of the current run
-ROCPROF_FILE = os.path.join(REPO, "profiles", "r05", "r05_s11_kernel_stats.csv")
+ROCPROF_FILE = os.path.join(REPO, "profiles", "r05", "r05_s23_kernel_stats.csv")
 
 
 def load_rocprof(kernel: str, path: str | None = None):
