@@ -142,3 +142,29 @@ def test_rollout_policy_rejects_vision_and_bad_groups():
     with pytest.raises(_lib.RtError, match="visionless"):
         venv.rollout_policy(ro)
     venv.close()
+
+
+@pytest.mark.parametrize("n,groups", [(1, 2), (17, 2), (33, 2), (70, 3), (5, 16), (33, 16)])
+def test_small_handles_rollout_bitwise(n, groups):
+    """Edge sizes of the dense rollout call: a single env, fewer envs than two
+    16-env groups (the call falls back to one group), group boundaries off
+    the block size, and the dataflow launch with fewer envs than chain waves
+    -- each bitwise the stepwise launches over 128 steps (every env passes
+    its t = 100 truncation autoreset)."""
+    from ppo_radiotherapy_amd import assets
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    lib = assets.synthetic_library((40, 36, 44), 60, 2)
+    a = _trainer(True, lib, n, "dense")
+    b = _trainer(False, lib, n, "dense")
+    a.env.set_rollout_groups(groups)
+    T = a.T
+    for it in range(4):
+        a.rollout_steps(0, T)
+        b.rollout_steps(0, T)
+        torch.cuda.synchronize()
+        _compare(a, b, it, loose_dose_lung=groups == 16)
+    assert a.fused_rollout
+    a.env.close()
+    b.env.close()

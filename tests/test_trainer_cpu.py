@@ -311,3 +311,35 @@ def test_vision_micro_batched_update_data_parallel_gloo():
     assert moved > 1e-3, moved
     assert err <= 2e-3 * moved, (err, moved)
     assert np.linalg.norm(local - want) > 20 * err, (np.linalg.norm(local - want), err)
+
+
+def test_rollout_struct_rows_and_refill():
+    """The rt_policy_rollout the trainer hands to rt_env_rollout_policy
+    (ppo.py _rollout_struct): storage-row addresses of the call's first row,
+    the Philox counter of the call, done_in only once terminated is valid --
+    and the cached struct refilled whenever the first row, the count, the
+    done validity or the env's observation buffer changes (the refill is
+    skipped otherwise: host time before the call's first launch)."""
+    import ctypes
+
+    tr = _trainer(16, 0)
+    tr._policy_ptrs = (ctypes.c_void_p * 13)()  # the CPU trainer has no fused policy; the struct still fills
+    env = tr.env
+    env.terminated = torch.zeros(16, dtype=torch.uint8)
+    tr._done_valid = False
+    ro = tr._rollout_struct(0, 8)
+    assert ro.n_steps == 8 and ro.step.done_in is None
+    assert ro.step.obs_in == env.obs.data_ptr()
+    assert ro.step.obs_store == tr.obs.data_ptr() and ro.reward_store == tr.rewards.data_ptr()
+    tr._done_valid = True
+    tr._policy_counter = 5
+    ro = tr._rollout_struct(3, 4)
+    assert ro.n_steps == 4 and ro.step.done_in == env.terminated.data_ptr() and ro.step.counter == 5
+    for name, field in (("obs", ro.step.obs_store), ("dones", ro.step.done_store), ("actions", ro.step.act_store),
+                        ("logprobs", ro.step.logp_store), ("values", ro.step.value_store),
+                        ("rewards", ro.reward_store), ("infos", ro.info_store)):
+        assert field == getattr(tr, name)[3].data_ptr(), name
+    tr._policy_counter = 9  # same call shape: only the counter moves
+    assert tr._rollout_struct(3, 4).step.counter == 9
+    env.obs = env.obs.clone()  # a new observation buffer is picked up
+    assert tr._rollout_struct(3, 4).step.obs_in == env.obs.data_ptr()
