@@ -62,9 +62,12 @@ def main():
     ap.add_argument("--total", type=int, default=25_000_000)
     ap.add_argument("--scratch", default="/tmp/repro_learning")
     ap.add_argument("--step-mode", default=None)
+    ap.add_argument("--seed", type=int, default=None, help="override the config's seed (seed spread)")
     a = ap.parse_args()
     cfg = config_mod.load(a.config)
     cfg.total_timesteps = a.total
+    if a.seed is not None:
+        cfg.seed = a.seed
     if a.step_mode:
         cfg.step_mode = a.step_mode
     cfg = config_mod.derive(cfg)
