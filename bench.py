@@ -33,7 +33,8 @@ Also reported:
                          rewards/termination, touches only the beam's voxels)
   roofline               k_dense (the dominant kernel) vs HBM: HIP events the
                          library records around it on the env stream over
-                         the timed region; traffic from profiles/k_dense_pmc.json
+                         the timed region; traffic from the committed PMC run
+                         (PMC_FILE), rocprofv3's average from ROCPROF_FILE
   steady_state           >= 101 steps (2 x num_steps) with the envs' episode
                          clocks staggered uniformly, so the window carries the
                          t = 100 truncation autoresets a long run pays
