@@ -23,7 +23,7 @@ import os
 import numpy as np
 import torch  # before the library: torch ships the process's libamdhip64
 
-RTENV_ABI_VERSION = 4
+RTENV_ABI_VERSION = 5
 RT_INFO_W = 20  # info row: RT_INFO_* in rtenv.h (0..3 reward_components, 17..19 episode _r / r / l)
 RT_STEP_DENSE, RT_STEP_INCREMENTAL = 0, 1
 

@@ -121,10 +121,9 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=0)
     ap.add_argument("--step-mode", choices=["dense", "incremental"], default="dense",
                     help="env step formulation measured as `value` (the other is reported beside it)")
-    ap.add_argument("--rollout-groups", type=int, default=2, choices=[0, 1, 2, 3, 4, 16],
+    ap.add_argument("--rollout-groups", type=int, default=2, choices=[1, 2, 3, 4],
                     help="dense mode: env groups of the rollout call (2 = two pipelined streams, "
-                         "0 = one persistent launch with a per-env dense pass, 16 = RT_ROLLOUT_FLOW: the "
-                         "dataflow rollout)")
+                         "1 = the stepwise launches on one stream)")
     ap.add_argument("--update-minibatches", type=int, default=0,
                     help="time only this many minibatch steps of the update (0 = all)")
     ap.add_argument("--conv-precision", choices=["f32", "bf16x3"], default="f32",
@@ -862,22 +861,13 @@ def main():
         bytes_launch = a.envs * 20 * V
         bytes_model = ("20 B x V x envs (k_dense_vis: dose read, the four observation channels written -- "
                        "lungs and dose, tumour and beam-view zeroed for k_finish's scatter)")
-    persistent_dense = (not a.vision and not a.env_only and a.step_mode == "dense" and a.rollout_groups == 0)
-    launches = max(kcalls, 1) / K  # launches per step (2: pipelined env groups; 1/K: one persistent launch)
-    if persistent_dense:
-        # one k_rollout_policy<dense> launch per rollout call: each wave streams
-        # its env's lung segment every step (dense_env); its whole duration is
-        # in the first interval, and its bytes are the dense stream's
-        dense_ms = sum(kms.values())
-        kernel_name = "k_rollout_policy<dense>"
-        traffic = load_pmc(grid, a.envs, "k_rollout_policy")
-    else:
-        dense_ms = kms["k_dense"]  # per step: the launches of all env groups
-        kernel_name = "k_dense"
-        if launches > 1.5:  # pipelined: k_dense_persist over half the envs (tools/archive/gpu_dense_persist_pmc.sh)
-            traffic = load_pmc(grid, a.envs // 2, "k_dense_persist")
-        else:  # whole-handle grid launches (tools/archive/gpu_dense_pmc.sh, bench.py --env-only)
-            traffic = load_pmc(grid, a.envs)
+    launches = max(kcalls, 1) / K  # launches per step (2: pipelined env groups)
+    dense_ms = kms["k_dense"]  # per step: the launches of all env groups
+    kernel_name = "k_dense"
+    if launches > 1.5:  # pipelined: k_dense_persist over half the envs (tools/archive/gpu_dense_persist_pmc.sh)
+        traffic = load_pmc(grid, a.envs // 2, "k_dense_persist")
+    else:  # whole-handle grid launches (tools/archive/gpu_dense_pmc.sh, bench.py --env-only)
+        traffic = load_pmc(grid, a.envs)
     achieved = bytes_launch / (dense_ms * 1e-3)  # = per-launch bytes / per-launch duration (per step)
     traffic_steady = traffic_src = None
     if isinstance(traffic, dict):
@@ -919,7 +909,7 @@ def main():
                                           "(read: reduced; copy: + plain 16-B stores, read+write bytes)")
         roof["frac_of_measured_ceiling"] = achieved / cel["read"]
         rmw_ceil = random_rmw_ceiling(dev, _lib.load(), a.envs * V)
-        if mlines is not None and a.rollout_groups > 0:
+        if mlines is not None:
             # the beam march (draw_line.py:49-100 + environment.py:107-110) runs in
             # k_step_policy (policy + pose + march, one wave per env): its random
             # 128-B line read-modify-writes against the measured random-RMW rate

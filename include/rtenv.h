@@ -41,10 +41,12 @@
 extern "C" {
 #endif
 
-#define RTENV_ABI_VERSION 4  /* 2: rt_env_config.struct_size (first member); 3: rt_adam_step grad_div,
+#define RTENV_ABI_VERSION 5  /* 2: rt_env_config.struct_size (first member); 3: rt_adam_step grad_div,
                                 rt_env_set_dense_handoff removed; 4: arithmetic per call
                                 (rt_ppo_hparams.precision, rt_conv_layer.precision) instead of the
-                                process-wide rt_ppo_/rt_conv_set_precision */
+                                process-wide rt_ppo_/rt_conv_set_precision; 5: RT_ROLLOUT_FLOW and
+                                the dense persistent rollout (groups 0 on dense handles) removed,
+                                rt_ppo_status added */
 
 enum {
     RT_OK = 0,
@@ -296,25 +298,11 @@ typedef struct rt_policy_rollout {
 
 int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* rollout, float* obs_d, uint8_t* terminated_d,
                           void* stream);
-/* Env groups of the dense-mode rt_env_rollout_policy: 2..4 (pipelined
- * library streams taking turns on k_dense in a ring; default 2), 1 (every
- * launch on the caller's stream) or 0 (one persistent launch: each env's wave
- * runs policy, march, the dense lung reduction of its own row and the finish,
- * step after step).  Setting 0 allocates the persistent kernel's global plan
- * scratch ([N][2 * largest tumour] f32) when the library's largest tumour
- * exceeds its LDS share -- a setup call, not graph-capturable; the rollout
- * returns RT_ELIMIT only when the per-wave LDS region cannot hold even the
- * policy's activations. */
+/* Env groups of the rollout call.  Dense step mode: 2..4 (pipelined library
+ * streams taking turns on k_dense in a ring; default 2) or 1 (every launch on
+ * the caller's stream).  Incremental step mode: 0, its one persistent launch
+ * (the only value it takes).  RT_EINVAL on any other value. */
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups);
-/* rt_env_set_rollout_groups value of the dataflow rollout (dense visionless
- * handles): the call runs as two concurrent persistent launches -- a chain
- * kernel (finish, policy, pose, march; the parameters staged once per call)
- * and the dose stream -- handing each env's step over through per-env device
- * counters instead of kernel boundaries (no per-turn hand-off, no per-step
- * parameter staging).  Same bits as the stepwise launches.  A hand-off wait
- * that runs out (~1 s: hardware fault) makes the next rollout call return
- * RT_EDEVICE. */
-#define RT_ROLLOUT_FLOW 16
 
 /* GAE reverse scan (train.py:163-181), one lane per env, f32 in [T][N] layout:
  * adv[t] = delta + gamma*lambda*(1-done[t+1])*adv[t+1]; ret = adv + values. */
@@ -397,6 +385,15 @@ int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_
                   const rt_ppo_hparams* hp, float* flat_param_d, float* flat_grad_d, float* exp_avg_d,
                   float* exp_avg_sq_d, int64_t n_flat, int64_t step0, double lr, float* workspace_d,
                   int64_t workspace_floats, float* stats_d, float* stats_accum_d, void* stream);
+
+/* RT_OK, or RT_EDEVICE when an rt_ppo_update on the current device lost the
+ * grid arrival of its fused reduce + Adam launch (the grid was not
+ * co-resident): that launch and every later one of the update then wrote no
+ * parameter, moment or gradient, so the state is the last complete
+ * minibatch's.  Sticky; every later rt_ppo_* call also returns RT_EDEVICE.
+ * Trainers call it after synchronising the update's stream, before saving a
+ * checkpoint. */
+int rt_ppo_status(void);
 
 /* Per-epoch helpers of the update: perm_d[i] = a keyed pseudo-random
  * permutation of [0, n) (train.py:195's shuffle); stats_d[n_mb][2] = mean and

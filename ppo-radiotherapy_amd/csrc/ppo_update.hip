@@ -1167,6 +1167,15 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
         if (lane == 0) __hip_atomic_store(Q.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
+    // A block of this launch or of an earlier one that gave up raised the
+    // flag before it left: every block that arrives after it -- late in this
+    // launch, or in the update's later launches, which start after it ended --
+    // reads it here and writes nothing either, so a lost arrival leaves the
+    // whole update's state as the last complete minibatch left it (never a
+    // partly updated parameter set); rt_ppo_status reports it after the sync.
+    int faulted = 0;
+    if (lane == 0) faulted = __hip_atomic_load(Q.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (__shfl(faulted, 0, 64)) return;
     if (!upd) return;
     const float g = a * coef;
     A.grad[i] = g;
@@ -1466,22 +1475,35 @@ int adam_launch(int64_t n, float* p, float* g, float* m, float* v, int64_t step,
     return RT_OK;
 }
 
-// The sticky fault flag of k_ppo_reduce_adam: one host-mapped int per
-// process (a lost grid arrival on any device sets it); nullptr when the host
+// The sticky fault flag of k_ppo_reduce_adam: one host-mapped int per device
+// (a lost grid arrival on that device sets it); nullptr when the host
 // allocation failed (rt_ppo_update then runs the two-kernel form)
 int* reduce_adam_fault() {
-    static int* flag = [] {
-        void* p = nullptr;
-        if (hipHostMalloc(&p, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return (int*)nullptr;
-        *static_cast<volatile int*>(p) = 0;
-        return static_cast<int*>(p);
-    }();
-    return flag;
+    static std::mutex mu;
+    static std::map<int, int*> flags;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    const auto f = flags.find(dev);
+    if (f != flags.end()) return f->second;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) p = nullptr;
+    if (p) *static_cast<volatile int*>(p) = 0;
+    return flags[dev] = static_cast<int*>(p);
 }
 
 bool reduce_adam_faulted() {
     int* f = reduce_adam_fault();
     return f && *static_cast<volatile int*>(f) != 0;
+}
+
+// Debug knob (tests): RT_PPO_UPDATE_SPLIT=1 makes rt_ppo_update run its
+// two-kernel form (k_ppo_grad + k_ppo_reduce, then k_adam) -- the path a
+// failed occupancy check or a missing host-mapped flag selects -- so the
+// test suite covers it on hardware where the fused form always runs.
+bool force_split_update() {
+    const char* v = std::getenv("RT_PPO_UPDATE_SPLIT");
+    return v && v[0] == '1';
 }
 
 // k_ppo_reduce_adam's grid arrival needs all kReduceBlocks blocks resident at
@@ -1571,7 +1593,7 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
     int* fault_d = nullptr;
     if (fault_h && hipHostGetDevicePointer(reinterpret_cast<void**>(&fault_d), fault_h, 0) != hipSuccess)
         fault_d = nullptr;
-    if (!fault_d || !reduce_adam_coresident()) {
+    if (!fault_d || !reduce_adam_coresident() || force_split_update()) {
         // the two-kernel form: k_ppo_grad_mfma + k_ppo_reduce, then k_adam
         for (int i = 0; i < n_minibatches; ++i) {
             int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
@@ -1611,6 +1633,12 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));
     }
+    return RT_OK;
+}
+
+extern "C" int rt_ppo_status(void) {
+    if (reduce_adam_faulted())
+        return rt_internal_fail(RT_EDEVICE, "rt_ppo_status: an rt_ppo_update on this device lost its grid arrival");
     return RT_OK;
 }
 

@@ -57,7 +57,6 @@ constexpr int kUnroll = RT_DENSE_UNROLL;  // k_dense: float4 loads in flight per
 // the system-scope release + acquire (L2 writeback and invalidate) a default
 // event record performs.  Kernel boundaries keep their device-scope release.
 constexpr unsigned kEventNoSysFence = hipEventDisableSystemFence;
-constexpr int kPDenseU = 4;  // persistent dense rollout: float4 loads per lane per register set (two sets)
 constexpr int kSliceVec = 8192;          // k_dense slice: 8192 float4 = 128 KiB of dose
 constexpr int kMaxTumourVoxels = 16384;  // tumour voxels (op slots n + n-1 < 2^16; k_finish LDS per wave)
 constexpr int kMaxGridDim = 1024;
@@ -420,7 +419,6 @@ struct BeamParams {
     int32_t e_begin;              //   (an env group of the pipelined dense rollout)
     int32_t is_reset_call;
     int32_t incremental;          // RT_STEP_INCREMENTAL (visionless only)
-    int32_t zero_reset;           // the env's own wave zeroes its row on RESET (persistent rollouts)
     uint64_t seed;
     int64_t env_id_base;
 };
@@ -498,24 +496,6 @@ __device__ BeamSetup pose_step(const BeamParams& P, int e, const float* act) {
     return s;
 }
 
-// Dose-row accesses of the dataflow rollout (k_flow_chain / k_flow_dose,
-// rollout groups RT_ROLLOUT_FLOW): the chain's march and tumour gather and the
-// dose kernel's stream and reset zeroing run concurrently on different CUs
-// (XCDs), so every load and store of the hand-off bytes is `sc1` (relaxed,
-// agent scope: global_load / global_store ... sc1), ordered by counters that
-// are published after the stores have drained (MI355X_MICROARCH.md, hand-off
-// table row 1).  COH = false: plain accesses (the launch-per-step paths).
-template <bool COH>
-__device__ __forceinline__ float ld_dose(const float* p) {
-    if constexpr (COH) return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *p;
-}
-template <bool COH>
-__device__ __forceinline__ void st_dose(float* p, float v) {
-    if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
-
 __device__ __forceinline__ int rfl_i(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ float rfl_f(float x) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
@@ -535,9 +515,6 @@ __device__ __forceinline__ float rfl_f(float x) {
 // ---------------------------------------------------------------------------
 // act: the env's 6 action floats in registers (fused policy step) or null
 // (read from P.actions).
-// act: the env's 6 action floats in registers (fused policy step) or null
-// (read from P.actions).
-template <bool COH = false>
 __device__ int beam_env(const BeamParams& P, int e, int lane, const float* act) {
     BeamSetup s{};
     if (lane == 0) {
@@ -549,7 +526,7 @@ __device__ int beam_env(const BeamParams& P, int e, int lane, const float* act) 
     }
     if (lane == 0) RT_STAMP(e, 12);
     const int mode = rfl_i(s.mode);
-    if ((P.incremental || P.zero_reset) && mode == MODE_RESET) {
+    if (P.incremental && mode == MODE_RESET) {
         // reset_dose (environment.py:104) when no k_dense runs (incremental step,
         // persistent rollouts): the env's own wave zeroes its row
         typedef float nf4 __attribute__((ext_vector_type(4)));
@@ -634,14 +611,14 @@ __device__ int beam_env(const BeamParams& P, int e, int lane, const float* act) 
         uint32_t lb[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            old_d[i] = own[i] ? ld_dose<COH>(dose + pv[i]) : 0.0f;
+            old_d[i] = own[i] ? dose[pv[i]] : 0.0f;
             lb[i] = (P.incremental && own[i]) ? lbits[ci[i] >> 5] : 0u;
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (!own[i]) continue;
             const float new_d = clip01(old_d[i] + wv[i] * bd);
-            st_dose<COH>(dose + pv[i], new_d);
+            dose[pv[i]] = new_d;
             if (P.incremental && ((lb[i] >> (ci[i] & 31)) & 1u)) {
                 dcnt += (new_d > thr ? 1 : 0) - (old_d[i] > thr ? 1 : 0);
                 dsum += (double)new_d - (double)old_d[i];
@@ -1144,7 +1121,7 @@ __device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const 
 // so the tail issues no dependent load (each one a few us beside the dose
 // stream).
 constexpr int kGatherU = 4;  // tumour voxels per lane in flight in the gather
-template <bool PF = false, bool COH = false>
+template <bool PF = false>
 __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char* wave_lds) {
     float* tvals = reinterpret_cast<float*>(wave_lds);
     if (lane == 0) RT_STAMP(e, 5);
@@ -1193,15 +1170,8 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     if constexpr (PF) {
         if (!P.incremental)
             for (int j = lane; j < P.slices; j += 64) {
-                if constexpr (COH) {  // written by the concurrently running dose kernel
-                    pf_cnt += __hip_atomic_load(const_cast<int32_t*>(P.part_cnt) + (size_t)e * P.slices + j,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    pf_dl += __hip_atomic_load(const_cast<double*>(P.part_sum) + (size_t)e * P.slices + j,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    pf_cnt += P.part_cnt[(size_t)e * P.slices + j];
-                    pf_dl += P.part_sum[(size_t)e * P.slices + j];
-                }
+                pf_cnt += P.part_cnt[(size_t)e * P.slices + j];
+                pf_dl += P.part_sum[(size_t)e * P.slices + j];
             }
         if (lane == 0) {
             pf_t = P.st.t[e];
@@ -1243,7 +1213,7 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
 #pragma unroll
         for (int u = 0; u < kGatherU; ++u) {
             const int i = i0 + 64 * u + lane;
-            x[u] = i < nt ? ld_dose<COH>(dose + pos[u]) : 0.0f;
+            x[u] = i < nt ? dose[pos[u]] : 0.0f;
         }
 #pragma unroll
         for (int u = 0; u < kGatherU; ++u) {
@@ -1420,62 +1390,6 @@ __global__ __launch_bounds__(1024) void k_step_policy(BeamParams B, FinishParams
 }
 
 // ---------------------------------------------------------------------------
-// dense_env: k_dense's reductions for ONE env by its own wave (the persistent
-// dense rollout): count(dose > 0.2) and the f64 sum over the lung segment of
-// the env's lung-first row (the first lung_n floats), written to the env's
-// lung_cnt / lung_sum, which finish_env then reads as in incremental mode.
-// 8 non-temporal 16-B loads in flight per lane; the 4096 waves of a launch
-// keep ~32 MB of loads in flight.  The count is an exact integer (rewards and
-// termination are those of k_dense bit for bit); the sum (info doses.lung)
-// rounds in another order than k_dense's slices.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void dense_env(const FinishParams& P, int e, int lane) {
-    constexpr int U = kPDenseU;
-    const float4* d4 = reinterpret_cast<const float4*>(P.st.dose + (size_t)e * P.G.Vpad);
-    const int n = P.lung_n;
-    const int nq = (n + 3) >> 2;
-    const float thr = P.C.lung_thr;
-    int cnt = 0;
-    double lsum = 0.0;
-    auto fetch = [&](float4 (&v)[U], int base) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = base + u * 64 + lane;
-            v[u] = q < nq ? load_nt(&d4[q]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    auto consume = [&](const float4 (&v)[U], int base) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = base + u * 64 + lane;
-            float4 x = v[u];
-            if (4 * q + 3 >= n) {  // the segment's last float4 may hold non-lung voxels
-                if (4 * q + 1 >= n) x.y = 0.0f;
-                if (4 * q + 2 >= n) x.z = 0.0f;
-                x.w = 0.0f;
-            }
-            cnt += (x.x > thr ? 1 : 0) + (x.y > thr ? 1 : 0) + (x.z > thr ? 1 : 0) + (x.w > thr ? 1 : 0);
-            lsum += (((double)x.x + (double)x.y) + (double)x.z) + (double)x.w;
-        }
-    };
-    // two register sets: the next U loads are in flight while the current U are reduced
-    float4 va[U], vb[U];
-    fetch(va, 0);
-    for (int base = 0; base < nq; base += 128 * U) {
-        fetch(vb, base + 64 * U);
-        consume(va, base);
-        fetch(va, base + 128 * U);
-        consume(vb, base + 64 * U);
-    }
-    cnt = wave_sum_i(cnt);
-    lsum = wave_sum_d(lsum);
-    if (lane == 0) {
-        P.st.lung_cnt[e] = cnt;
-        P.st.lung_sum[e] = lsum;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // k_rollout_policy: n_steps rollout steps of the visionless agent in ONE
 // persistent launch (incremental step mode).  Envs never interact, so a wave
 // can run its env's whole step chain -- policy sample, pose update, march,
@@ -1504,7 +1418,6 @@ struct RolloutArgs {
     RolloutParams R;
 };
 
-template <bool DENSE>
 __global__ __launch_bounds__(1024) void k_rollout_policy(RolloutArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     rtpol::Lds& L = *reinterpret_cast<rtpol::Lds*>(rsm);
@@ -1582,17 +1495,10 @@ __global__ __launch_bounds__(1024) void k_rollout_policy(RolloutArgs A) {
         float a6[rtpol::NACT];
 #pragma unroll
         for (int i = 0; i < rtpol::NACT; ++i) a6[i] = rtpol::lane_f(smp.action, i);
-        const int mode = beam_env(B, e, lane, a6);
+        beam_env(B, e, lane, a6);
         // this wave's dose stores are visible to its own lanes' loads below
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        if constexpr (DENSE) {
-            if (mode == MODE_STEP) {
-                dense_env(F, e, lane);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            }
-        }
         FinishParams Ft = F;
-        if constexpr (DENSE) Ft.incremental = 1;  // the counts dense_env just wrote
         Ft.reward = R.reward_store + (size_t)t * N;
         Ft.info = R.info_store ? R.info_store + (size_t)t * N * RT_INFO_W : nullptr;
         finish_env(Ft, e, lane, fin);
@@ -1601,278 +1507,6 @@ __global__ __launch_bounds__(1024) void k_rollout_policy(RolloutArgs A) {
         __builtin_amdgcn_wave_barrier();
     }
     if (lane0 == 0) RT_STAMP(e0, 14);
-}
-
-// ---------------------------------------------------------------------------
-// Dataflow dense rollout (rt_env_set_rollout_groups(env, RT_ROLLOUT_FLOW)):
-// the whole rollout call as ONE persistent launch, one 16-wave block per CU,
-// whose waves take two roles and hand each env's step over through per-env
-// device counters instead of kernel boundaries and events:
-//
-//   chain waves (0..7)  wave cw owns envs cw, cw + W, ... (W = chain waves of
-//                       the launch) and runs, per step and env: wait for the
-//                       env's dose items of the previous step, finish it
-//                       (finish_env), sample the next action from the
-//                       parameters staged once per call (policy_core.h),
-//                       pose + march (beam_env), publish "marched step t,
-//                       mode m";
-//   dose waves (8..15)  claim (step, env, slice) items in the chain's
-//                       production order, wait for the env's march, stream
-//                       the slice of its lung segment (k_dense's reduction;
-//                       one wave per 128 KiB slice, 16 float4 in flight per
-//                       lane) or zero a share of a RESET env's row
-//                       (environment.py:104), publish.
-//
-// Both roles in one launch: every block is resident at once on the idle
-// device (two dependent persistent launches on two streams would rely on
-// the runtime running them concurrently, which HIP does not promise).  What it
-// removes against the two-group pipeline (§3): the per-turn hand-off gaps
-// (~12 us twice a step), the parameter staging of every policy launch beside
-// the stream (36-43 us), the group-wide turns (a slow env delays its own
-// items only), and ~120 launches and 80 event operations per 20-step call.
-// Every hand-off byte is sc1 on both sides (ld_dose / st_dose, the partial
-// sums, the zeroing) and published after the stores drained
-// (MI355X_MICROARCH.md, hand-off table row 1); bounded waits (~1 s) raise the
-// handle's host-mapped fault flag and drain the kernel instead of hanging it
-// (the next rollout call returns RT_EDEVICE).  Rewards, termination,
-// observations and doses are the stepwise launches' bits
-// (tests/test_gpu_rollout.py); info doses.lung sums each slice in another
-// order (f64, then f32: within rounding).
-// ---------------------------------------------------------------------------
-#ifndef RT_FLOW_CW
-#define RT_FLOW_CW 8
-#endif
-#ifndef RT_FLOW_U
-#define RT_FLOW_U 8
-#endif
-#ifndef RT_FLOW_CHUNK
-#define RT_FLOW_CHUNK 2
-#endif
-#ifndef RT_FLOW_AUX
-#define RT_FLOW_AUX 16
-#endif
-#ifndef RT_FLOW_DIAG  // timing-only variant builds: 1 dose waves skip their waits, 2 chain waves theirs
-#define RT_FLOW_DIAG 0
-#endif
-constexpr int kFlowWaves = RT_FLOW_CW;      // chain waves per block
-constexpr int kFlowDoseWaves = 16 - kFlowWaves;  // dose waves per block
-constexpr int kFlowU = RT_FLOW_U;           // dose waves: float4 per lane per register set (two sets)
-constexpr int kFlowChunk = RT_FLOW_CHUNK;   // items per claim
-
-struct FlowParams {
-    uint32_t* march;     // [N] ((t + 1) << 2) | mode: the env's last march of this call
-    uint32_t* dense;     // [N] the env's dose items completed in this call
-    uint32_t* claim;     // the dose waves' next chunk of items
-    int* fault;          // host-mapped sticky flag: a bounded wait ran out
-    int32_t epw;         // envs per chain wave
-    int32_t W;           // chain waves of the launch
-    int32_t n_steps;
-    int32_t N;           // envs of the handle
-};
-
-struct FlowArgs {
-    BeamParams B;
-    FinishParams F;
-    RolloutParams R;
-    FlowParams X;
-    DenseParams D;
-};
-
-// one lane: wait until *p >= target (sc1 loads, s_sleep between polls);
-// false when ~1 s passes first
-__device__ __forceinline__ bool flow_wait(uint32_t* p, uint32_t target) {
-    uint64_t t_end = 0;
-    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if (t_end == 0) {
-            t_end = now + 100000000ull;  // s_memrealtime: 100 MHz
-        } else if (now > t_end) {
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-    return true;
-}
-
-__device__ __forceinline__ void flow_fault(int* fault) {
-    __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// A dose wave: claims item chunks until the call's items are exhausted.
-__device__ void flow_dose_wave(const DenseParams& P, const FlowParams& X, int lane) {
-    const int S = P.slices, N = X.N;
-    const int per_step = N * S;
-    const int n_items = X.n_steps * per_step;
-    const float thr = P.lung_thr;
-    const int n = P.lung_n, nq = (n + 3) >> 2;
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-    for (;;) {
-        uint32_t c = 0;
-        if (lane == 0) c = __hip_atomic_fetch_add(X.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int i0 = __builtin_amdgcn_readfirstlane((int)c) * kFlowChunk;
-        if (i0 >= n_items) return;
-        const int i1 = min(i0 + kFlowChunk, n_items);
-        for (int it = i0; it < i1; ++it) {
-            const int t = it / per_step, r = it - t * per_step;
-            const int e = r / S, sl = r - e * S;
-            int m = -1;
-            if (RT_FLOW_DIAG & 1) m = MODE_STEP;
-            else if (lane == 0 && flow_wait(X.march + e, (uint32_t)(t + 1) << 2))
-                m = (int)(__hip_atomic_load(X.march + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 3u);
-            m = __builtin_amdgcn_readfirstlane(m);
-            if (m < 0) {  // the chain never published: drain
-                if (lane == 0) flow_fault(X.fault);
-                return;
-            }
-            const __amdgpu_buffer_rsrc_t rsrc =
-                __builtin_amdgcn_make_buffer_rsrc(P.st.dose + (size_t)e * P.G.Vpad, 0, P.G.Vpad * 4, 0x00020000);
-            if (m == MODE_STEP) {
-                // the slice's float4 [q0, q1) of the lung segment, 16 loads in flight per lane
-                const int q0 = sl * P.vec_per_slice, q1 = min(q0 + P.vec_per_slice, nq);
-                int cnt = 0;
-                double lsum = 0.0;
-                auto fetch = [&](f4v (&v)[kFlowU], int base) {
-#pragma unroll
-                    for (int u = 0; u < kFlowU; ++u) {
-                        const int q = base + u * 64 + lane;
-                        v[u] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                           rsrc, 16 * (q < q1 ? q : q0), 0, RT_FLOW_AUX));  // 16: sc1
-                    }
-                };
-                auto consume = [&](const f4v (&v)[kFlowU], int base) {
-#pragma unroll
-                    for (int u = 0; u < kFlowU; ++u) {
-                        const int q = base + u * 64 + lane;
-                        f4v x = q < q1 ? v[u] : f4v{0.f, 0.f, 0.f, 0.f};
-                        if (4 * q + 3 >= n) {  // the segment's last float4 may hold non-lung voxels
-                            if (4 * q + 1 >= n) x.y = 0.0f;
-                            if (4 * q + 2 >= n) x.z = 0.0f;
-                            x.w = 0.0f;
-                        }
-                        cnt += (x.x > thr ? 1 : 0) + (x.y > thr ? 1 : 0) + (x.z > thr ? 1 : 0) + (x.w > thr ? 1 : 0);
-                        lsum += (((double)x.x + (double)x.y) + (double)x.z) + (double)x.w;
-                    }
-                };
-                f4v va[kFlowU], vb[kFlowU];
-                fetch(va, q0);
-                for (int base = q0; base < q1; base += 128 * kFlowU) {
-                    fetch(vb, base + 64 * kFlowU);
-                    consume(va, base);
-                    fetch(va, base + 128 * kFlowU);
-                    consume(vb, base + 64 * kFlowU);
-                }
-                cnt = wave_sum_i(cnt);
-                lsum = wave_sum_d(lsum);
-                if (lane == 0) {
-                    __hip_atomic_store(P.part_cnt + (size_t)e * S + sl, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(P.part_sum + (size_t)e * S + sl, lsum, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else if (m == MODE_RESET) {
-                // reset_dose (environment.py:104): slice sl zeroes its share of the whole row
-                const int rowv = P.G.Vpad >> 2;
-                const int per = (rowv + S - 1) / S;
-                const int z0 = sl * per, z1 = min(z0 + per, rowv);
-                const u4v z = {0u, 0u, 0u, 0u};
-                for (int q = z0 + lane; q < z1; q += 64) __builtin_amdgcn_raw_buffer_store_b128(z, rsrc, 16 * q, 0, 16);
-            }
-            // every lane's stores have drained, then the item's arrival
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_fetch_add(X.dense + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-__global__ __launch_bounds__(1024) void k_flow(FlowArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
-    rtpol::Lds& L = *reinterpret_cast<rtpol::Lds*>(fsm);
-    const int tid = threadIdx.x, lane0 = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // every wave stages the parameters, then the block's only barrier: after
-    // the role split the waves never wait for each other
-    rtpol::stage(L, A.R.q.w, tid, (int)blockDim.x);
-    __syncthreads();
-    if (w >= kFlowWaves) {
-        flow_dose_wave(A.D, A.X, lane0);
-        return;
-    }
-    const int cw = blockIdx.x * kFlowWaves + w;
-    unsigned char* const fin_0 = fsm + A.R.fin_off + (size_t)w * A.F.wave_lds;
-    const int n_steps = A.X.n_steps, epw = A.X.epw;
-    for (int t = 0; t <= n_steps; ++t) {
-        for (int j = 0; j < epw; ++j) {
-            // the loop-invariant inputs re-derived every iteration (as in
-            // k_rollout_policy: hoisted, they push the body past 128 VGPRs)
-            typedef const __attribute__((address_space(4))) FlowArgs* KPtr;
-            KPtr ap = (KPtr)(__builtin_amdgcn_kernarg_segment_ptr());
-            asm volatile("" : "+s"(ap));
-            const FlowArgs& K = *(const FlowArgs*)ap;
-            const BeamParams& B = K.B;
-            const FinishParams& F = K.F;
-            const RolloutParams& R = K.R;
-            const FlowParams& X = K.X;
-            const PolicyStepParams& Q = R.q;
-            int lane = lane0;
-            asm volatile("" : "+v"(lane));
-            const int e = cw + j * X.W;
-            if (e >= B.N) break;  // wave-uniform
-            unsigned char* fin = fin_0;
-            float* h1 = reinterpret_cast<float*>(fin_0);
-            asm volatile("" : "+s"(fin));
-            asm volatile("" : "+s"(h1));
-            const size_t N = (size_t)B.N;
-            if (t > 0) {
-                // step t - 1's dose items of this env (its slices, or its row zeroed)
-                int ok = 1;
-                if (lane == 0 && !(RT_FLOW_DIAG & 2)) ok = flow_wait(X.dense + e, (uint32_t)(F.slices * t)) ? 1 : 0;
-                if (!__builtin_amdgcn_readfirstlane(ok)) {
-                    if (lane == 0) flow_fault(X.fault);
-                    return;
-                }
-                FinishParams Ft = F;
-                Ft.reward = R.reward_store + (size_t)(t - 1) * N;
-                Ft.info = R.info_store ? R.info_store + (size_t)(t - 1) * N * RT_INFO_W : nullptr;
-                finish_env<true, true>(Ft, e, lane, fin);
-                // obs / terminated / state of this env -> every lane below
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-            }
-            if (t == n_steps) continue;
-            const float* obs_in = t == 0 ? Q.obs_in : F.obs;
-            const uint8_t* done_in = t == 0 ? Q.done_in : F.terminated;
-            float x[rtpol::NOBS];
-#pragma unroll
-            for (int i = 0; i < rtpol::NOBS; ++i) x[i] = obs_in[(size_t)e * rtpol::NOBS + i];
-            const rtpol::Sample smp =
-                rtpol::policy_env(L, h1, x, lane, Q.seed, Q.counter + (uint64_t)t, (uint64_t)(Q.id_base + e));
-            const size_t r9 = (size_t)t * N * rtpol::NOBS + (size_t)e * rtpol::NOBS;
-            const size_t r6 = (size_t)t * N * rtpol::NACT + (size_t)e * rtpol::NACT;
-            const size_t r1 = (size_t)t * N + (size_t)e;
-            if (lane < rtpol::NOBS) {
-                float xi = x[0];
-#pragma unroll
-                for (int i = 1; i < rtpol::NOBS; ++i) xi = lane == i ? x[i] : xi;
-                Q.obs_store[r9 + lane] = xi;
-            }
-            if (lane == rtpol::NOBS) Q.done_store[r1] = done_in ? (float)done_in[e] : 0.0f;
-            if (lane < rtpol::NACT) Q.act_store[r6 + lane] = smp.action;
-            if (lane == 0) {
-                Q.logp_store[r1] = smp.logp;
-                Q.value_store[r1] = smp.value;
-            }
-            float a6[rtpol::NACT];
-#pragma unroll
-            for (int i = 0; i < rtpol::NACT; ++i) a6[i] = rtpol::lane_f(smp.action, i);
-            const int mode = beam_env<true>(B, e, lane, a6);
-            // every lane's dose stores have left (sc1: written through), then the flag
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_store(X.march + e, ((uint32_t)(t + 1) << 2) | (uint32_t)mode, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2184,17 +1818,6 @@ struct rt_env {
     int rollout_wave_lds = 0;// bytes per wave region
     int rollout_cap = 0;     // largest tumour whose sum plan fits a region
     float* gscratch = nullptr;  // [N][2 * max_tvox] plan slots of tumours above a kernel's LDS capacity
-    // dataflow rollout (RT_ROLLOUT_FLOW): k_flow_chain's LDS, the hand-off
-    // counters and the host-mapped fault flag (allocated by
-    // rt_env_set_rollout_groups)
-    size_t flow_smem = 0;
-    int flow_fin_off = 0;
-    int flow_wave_lds = 0;
-    int flow_cap = 0;
-    uint32_t* flow_march = nullptr;  // [N]
-    uint32_t* flow_dense = nullptr;  // [N]
-    int* flow_fault_h = nullptr;     // host-mapped
-    int* flow_fault_d = nullptr;
     uint32_t view_hash_mask = 0;
     int32_t* part_cnt = nullptr;
     double* part_sum = nullptr;
@@ -2248,7 +1871,6 @@ void free_env(rt_env* env) {
     for (hipStream_t q : env->pipe)
         if (q) (void)hipStreamDestroy(q);
     for (void* p : env->allocs) (void)hipFree(p);
-    if (env->flow_fault_h) (void)hipHostFree(env->flow_fault_h);
     (void)hipSetDevice(cur);
     delete env;
 }
@@ -2539,21 +2161,6 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         }
     }
 
-    // k_flow_chain: the parameters once per block, then kFlowWaves per-wave
-    // regions (h1, then the finish scratch), in ~159 KiB (one block per CU;
-    // the dose blocks beside it take a few hundred bytes)
-    {
-        const size_t off = (sizeof(rtpol::Lds) + 15) / 16 * 16;
-        const size_t per_wave = (159 * 1024 - off) / kFlowWaves / 16 * 16;
-        const int cap = (int)((per_wave - kMaxPlanLevels * sizeof(int32_t)) / (3 * sizeof(float)));
-        if (env->visionless && env->lung_first && per_wave >= rtpol::H * sizeof(float) && cap >= 1) {
-            env->flow_fin_off = (int)off;
-            env->flow_wave_lds = (int)per_wave;
-            env->flow_cap = std::min(cap, max_n);
-            env->flow_smem = off + (size_t)kFlowWaves * per_wave;
-        }
-    }
-
     // ---- device allocations ----
     const int N = env->N;
     uint32_t* d_lbits;
@@ -2577,9 +2184,7 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         (rc = dev_alloc(env, &env->part_cnt, (size_t)N * env->slices)) ||
         (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices)) ||
         (rc = dev_alloc(env, &st.lung_cnt, N)) || (rc = dev_alloc(env, &st.lung_sum, N)) ||
-        // the persistent rollout's plan slots for tumours above its LDS share:
-        // incremental handles (their default rollout); dense handles allocate
-        // them in rt_env_set_rollout_groups(env, 0), the only way they reach it
+        // the persistent rollout's plan slots for tumours above its LDS share
         (env->incremental && env->rollout_wpb && env->rollout_cap < max_n &&
          (rc = dev_alloc(env, &env->gscratch, (size_t)N * 2 * max_n)))) {
         free_env(env);
@@ -2958,53 +2563,20 @@ static int rollout_dense(rt_env* env, const rt_policy_rollout* r, float* obs_d, 
 }
 
 int rt_env_set_rollout_groups(rt_env* env, int32_t groups) {
-    if (!env || groups < 0 || (groups > kMaxRolloutGroups && groups != RT_ROLLOUT_FLOW))
-        return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups must be 0 (persistent), 1..4 or RT_ROLLOUT_FLOW");
-    if (groups == RT_ROLLOUT_FLOW) {
-        if (!env->visionless || env->incremental || !env->lung_first || !env->flow_smem)
-            return fail(RT_EINVAL, "rt_env_set_rollout_groups: RT_ROLLOUT_FLOW needs a dense-mode visionless handle");
-        int cur = 0;
-        (void)hipGetDevice(&cur);
-        RT_HIP(hipSetDevice(env->device));
-        int rc = RT_OK;
-        if (!env->flow_march && ((rc = dev_alloc(env, &env->flow_march, (size_t)env->N + 1)) ||
-                                 (rc = dev_alloc(env, &env->flow_dense, env->N)))) {
-            (void)hipSetDevice(cur);
-            return rc;
-        }
-        if (!env->flow_fault_h) {
-            void* h = nullptr;
-            if (hipHostMalloc(&h, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-                hipHostGetDevicePointer(reinterpret_cast<void**>(&env->flow_fault_d), h, 0) != hipSuccess) {
-                if (h) (void)hipHostFree(h);
-                (void)hipSetDevice(cur);
-                return fail(RT_ENOMEM, "rt_env_set_rollout_groups: host-mapped fault flag");
-            }
-            env->flow_fault_h = static_cast<int*>(h);
-            *static_cast<volatile int*>(env->flow_fault_h) = 0;
-        }
-        if (env->flow_cap < env->max_tvox && !env->gscratch)
-            rc = dev_alloc(env, &env->gscratch, (size_t)env->N * 2 * env->max_tvox);
-        (void)hipSetDevice(cur);
-        if (rc) return rc;
-        env->rollout_groups = groups;
-        return RT_OK;
-    }
-    if (groups == 0 && env->visionless && env->rollout_wpb && env->rollout_cap < env->max_tvox && !env->gscratch) {
-        int cur = 0;
-        (void)hipGetDevice(&cur);
-        RT_HIP(hipSetDevice(env->device));
-        const int rc = dev_alloc(env, &env->gscratch, (size_t)env->N * 2 * env->max_tvox);
-        (void)hipSetDevice(cur);
-        if (rc) return rc;
-    }
+    if (!env || groups < 0 || groups > kMaxRolloutGroups)
+        return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups must be 0 (persistent) or 1..4");
+    if (groups == 0 && !env->incremental)
+        return fail(RT_EINVAL, "rt_env_set_rollout_groups: groups 0 (one persistent launch) is the incremental "
+                               "step mode's rollout; dense handles take 1..4");
+    if (groups > 0 && env->incremental)
+        return fail(RT_EINVAL, "rt_env_set_rollout_groups: incremental handles roll out in one persistent launch "
+                               "(groups 0)");
     env->rollout_groups = groups;
     return RT_OK;
 }
 
-// One persistent launch for the whole rollout: k_rollout_policy<false>
-// (incremental step mode) or <true> (dense mode, rollout groups 0: each wave
-// streams its env's lung segment after the march, dense_env).
+// Incremental step mode: one persistent launch for the whole rollout
+// (k_rollout_policy).
 static int rollout_persistent(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
                               hipStream_t s) {
     const rt_policy_step* ps = &r->step;
@@ -3032,92 +2604,21 @@ static int rollout_persistent(rt_env* env, const rt_policy_rollout* r, float* ob
     hipEvent_t* ev = next_timing_slot(env);
     if (ev) (void)hipEventRecord(ev[0], s);
     BeamParams bp = beam_params(env, false, nullptr, nullptr, nullptr);
-    bp.zero_reset = 1;
     FinishParams fp = finish_params(env, obs_d, nullptr, terminated_d, nullptr);
     fp.max_tvox = env->rollout_cap;
     fp.wave_lds = env->rollout_wave_lds;
     if (env->rollout_cap < env->max_tvox && !env->gscratch)
-        return fail(RT_EINVAL, "rt_env_rollout_policy: persistent rollout scratch missing (rollout groups 0 not set)");
+        return fail(RT_EINVAL, "rt_env_rollout_policy: persistent rollout scratch missing");
     fp.gscratch = env->gscratch;
     fp.gscratch_stride = 2 * (int64_t)env->max_tvox;
     const dim3 grid((env->N + Q.wpb - 1) / Q.wpb), block(64 * Q.wpb);
     RolloutArgs A{bp, fp, R};
-    if (env->incremental) {
-        static bool big = false;
-        if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_rollout_policy<false>), big)) return rc_lds;
-        hipLaunchKernelGGL(k_rollout_policy<false>, grid, block, env->rollout_smem, s, A);
-    } else {
-        static bool big = false;
-        if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_rollout_policy<true>), big)) return rc_lds;
-        hipLaunchKernelGGL(k_rollout_policy<true>, grid, block, env->rollout_smem, s, A);
-    }
+    static bool big = false;
+    if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_rollout_policy), big)) return rc_lds;
+    hipLaunchKernelGGL(k_rollout_policy, grid, block, env->rollout_smem, s, A);
     RT_LAUNCH_CHECK("k_rollout_policy");
     if (ev)
         for (int k = 1; k < 4; ++k) (void)hipEventRecord(ev[k], s);
-    return RT_OK;
-}
-
-// Dense step mode, rollout groups RT_ROLLOUT_FLOW: k_flow_chain and
-// k_flow_dose run the whole call concurrently on the two library streams
-// (fork / join with `stream` by events), handing each env's step over through
-// the per-env counters, zeroed on `stream` first.
-static int rollout_flow(rt_env* env, const rt_policy_rollout* r, float* obs_d, uint8_t* terminated_d,
-                        hipStream_t s) {
-    if (*static_cast<volatile int*>(env->flow_fault_h))
-        return fail(RT_EDEVICE, "rt_env_rollout_policy: an earlier dataflow rollout ran out a bounded wait");
-    const rt_policy_step* ps = &r->step;
-    RolloutParams R{};
-    PolicyStepParams& Q = R.q;
-    for (int i = 0; i < rtpol::kTensors; ++i) {
-        if (!ps->params[i]) return fail(RT_EINVAL, "rt_env_rollout_policy: NULL parameter");
-        Q.w.p[i] = ps->params[i];
-    }
-    Q.obs_in = ps->obs_in;
-    Q.done_in = ps->done_in;
-    Q.obs_store = ps->obs_store;
-    Q.done_store = ps->done_store;
-    Q.act_store = ps->act_store;
-    Q.logp_store = ps->logp_store;
-    Q.value_store = ps->value_store;
-    Q.seed = ps->seed;
-    Q.counter = ps->counter;
-    Q.id_base = ps->env_id_base;
-    R.reward_store = r->reward_store;
-    R.info_store = r->info_store;
-    R.n_steps = r->n_steps;
-    R.fin_off = env->flow_fin_off;
-    BeamParams bp = beam_params(env, false, nullptr, nullptr, nullptr);
-    FinishParams fp = finish_params(env, obs_d, nullptr, terminated_d, nullptr);
-    fp.max_tvox = env->flow_cap;
-    fp.wave_lds = env->flow_wave_lds;
-    fp.gscratch = env->gscratch;
-    fp.gscratch_stride = 2 * (int64_t)env->max_tvox;
-    const int N = env->N;
-    // one block per CU (its LDS holds one); fewer for small handles, >= 2 envs per chain wave
-    const int nblk = std::max(1, std::min(env->num_cu, (N + 2 * kFlowWaves - 1) / (2 * kFlowWaves)));
-    FlowParams X{};
-    X.march = env->flow_march;
-    X.dense = env->flow_dense;
-    X.claim = env->flow_march + N;
-    X.fault = env->flow_fault_d;
-    X.W = nblk * kFlowWaves;
-    X.epw = (N + X.W - 1) / X.W;
-    X.n_steps = r->n_steps;
-    X.N = N;
-    FlowArgs A{bp, fp, R, X, dense_params(env, 0)};
-    hipEvent_t* ev = next_timing_slot(env);
-    if (ev) (void)hipEventRecord(ev[0], s);
-    RT_HIP(hipMemsetAsync(env->flow_march, 0, ((size_t)N + 1) * sizeof(uint32_t), s));
-    RT_HIP(hipMemsetAsync(env->flow_dense, 0, (size_t)N * sizeof(uint32_t), s));
-    if (ev) (void)hipEventRecord(ev[1], s);
-    static bool big = false;
-    if (const int rc_lds = allow_lds(reinterpret_cast<const void*>(&k_flow), big)) return rc_lds;
-    hipLaunchKernelGGL(k_flow, dim3(nblk), dim3(64 * (kFlowWaves + kFlowDoseWaves)), env->flow_smem, s, A);
-    RT_LAUNCH_CHECK("k_flow");
-    if (ev) {
-        (void)hipEventRecord(ev[2], s);  // k_dense interval: the whole launch (its dose waves span it)
-        (void)hipEventRecord(ev[3], s);
-    }
     return RT_OK;
 }
 
@@ -3131,9 +2632,7 @@ int rt_env_rollout_policy(rt_env* env, const rt_policy_rollout* r, float* obs_d,
     if (!env->visionless) return fail(RT_EINVAL, "rt_env_rollout_policy: the fused policy is the visionless MLP");
     if (ps->n_params != rtpol::kTensors) return fail(RT_EINVAL, "rt_env_rollout_policy: expected 13 parameter tensors");
     if (r->n_steps < 1) return fail(RT_EINVAL, "rt_env_rollout_policy: n_steps < 1");
-    if (!env->incremental && env->rollout_groups == RT_ROLLOUT_FLOW)
-        return rollout_flow(env, r, obs_d, terminated_d, as_stream(stream));
-    if (!env->incremental && env->rollout_groups > 0) return rollout_dense(env, r, obs_d, terminated_d, as_stream(stream));
+    if (!env->incremental) return rollout_dense(env, r, obs_d, terminated_d, as_stream(stream));
     if (env->rollout_wpb == 0)
         return fail(RT_ELIMIT, "rt_env_rollout_policy: policy + finish scratch exceed LDS (largest tumour too big)");
     return rollout_persistent(env, r, obs_d, terminated_d, as_stream(stream));

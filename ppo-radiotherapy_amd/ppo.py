@@ -670,6 +670,15 @@ class PPOTrainer:
             self.optimizer.param_groups[0]["lr"] = frac * float(self.cfg.learning_rate)
 
     # ------------------------------------------------------------------ checkpoint / resume
+    def check_device_status(self):
+        """Raise if a fused update on this device lost the grid arrival of its
+        reduce + Adam launch (rt_ppo_status, after the stream sync): the
+        parameters are then the last complete minibatch's, and a checkpoint of
+        them must not be saved as if the update had run."""
+        if self.fused_update:
+            torch.cuda.synchronize(self.device)
+            _lib.check(_lib.load().rt_ppo_status(), "rt_ppo_status")
+
     def _rng_states(self) -> dict:
         d = {}
         if self.gen is not None:

@@ -106,6 +106,8 @@ def train(cfg, writer, device, output_dir=None, run_name=None, rank=0, world=1):
         if (cfg.save_model and output_dir is not None and
                 ((cfg.save_frequency_iterations and iteration % cfg.save_frequency_iterations == 0)
                  or iteration == cfg.num_iterations)):
+            # the fused update's state is whole (no lost grid arrival) before it is saved
+            tr.check_device_status()
             # every rank takes part (the checkpoint gathers all ranks' generator states)
             ckpt = tr.state_dict() if cfg.get("save_checkpoint", True) else None
             if rank == 0:

@@ -189,8 +189,8 @@ class RadiotherapyVecEnv:
         return rc
 
     def set_rollout_groups(self, groups: int):
-        """Env groups of the dense-mode rollout_policy: 2..4 (pipelined streams; default 2), 1, 0 (persistent)
-        or _lib.ROLLOUT_FLOW (the dataflow rollout: a chain and a dose kernel handing steps over per env)."""
+        """Env groups of the dense-mode rollout_policy: 2..4 (pipelined streams; default 2) or 1 (the
+        stepwise launches on one stream); incremental handles take only 0 (their persistent launch)."""
         _lib.check(self._L.rt_env_set_rollout_groups(self._h, int(groups)), "rt_env_set_rollout_groups")
 
     def set_next_tumours(self, ids):

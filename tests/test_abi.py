@@ -71,7 +71,7 @@ def test_config_defaults_are_reference_constants():
     assert c.tumour_dose_threshold == np.float32(0.9) and c.min_angle_z == math.pi / 4
     assert c.movement_speed == 0.2 and c.rotation_speed == 0.5
     assert (c.lung_dose_reward, c.tumour_dose_reward, c.distance_reward) == (-1.0, 10.0, -1.0)
-    assert L.rt_abi_version() == 4
+    assert L.rt_abi_version() == 5
     assert c.struct_size == ctypes.sizeof(_lib.RtEnvConfig)
 
 

@@ -406,6 +406,55 @@ def test_update_call_equals_grad_plus_adam(max_norm):
     assert not torch.equal(got[0], start[0])  # the update moved the parameters
 
 
+@pytest.mark.parametrize("max_norm", [0.5, 0.0])
+def test_update_split_form_equals_fused(max_norm, monkeypatch):
+    """rt_ppo_update's two-kernel form (k_ppo_grad + k_ppo_reduce, then k_adam
+    with the reduce's norm partials) -- what a failed co-residency check or a
+    missing host-mapped fault flag selects, forced here by the debug knob
+    RT_PPO_UPDATE_SPLIT -- is bitwise the fused reduce + Adam form
+    (k_adam sums the same partials in the same order), and neither raises the
+    lost-arrival flag (rt_ppo_status)."""
+    import ctypes
+
+    from ppo_radiotherapy_amd import _lib
+
+    tr = _make(fused=True)
+    dev = tr.device
+    tr._bind_batch()
+    batch = tr._batch_struct()
+    L = _lib.load()
+    mbs, n_mb = tr.minibatch_size, tr.batch_size // tr.minibatch_size
+    perm = torch.randperm(tr.batch_size, generator=torch.Generator().manual_seed(5)).to(dev)
+    adv = torch.empty((n_mb, 2), device=dev)
+    _lib.check(L.rt_ppo_adv_stats(tr._b_adv.data_ptr(), perm.data_ptr(), mbs, n_mb, adv.data_ptr(),
+                                  tr._ws.data_ptr(), tr._ws.numel(), None), "rt_ppo_adv_stats")
+    hp = _lib.RtPpoHparams(clip_coef=0.1, clip_vloss=1, norm_adv=1, ent_coef=0.01, vf_coef=0.5,
+                           max_grad_norm=max_norm, adam_beta1=0.9, adam_beta2=0.999, adam_eps=1e-5)
+    state = [tr.flat_param, tr._exp_avg, tr._exp_avg_sq]
+    start = [t.clone() for t in state]
+    n = tr.flat_param.numel()
+    outs = []
+    for split in (False, True):
+        with torch.no_grad():
+            for t, s0 in zip(state, start):
+                t.copy_(s0)
+        if split:
+            monkeypatch.setenv("RT_PPO_UPDATE_SPLIT", "1")
+        stats, acc = torch.zeros(6, device=dev), torch.zeros(6, device=dev)
+        _lib.check(L.rt_ppo_update(tr._policy_ptrs, tr._grad_ptrs, ctypes.byref(batch), perm.data_ptr(), mbs, n_mb,
+                                   adv.data_ptr(), ctypes.byref(hp), tr.flat_param.data_ptr(),
+                                   tr.flat_grad.data_ptr(), tr._exp_avg.data_ptr(), tr._exp_avg_sq.data_ptr(), n, 3,
+                                   3e-4, tr._ws.data_ptr(), tr._ws.numel(), stats.data_ptr(), acc.data_ptr(), None),
+                   "rt_ppo_update")
+        torch.cuda.synchronize()
+        monkeypatch.delenv("RT_PPO_UPDATE_SPLIT", raising=False)
+        outs.append([t.clone() for t in state] + [tr.flat_grad.clone(), stats, acc])
+        assert L.rt_ppo_status() == 0
+    for name, a, b in zip(("param", "exp_avg", "exp_avg_sq", "grad", "stats", "accum"), *outs):
+        assert torch.equal(a, b), name
+    assert not torch.equal(outs[0][0], start[0])
+
+
 @pytest.mark.parametrize("n,mb,epochs", [(262144, 32768, 10), (8192, 2048, 3), (3000, 1000, 33)])
 def test_shuffle_adv_equals_separate_calls(n, mb, epochs):
     """rt_ppo_shuffle_adv (the epochs' permutations and the minibatch
