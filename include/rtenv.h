@@ -46,7 +46,8 @@ extern "C" {
                                 (rt_ppo_hparams.precision, rt_conv_layer.precision) instead of the
                                 process-wide rt_ppo_/rt_conv_set_precision; 5: RT_ROLLOUT_FLOW and
                                 the dense persistent rollout (groups 0 on dense handles) removed,
-                                rt_ppo_status added */
+                                rt_ppo_status and rt_host_lung_sum added, dense-mode
+                                doses.lung in numpy's exact order */
 
 enum {
     RT_OK = 0,
@@ -85,7 +86,8 @@ enum {
                                 whole dose volume (k_dense, HBM-bound) */
     RT_STEP_INCREMENTAL = 1  /* visionless only: the lung over-threshold count and lung dose sum
                                 are updated on the voxels the beam touches;
-                                rewards and termination identical, doses.lung within f64 rounding */
+                                rewards and termination identical, doses.lung an f64 running
+                                sum rounded once (the dense mode's is numpy's f32 order) */
 };
 
 typedef struct {
@@ -231,6 +233,12 @@ int rt_host_sincos(int32_t n, const double* x_h, double* sin_h, double* cos_h);
  * np.sum(dose * tumours) over a V-voxel volume whose nonzeros are vals_h at
  * the sorted flat indices idx_h (no device needed; parity hook). */
 int rt_host_tumour_sum(int64_t V, int32_t n, const int32_t* idx_h, const float* vals_h, float* out_h);
+
+/* Host-side evaluation of the plan k_dense + k_finish use for info doses.lung
+ * = np.sum(dose * lungs) (environment.py:235) in numpy's exact order, on a
+ * C-order f32 volume dose_h with the u8 mask lungs_h (no device needed;
+ * parity hook). */
+int rt_host_lung_sum(const int32_t grid[3], const uint8_t* lungs_h, const float* dose_h, float* out_h);
 
 /* Fused rollout policy step of the visionless agent (networks.py PPO,
  * feature_dim 64): for every env, obs -> actor/critic MLPs -> Gaussian sample

@@ -35,7 +35,7 @@ EXPORTS = [
     "rt_env_set_next_tumours", "rt_env_reseed", "rt_env_dose", "rt_env_dose_index", "rt_env_get_state", "rt_env_set_pose", "rt_env_set_tumours", "rt_env_set_render_source",
     "rt_env_num_envs",
     "rt_env_kernel_timing", "rt_env_kernel_timing_read",
-    "rt_debug_beam", "rt_debug_pose", "rt_env_beam_list", "rt_probe_random_rmw", "rt_probe_stream", "rt_host_sincos", "rt_host_tumour_sum", "rt_policy_sample", "rt_gae",
+    "rt_debug_beam", "rt_debug_pose", "rt_env_beam_list", "rt_probe_random_rmw", "rt_probe_stream", "rt_host_sincos", "rt_host_tumour_sum", "rt_host_lung_sum", "rt_policy_sample", "rt_gae",
     "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update", "rt_ppo_status",
     "rt_ppo_shuffle", "rt_ppo_shuffle_epochs", "rt_ppo_shuffle_adv", "rt_ppo_adv_stats", "rt_ppo_adv_sums", "rt_ppo_adv_finalize",
@@ -168,6 +168,7 @@ def load(build_if_missing: bool = True):
         "rt_probe_stream": ([vp, vp, i64, i32, i32, vp], ctypes.c_int),
         "rt_host_sincos": ([i32, vp, vp, vp], ctypes.c_int),
         "rt_host_tumour_sum": ([i64, i32, vp, vp, vp], ctypes.c_int),
+        "rt_host_lung_sum": ([ctypes.POINTER(i32), vp, vp, vp], ctypes.c_int),
         "rt_gae": ([i32, i32, vp, vp, vp, vp, vp, f64, f64, vp, vp, vp], ctypes.c_int),
         "rt_policy_sample": ([ctypes.POINTER(vp), i32, i32, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint64,
                               ctypes.c_uint64, i64, vp], ctypes.c_int),

@@ -43,15 +43,11 @@
 namespace {
 
 constexpr int kStepThreads = 256;
-// variant builds (tools/build_variant.py) override these two for sweeps
-#ifndef RT_DENSE_UNROLL
-#define RT_DENSE_UNROLL 8
-#endif
+// variant builds (tools/build_variant.py) override this for sweeps
 #ifndef RT_PIPE_DENSE_BPC
 #define RT_PIPE_DENSE_BPC 5
 #endif
 
-constexpr int kUnroll = RT_DENSE_UNROLL;  // k_dense: float4 loads in flight per thread (4/8 measured equal)
 // Library events order work between the library's own streams on one device
 // (the pipelined rollout's fork / turns / join) or time kernels; neither needs
 // the system-scope release + acquire (L2 writeback and invalidate) a default
@@ -669,98 +665,222 @@ __device__ __forceinline__ int wave_sum_i(int v) {
     return v;
 }
 
+__device__ __forceinline__ void lds_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Executes an exact-order sum plan (a tumour's, or a partial numpy buffer's
+// leaf tree) over the slots `tv` (leaves
+// 0..n-1 filled; op o writes slot n+o) level by level; returns the final sum
+// (0 for an empty tumour).  Every lane returns it.
+__device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const int32_t* lev, int nt, int nlev,
+                                          int result, int lane) {
+    int lo = 0;
+    for (int l = 0; l < nlev; ++l) {
+        lds_wave_sync();
+        const int hi = lev[l];
+        for (int o = lo + lane; o < hi; o += 64) {
+            const uint32_t ab = ops[o];
+            tv[nt + o] = tv[ab & 0xffffu] + tv[ab >> 16];
+        }
+        lo = hi;
+    }
+    lds_wave_sync();
+    return result >= 0 ? tv[result] : 0.0f;
+}
+
+// ---------------------------------------------------------------------------
+// The lung sum plan: np.sum(dose * lungs) (info doses.lung, environment.py:235)
+// in numpy's exact order.  numpy reduces a contiguous f32 volume in 8192-element
+// buffers, sequentially, each by pairwise summation: a buffer is split at
+// n/2 rounded down to a multiple of 8 until a part has <= 128 elements, and a
+// part (a "leaf") keeps 8 accumulators -- element i of the leaf goes to r[i % 8]
+// for the first n - n % 8 elements -- combined as ((r0+r1)+(r2+r3))+((r4+r5)+
+// (r6+r7)), then the n % 8 tail elements are added one by one (oracle/
+// rt_oracle.c:pairwise_f32).  Non-lung terms are exact zeros, and adding +0 to
+// a non-negative sum is exact, so each accumulator r[j] is the sequential sum of
+// its leaf's LUNG voxels of class j (a "chain", <= 16 long), a tail voxel is a
+// chain of one, and everything above the chains is a fixed tree.
+//
+// Dense visionless handles keep each dose row lung-first; the host builder
+// (build_lung_plan) orders the lung segment by numpy buffer ("chunk") and, inside
+// a chunk, by chain: the chains sorted by length, in groups of 64 (one per
+// lane), group rows stored ragged -- row k of a group holds element k of its
+// first nk[k] chains, contiguously -- so a wave streams a chunk with
+// coalesced dword loads, each lane summing its own chain in order with no
+// padding bytes.  The chain sums go to LDS slots [leaf][class]; lane = leaf
+// then combines its 8 slots, and a whole 8192-element buffer (64 leaves of
+// 128, a perfect tree) finishes with a 6-step xor butterfly (IEEE addition
+// commutes, so both lanes of a pair form the same sum).  A partial buffer (the
+// last one of a volume whose size is not a multiple of 8192) has an irregular
+// tree: its leaves add their tail voxels and run a level plan (run_plan).  The
+// chunk sums go to part_sum[e][chunk]; k_finish adds them in chunk order from
+// 0.0f -- numpy's outer loop (chunks without lung voxels add +0).
+// Vision handles keep C-order rows: the same plan, each segment position
+// gathered through lpos (segment position -> voxel).
+// ---------------------------------------------------------------------------
+constexpr int kLungChunk = 8192;        // numpy's reduction buffer
+constexpr int kLungLeafMax = 65;        // leaves of a buffer of <= 8192 elements (65 at 8185..8191)
+constexpr int kLungSlotFloats = 528;    // [leaf][8 classes], 16-B padded
+constexpr int kLungWaveFloats = kLungSlotFloats;  // a partial buffer's plan slots (2 x leaves) alias the slots
+constexpr uint16_t kNoSlot = 0xFFFFu;
+
+struct LChunk {          // one numpy buffer holding lung voxels
+    int32_t seg_base;    // segment position of its first chain element
+    int32_t grp_base;    // its first chain group
+    int32_t n_grp;
+    int32_t gen;         // -1: a whole 8192-element buffer (butterfly); else its LGeneric record
+};
+struct LGroup {          // 64 chains (lane l = chain l), sorted by length
+    int32_t seg_off;     // first element, relative to the chunk's seg_base
+    int32_t rows;        // length of its longest chain (lane 0)
+    uint8_t nk[16];      // lanes active in row k (non-increasing; 0 past `rows`)
+};
+struct LGeneric {        // a partial buffer's leaf tree
+    int32_t n_leaf, op_base, lvl_base, nlev, result, tail_base;
+};
+struct LungParams {
+    const LChunk* chunk;
+    const LGroup* grp;
+    const uint16_t* slot;     // [group][64] leaf * 8 + class, kNoSlot (tail voxel / no chain)
+    const LGeneric* gen;
+    const uint32_t* ops;      // partial buffers' leaf trees: (a | b << 16), dst = n_leaf + op
+    const int32_t* lvl_end;
+    const int32_t* tail_off;  // per partial buffer: [n_leaf + 1] into tail_pos
+    const int32_t* tail_pos;  // segment positions of each leaf's tail voxels, C order
+    const int32_t* lpos;      // C-order rows (vision): segment position -> voxel; null: lung-first
+    const int32_t* order;     // chunk indices, largest first (the persistent item order)
+    int32_t n_chunk;
+};
+
 struct DenseParams {
     Geom G;
     float lung_thr;
     EnvState st;
     const uint32_t* lung_bits;
-    int32_t* part_cnt;     // [N][slices]
-    double* part_sum;      // [N][slices]
-    int32_t slices;
-    int32_t vec_per_slice; // float4 per slice (of the streamed segment), multiple of 256
-    int32_t lung_n;        // lung-first rows: # lung voxels (the segment k_dense streams)
-    int32_t e_begin;       // env of blockIdx.y == 0 (env group of the pipelined rollout)
+    LungParams L;
+    int32_t* part_cnt;     // [N][L.n_chunk] lung voxels above the threshold per numpy buffer
+    float* part_sum;       // [N][L.n_chunk] np.sum order partial of each numpy buffer
+    int32_t slices;        // k_dense_vis: row slices per env
+    int32_t vec_per_slice; // k_dense_vis: float4 per slice
+    int32_t e_begin;       // first env (env group of the pipelined rollout)
 };
-
-#define LUNG_VOXEL(comp, bit)                                                      \
-    if ((lb >> (bit)) & 1u) {                                                      \
-        part += comp;                                                              \
-        cnt += comp > thr ? 1 : 0;                                                 \
-    }
 
 // ---------------------------------------------------------------------------
 // k_dense: the full-volume reductions of lungs_dose_reward
-// (environment.py:173-182) and info doses.lung (environment.py:235):
-// count(dose > 0.2 over lung voxels) and sum(dose over lung voxels) for every
-// env.  Only lung voxels contribute, and the rows are laid out lung-first, so
-// the reduction is a read-only float4 stream of each row's lung segment
-// (the first lung_n floats), split in 128 KiB slices (grid = slices x N); no
-// per-voxel mask.  Tumour voxels are corrected in k_finish.  A RESET env's
-// slices zero the whole row instead (reset_dose, environment.py:104).
+// (environment.py:173-182) and info doses.lung (environment.py:235) for every
+// env: count(dose > 0.2) over the lung voxels (tumour voxels are corrected in
+// k_finish) and np.sum(dose * lungs) in numpy's order (the lung sum plan
+// above).  Only lung voxels contribute and the rows are laid out lung-first,
+// so the reduction is a read-only stream of each row's lung segment with no
+// per-voxel mask; the work item is (env, numpy buffer), one wave each.
+// RESET envs' rows are zeroed instead (reset_dose, environment.py:104), by
+// zero_reset_share.
 // ---------------------------------------------------------------------------
-// Non-temporal 16-B load: the 4 GiB dose stream is read once per step and
-// far exceeds L2 / Infinity Cache; the nt policy lifts k_dense from 6.1 to
-// 7.0 TB/s (87 % of the HBM3E spec; profiles/r01_v6_*).
+// Non-temporal loads: the 1.6 GB of lung segments a step reads far exceed L2
+// and the Infinity Cache, and are read once (plain loads: 6.1 TB/s, nt: the
+// 6.3-6.6 TB/s regime; profiles/r01_v3..v6).
 __device__ __forceinline__ float4 load_nt(const float4* p) {
     typedef float nf4 __attribute__((ext_vector_type(4)));
     const nf4 t = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
     return make_float4(t.x, t.y, t.z, t.w);
 }
 
-// RESET envs' rows are zeroed by zero_reset_share, not by their slices.
-__device__ __forceinline__ void dense_item(const DenseParams& P, int sl, int e) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (P.st.setup[e].mode != MODE_STEP) return;
-    const float4* d4 = reinterpret_cast<const float4*>(P.st.dose + (size_t)e * P.G.Vpad);
-    const int n = P.lung_n;
-    const int q0 = sl * P.vec_per_slice;
-    const int q1 = min(q0 + P.vec_per_slice, (n + 3) >> 2);
+template <bool GATHER>
+__device__ __forceinline__ float lung_load(const DenseParams& P, const float* row, int pos) {
+    if constexpr (GATHER) return row[P.L.lpos[pos]];  // C-order row (vision): L2-resident map
+    else return __builtin_nontemporal_load(row + pos);
+}
+
+// One chain group: element k of lane l's chain (k < rows, l < nk[k]) -> x[k];
+// 0 elsewhere (an exact no-op for the chain sum and the count).
+template <bool GATHER>
+__device__ __forceinline__ void lung_fetch(const DenseParams& P, const float* row, int seg_base, int g, int lane,
+                                           float (&x)[16], int& slot) {
+    const LGroup& G = P.L.grp[g];
+    int pos = seg_base + G.seg_off;
+    const int rows = G.rows;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int nk = k < rows ? (int)G.nk[k] : 0;
+        x[k] = lane < nk ? lung_load<GATHER>(P, row, pos + lane) : 0.0f;
+        pos += nk;
+    }
+    slot = P.L.slot[(size_t)g * 64 + lane];
+}
+
+// the lane's chain in order (numpy's r[j] += a[i] sequence), its over-threshold
+// count, and the chain sum into its LDS slot
+__device__ __forceinline__ void lung_consume(const float (&x)[16], int rows, int slot, float thr, int& cnt,
+                                             float* slots) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (k < rows) {  // wave-uniform
+            acc = acc + x[k];
+            cnt += x[k] > thr ? 1 : 0;
+        }
+    }
+    if (slot != kNoSlot) slots[slot] = acc;
+}
+
+// Work item (env e, lung chunk j) of one wave: count and exact-order sum of
+// the chunk's lung voxels -> part_cnt / part_sum[e][j].  `wl`: the wave's
+// kLungWaveFloats of LDS.  The next group's loads are in flight while the
+// current one is summed.
+template <bool GATHER>
+__device__ void lung_item(const DenseParams& P, int e, int j, int lane, float* wl) {
+    const LChunk c = P.L.chunk[j];
+    const float* row = P.st.dose + (size_t)e * P.G.Vpad;
+    float* slots = wl;
+    // a partial buffer's leaf values and plan slots overwrite the class slots:
+    // lane L reads leaf L's 8 slots (all lanes in one instruction) before it
+    // writes leafv[L], and leaf L + 64 (lane 0's second pass) lies above 64
+    float* leafv = wl;
+    lds_wave_sync();  // the previous item's combine has read the slots
+    typedef float nf4 __attribute__((ext_vector_type(4)));
+    for (int i = lane; i < kLungSlotFloats / 4; i += 64) reinterpret_cast<nf4*>(slots)[i] = nf4{0.f, 0.f, 0.f, 0.f};
+    lds_wave_sync();
     const float thr = P.lung_thr;
     int cnt = 0;
-    double lsum = 0.0;
-    for (int base = q0; base < q1; base += kStepThreads * kUnroll) {
-        float4 v[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            int q = base + u * kStepThreads + tid;
-            v[u] = q < q1 ? load_nt(&d4[q]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const int q = base + u * kStepThreads + tid;
-            if (base + u * kStepThreads >= q1) break;  // block-uniform tail
-            // the segment's last float4 may hold non-lung voxels: zero them
-            // (a zero adds nothing and is never above the threshold)
-            float4 x = v[u];
-            if (4 * q + 3 >= n) {
-                if (4 * q + 1 >= n) x.y = 0.0f;
-                if (4 * q + 2 >= n) x.z = 0.0f;
-                if (4 * q + 3 >= n) x.w = 0.0f;
-            }
-            cnt += (x.x > thr ? 1 : 0) + (x.y > thr ? 1 : 0) + (x.z > thr ? 1 : 0) + (x.w > thr ? 1 : 0);
-            lsum += (((double)x.x + (double)x.y) + (double)x.z) + (double)x.w;
-        }
+    float xa[16], xb[16];
+    int sa = kNoSlot, sb = kNoSlot;
+    const int g0 = c.grp_base, g1 = c.grp_base + c.n_grp;
+    lung_fetch<GATHER>(P, row, c.seg_base, g0, lane, xa, sa);
+    for (int g = g0; g < g1; g += 2) {
+        if (g + 1 < g1) lung_fetch<GATHER>(P, row, c.seg_base, g + 1, lane, xb, sb);
+        lung_consume(xa, P.L.grp[g].rows, sa, thr, cnt, slots);
+        if (g + 2 < g1) lung_fetch<GATHER>(P, row, c.seg_base, g + 2, lane, xa, sa);
+        if (g + 1 < g1) lung_consume(xb, P.L.grp[g + 1].rows, sb, thr, cnt, slots);
     }
-    __shared__ int s_cnt[kStepThreads / 64];
-    __shared__ double s_sum[kStepThreads / 64];
+    lds_wave_sync();
+    float v;
+    if (c.gen < 0) {
+        // a whole buffer: lane = leaf (64 x 128 elements), leaf formula, then the
+        // perfect tree over the 64 leaves as an xor butterfly
+        const nf4 a = reinterpret_cast<const nf4*>(slots)[2 * lane];
+        const nf4 b = reinterpret_cast<const nf4*>(slots)[2 * lane + 1];
+        v = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
+    } else {
+        const LGeneric q = P.L.gen[c.gen];
+        for (int L = lane; L < q.n_leaf; L += 64) {
+            const nf4 a = reinterpret_cast<const nf4*>(slots)[2 * L];
+            const nf4 b = reinterpret_cast<const nf4*>(slots)[2 * L + 1];
+            float t = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+            const int t0 = P.L.tail_off[q.tail_base + L], t1 = P.L.tail_off[q.tail_base + L + 1];
+            for (int i = t0; i < t1; ++i) t = t + lung_load<GATHER>(P, row, P.L.tail_pos[i]);
+            leafv[L] = t;
+        }
+        v = run_plan(leafv, P.L.ops + q.op_base, P.L.lvl_end + q.lvl_base, q.n_leaf, q.nlev, q.result, lane);
+    }
     cnt = wave_sum_i(cnt);
-    lsum = wave_sum_d(lsum);
     if (lane == 0) {
-        s_cnt[wid] = cnt;
-        s_sum[wid] = lsum;
+        P.part_cnt[(size_t)e * P.L.n_chunk + j] = cnt;
+        P.part_sum[(size_t)e * P.L.n_chunk + j] = v;
     }
-    __syncthreads();
-    if (tid == 0) {
-        int c = 0;
-        double t = 0.0;
-        for (int w = 0; w < kStepThreads / 64; ++w) {
-            c += s_cnt[w];
-            t += s_sum[w];
-        }
-        P.part_cnt[(size_t)e * P.slices + sl] = c;
-        P.part_sum[(size_t)e * P.slices + sl] = t;
-    }
-    __syncthreads();  // s_cnt / s_sum are reused by the next item of a persistent block
 }
 
 // reset_dose (environment.py:104) of the RESET envs is not done by their own
@@ -833,26 +953,40 @@ __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, i
 }
 
 // Grid k_dense: the first zero_rows rows of blocks (dispatched first) zero
-// the RESET envs' rows in equal shares; the env blocks skip RESET envs.  (A
-// RESET env's own slices used to zero its row: 2.7x a slice's bytes, and such
-// a block dispatched near the end of the grid set the launch's tail.)
+// the RESET envs' rows in equal shares; the other blocks run 4 (env, chunk)
+// items, one per wave, largest chunks first so the launch's tail is made of
+// small items.  GATHER: C-order rows (vision handles, after k_dense_vis).
+template <bool GATHER>
 __global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env, int zero_rows) {
-    if ((int)blockIdx.y < zero_rows) {
+    if (!GATHER && (int)blockIdx.y < zero_rows) {
         zero_reset_share(P, P.e_begin, n_env, blockIdx.y * gridDim.x + blockIdx.x, zero_rows * gridDim.x);
         return;
     }
-    dense_item(P, blockIdx.x, P.e_begin + blockIdx.y - zero_rows);
+    __shared__ __attribute__((aligned(16))) float dsm[4 * kLungWaveFloats];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int it = (int)(((blockIdx.y - (GATHER ? 0 : zero_rows)) * gridDim.x + blockIdx.x) * 4 + w);
+    if (it >= n_env * P.L.n_chunk) return;  // wave-uniform
+    const int e = P.e_begin + it % n_env, j = P.L.order[it / n_env];
+    if (P.st.setup[e].mode != MODE_STEP) return;
+    lung_item<GATHER>(P, e, j, lane, dsm + w * kLungWaveFloats);
 }
 
-// k_dense with a fixed grid (a few blocks per CU) looping over the (env,
-// slice) items of envs [e_begin, e_begin + n_env): the pipelined dense
+// k_dense with a fixed grid (a few blocks per CU) whose waves stride over the
+// (env, chunk) items of envs [e_begin, e_begin + n_env): the pipelined dense
 // rollout's dose stream.  It leaves CU slots free for the other env group's
 // latency-bound kernels (the grid version fills every slot and has a launch
-// tail), and 6 blocks x 4 waves per CU keep ~16 MB of loads in flight.
+// tail).  Items are ordered chunk-major, largest chunks first, env-minor, so a
+// wave's strided items sample every chunk size (an env-major order would give
+// each wave one fixed chunk index: a 250x spread of bytes per wave).
 __global__ __launch_bounds__(256) void k_dense_persist(DenseParams P, int n_env) {
-    const int n_items = n_env * P.slices;
-    for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-        dense_item(P, it % P.slices, P.e_begin + it / P.slices);
+    __shared__ __attribute__((aligned(16))) float dsm[4 * kLungWaveFloats];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n_items = n_env * P.L.n_chunk;
+    for (int it = blockIdx.x * 4 + w; it < n_items; it += gridDim.x * 4) {
+        const int e = P.e_begin + it % n_env, j = P.L.order[it / n_env];
+        if (P.st.setup[e].mode != MODE_STEP) continue;  // wave-uniform
+        lung_item<false>(P, e, j, lane, dsm + w * kLungWaveFloats);
+    }
     zero_reset_share(P, P.e_begin, n_env, blockIdx.x, gridDim.x);
 }
 
@@ -884,17 +1018,18 @@ struct DenseVisParams {
 };
 
 // ---------------------------------------------------------------------------
-// k_dense_vis: k_dense plus the dense channels of the vision observation
+// k_dense_vis: the dense channels of the vision observation
 // (environment.py:252-257, get_volumes): channel 0 = clip(lungs), channel 2 =
 // clip(dose) (dose is already in [0,1]); channels 1 (tumour) and 3 (beam view)
-// are zeroed here and scattered by k_finish.  Runs for every mode: STEP also
-// reduces, RESET zeroes the dose, NOOP (a reset call's unselected envs) only
-// re-emits the observation.
+// are zeroed here and scattered by k_finish.  Runs for every mode: RESET
+// zeroes the dose, NOOP (a reset call's unselected envs) only re-emits the
+// observation.  The STEP envs' lung reductions follow as k_dense<true> (the
+// lung sum plan gathered from the C-order row).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_dense_vis(DenseVisParams PV) {
     const DenseParams& P = PV.d;
     const int sl = blockIdx.x, e = P.e_begin + blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x;
     const int mode = P.st.setup[e].mode;
     float4* d4 = reinterpret_cast<float4*>(P.st.dose + (size_t)e * P.G.Vpad);
     if (mode == MODE_NOOP && e < PV.src_n)  // (the source rows are 16-B aligned: checked by the setter)
@@ -909,9 +1044,6 @@ __global__ __launch_bounds__(256) void k_dense_vis(DenseVisParams PV) {
     const int q0 = sl * P.vec_per_slice;
     const int q1 = min(q0 + P.vec_per_slice, nvec);
     const uint32_t* lbits = P.lung_bits;
-    const float thr = P.lung_thr;
-    int cnt = 0;
-    double lsum = 0.0;
     for (int q = q0 + tid; q < q1; q += kStepThreads) {
         const int v0 = q << 2;
         float4 v;
@@ -929,34 +1061,6 @@ __global__ __launch_bounds__(256) void k_dense_vis(DenseVisParams PV) {
             store4(o2, v0, V, al4, v.x, v.y, v.z, v.w);
             store4(o3, v0, V, al4, 0.f, 0.f, 0.f, 0.f);
         }
-        if (mode == MODE_STEP) {
-            float part = 0.0f;
-            LUNG_VOXEL(v.x, 0)
-            LUNG_VOXEL(v.y, 1)
-            LUNG_VOXEL(v.z, 2)
-            LUNG_VOXEL(v.w, 3)
-            lsum += (double)part;
-        }
-    }
-    if (mode != MODE_STEP) return;  // block-uniform
-    __shared__ int s_cnt[kStepThreads / 64];
-    __shared__ double s_sum[kStepThreads / 64];
-    cnt = wave_sum_i(cnt);
-    lsum = wave_sum_d(lsum);
-    if (lane == 0) {
-        s_cnt[wid] = cnt;
-        s_sum[wid] = lsum;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int c = 0;
-        double t = 0.0;
-        for (int w = 0; w < kStepThreads / 64; ++w) {
-            c += s_cnt[w];
-            t += s_sum[w];
-        }
-        P.part_cnt[(size_t)e * P.slices + sl] = c;
-        P.part_sum[(size_t)e * P.slices + sl] = t;
     }
 }
 
@@ -986,9 +1090,9 @@ struct FinishParams {
     float* reward;       // [N]
     uint8_t* terminated; // [N]
     float* info;         // [N][RT_INFO_W] or null
-    const int32_t* part_cnt;
-    const double* part_sum;
-    int32_t slices;
+    const int32_t* part_cnt;  // [N][n_chunk] (k_dense)
+    const float* part_sum;    // [N][n_chunk]
+    int32_t n_chunk;          // numpy buffers holding lung voxels
     int32_t max_tvox;    // per-wave LDS holds the sum plan of tumours up to max_tvox voxels
     float* gscratch;     // larger tumours (k_rollout_policy's smaller LDS share): plan slots
     int64_t gscratch_stride;  //   here, gscratch + e * stride, operands read from the library
@@ -999,8 +1103,26 @@ struct FinishParams {
     uint32_t hash_mask;  // vision: beam-view hash slots - 1
     int32_t wave_lds;    // bytes of LDS per wave
     int32_t wpb;         // envs (waves) per block: 4, or fewer when big tumours need the LDS
-    int32_t lung_n;      // lung-first rows: # lung voxels (persistent dense rollout: the wave's stream)
 };
+
+// np.sum(dose * lungs) from the env's chunk partials (lane u of pv[k] holds
+// chunk 64 k + u): numpy's outer loop, sequential in chunk order from 0.0f
+// (buffers without lung voxels add +0, an exact no-op).
+constexpr int kPartPF = 4;  // chunk partials per lane loaded ahead of the tumour gather (<= 256 chunks)
+__device__ __forceinline__ float chunk_fold(const float (&pv)[kPartPF], const FinishParams& P, int e, int lane) {
+    float acc = 0.0f;
+    const int n = P.n_chunk;
+#pragma unroll
+    for (int k = 0; k < kPartPF; ++k)
+        for (int u = 0; u < 64 && 64 * k + u < n; ++u)
+            acc = acc + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv[k]), u));
+    for (int j0 = 64 * kPartPF; j0 < n; j0 += 64) {  // > 256 chunks (grids above ~2.1 M voxels)
+        const float x = j0 + lane < n ? P.part_sum[(size_t)e * n + j0 + lane] : 0.0f;
+        for (int u = 0; u < 64 && j0 + u < n; ++u)
+            acc = acc + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), u));
+    }
+    return acc;
+}
 
 __device__ __forceinline__ void write_obs9(float* obs, const Geom& G, int e, const double* pose,
                                            const TumourMeta& m) {
@@ -1013,10 +1135,6 @@ __device__ __forceinline__ void write_obs9(float* obs, const Geom& G, int e, con
     }
 }
 
-__device__ __forceinline__ void lds_wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // Splats of one beam into the wave's LDS hash (lane k: iterations k, k+64, ...).
 __device__ void hash_beam(const Geom& G, const BeamSetup& b, int lane, int32_t* keys, float* vals,
@@ -1096,25 +1214,6 @@ __device__ void vision_scatter(const FinishParams& P, int e, int lane, const dou
 //  - combine k_dense slices; rewards (environment.py:164-191), termination,
 //    obs (environment.py:259-268), info, episode statistics
 // ---------------------------------------------------------------------------
-// Executes a tumour's exact-order sum plan over the slots `tv` (leaves
-// 0..n-1 filled; op o writes slot n+o) level by level; returns the final sum
-// (0 for an empty tumour).  Every lane returns it.
-__device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const int32_t* lev, int nt, int nlev,
-                                          int result, int lane) {
-    int lo = 0;
-    for (int l = 0; l < nlev; ++l) {
-        lds_wave_sync();
-        const int hi = lev[l];
-        for (int o = lo + lane; o < hi; o += 64) {
-            const uint32_t ab = ops[o];
-            tv[nt + o] = tv[ab & 0xffffu] + tv[ab >> 16];
-        }
-        lo = hi;
-    }
-    lds_wave_sync();
-    return result >= 0 ? tv[result] : 0.0f;
-}
-
 // PF (k_finish): the step's independent scalars (the env's dense partial
 // sums, t, episode return / length) are loaded before the tumour gather; the
 // nearest tumour voxel's packed coordinates travel with the distance argmin,
@@ -1166,13 +1265,22 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     }
     // PF: independent loads of the tail, issued before the gather
     int pf_cnt = 0, pf_t = 0, pf_len = 0;
-    double pf_dl = 0.0, pf_ret = 0.0;
+    double pf_ret = 0.0;
+    float pv[kPartPF];
+#pragma unroll
+    for (int k = 0; k < kPartPF; ++k) pv[k] = 0.0f;
     if constexpr (PF) {
-        if (!P.incremental)
-            for (int j = lane; j < P.slices; j += 64) {
-                pf_cnt += P.part_cnt[(size_t)e * P.slices + j];
-                pf_dl += P.part_sum[(size_t)e * P.slices + j];
+        if (!P.incremental) {
+#pragma unroll
+            for (int k = 0; k < kPartPF; ++k) {
+                const int j = 64 * k + lane;
+                if (j < P.n_chunk) {
+                    pf_cnt += P.part_cnt[(size_t)e * P.n_chunk + j];
+                    pv[k] = P.part_sum[(size_t)e * P.n_chunk + j];
+                }
             }
+            for (int j = 64 * kPartPF + lane; j < P.n_chunk; j += 64) pf_cnt += P.part_cnt[(size_t)e * P.n_chunk + j];
+        }
         if (lane == 0) {
             pf_t = P.st.t[e];
             pf_ret = P.st.ep_return[e];
@@ -1244,22 +1352,22 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
     }
     if (lane == 0) RT_STAMP(e, 7);
     int cnt = 0;
-    double dl = 0.0;
+    float dl = 0.0f;
     if (P.incremental) {
+        // maintained by k_beam: exact count, f64 sum rounded once
         cnt = P.st.lung_cnt[e];
-        dl = P.st.lung_sum[e];
+        dl = (float)P.st.lung_sum[e];
     } else {
         if constexpr (PF) {
             cnt = pf_cnt;
-            dl = pf_dl;
         } else {
-            for (int j = lane; j < P.slices; j += 64) {
-                cnt += P.part_cnt[(size_t)e * P.slices + j];
-                dl += P.part_sum[(size_t)e * P.slices + j];
-            }
+#pragma unroll
+            for (int k = 0; k < kPartPF; ++k)
+                if (64 * k + lane < P.n_chunk) pv[k] = P.part_sum[(size_t)e * P.n_chunk + 64 * k + lane];
+            for (int j = lane; j < P.n_chunk; j += 64) cnt += P.part_cnt[(size_t)e * P.n_chunk + j];
         }
         cnt = wave_sum_i(cnt);
-        dl = wave_sum_d(dl);
+        dl = chunk_fold(pv, P, e, lane);
     }
     if (lane == 0) {
         const long long c = (long long)cnt - ctum;  // lungs * (1 - tumours)
@@ -1287,7 +1395,7 @@ __device__ void finish_env(const FinishParams& P, int e, int lane, unsigned char
             inf[RT_INFO_LUNG] = (float)r_lung;
             inf[RT_INFO_DISTANCE] = (float)r_dist;
             inf[RT_INFO_DOSE_TUMOUR] = S;
-            inf[RT_INFO_DOSE_LUNG] = (float)dl;
+            inf[RT_INFO_DOSE_LUNG] = dl;
             for (int i = 0; i < 3; ++i) {
                 inf[RT_INFO_OVERSHOOT_T + i] = s.os_t[i];
                 inf[RT_INFO_POS + i] = (float)pose[i];
@@ -1781,6 +1889,216 @@ struct PlanBuilder {
     }
 };
 
+// Host side of the lung sum plan (see LChunk): numpy's leaves of one buffer
+// [start, start + len) in order, and its tree as PlanBuilder-style ops.
+struct LeafTree {
+    std::vector<std::pair<int64_t, int64_t>> leaves;
+    std::vector<int> opa, opb, lvl;
+    int n_leaf = 0;
+    int level(int s) const { return s < n_leaf ? 0 : lvl[s - n_leaf]; }
+    void split(int64_t start, int64_t len) {
+        if (len <= 128) {
+            leaves.push_back({start, len});
+            return;
+        }
+        int64_t n2 = len / 2;
+        n2 -= n2 % 8;
+        split(start, n2);
+        split(start + n2, len - n2);
+    }
+    int tree(int64_t len, int& next_leaf) {  // same recursion, emitting the adds
+        if (len <= 128) return next_leaf++;
+        int64_t n2 = len / 2;
+        n2 -= n2 % 8;
+        const int a = tree(n2, next_leaf);
+        const int b = tree(len - n2, next_leaf);
+        opa.push_back(a);
+        opb.push_back(b);
+        lvl.push_back(std::max(level(a), level(b)) + 1);
+        return n_leaf + (int)opa.size() - 1;
+    }
+};
+
+struct LungPlanHost {
+    int64_t V = 0;
+    int32_t n_seg = 0;            // lung voxels
+    std::vector<int32_t> pos_of;  // [V] voxel -> segment position (-1: not lung)
+    std::vector<int32_t> lpos;    // [n_seg] segment position -> voxel
+    std::vector<LChunk> chunk;
+    std::vector<LGroup> grp;
+    std::vector<uint16_t> slot;
+    std::vector<LGeneric> gen;
+    std::vector<uint32_t> ops;
+    std::vector<int32_t> lvl_end, tail_off, tail_pos, order;
+};
+
+// Lays out the lung segment by numpy buffer, then by chain (LChunk comment):
+// chains of a buffer sorted by length (longest first, ties in slot order),
+// 64 per group, ragged rows.
+int build_lung_plan(const uint8_t* lungs, int64_t V, LungPlanHost& P) {
+    P.V = V;
+    P.pos_of.assign((size_t)V, -1);
+    P.lpos.clear();
+    int32_t seg = 0;
+    struct Chain {
+        uint16_t slot;
+        std::vector<int32_t> vox;
+    };
+    for (int64_t c0 = 0; c0 < V; c0 += kLungChunk) {
+        const int64_t len = std::min<int64_t>(kLungChunk, V - c0);
+        bool any = false;
+        for (int64_t v = c0; v < c0 + len && !any; ++v) any = lungs[v] != 0;
+        if (!any) continue;
+        LeafTree lt;
+        lt.split(c0, len);
+        const int nl = (int)lt.leaves.size();
+        if (nl > kLungLeafMax) return fail(RT_ELIMIT, "lung sum plan: more leaves per buffer than expected");
+        std::vector<Chain> chains;
+        std::vector<std::vector<int32_t>> tails(nl);
+        for (int li = 0; li < nl; ++li) {
+            const int64_t s = lt.leaves[li].first, n = lt.leaves[li].second;
+            const int64_t m = n < 8 ? 0 : n - n % 8;
+            for (int j = 0; j < 8; ++j) {
+                Chain ch{(uint16_t)(li * 8 + j), {}};
+                for (int64_t v = s + j; v < s + m; v += 8)
+                    if (lungs[v]) ch.vox.push_back((int32_t)v);
+                if (!ch.vox.empty()) chains.push_back(std::move(ch));
+            }
+            for (int64_t v = s + m; v < s + n; ++v)
+                if (lungs[v]) {
+                    tails[li].push_back((int32_t)v);
+                    chains.push_back(Chain{kNoSlot, {(int32_t)v}});
+                }
+        }
+        std::stable_sort(chains.begin(), chains.end(),
+                         [](const Chain& a, const Chain& b) { return a.vox.size() > b.vox.size(); });
+        LChunk ch{};
+        ch.seg_base = seg;
+        ch.grp_base = (int32_t)P.grp.size();
+        for (size_t g0 = 0; g0 < chains.size(); g0 += 64) {
+            const size_t g1 = std::min(chains.size(), g0 + 64);
+            LGroup G{};
+            G.seg_off = seg - ch.seg_base;
+            G.rows = (int32_t)chains[g0].vox.size();
+            if (G.rows > 16) return fail(RT_ELIMIT, "lung sum plan: chain longer than 16");
+            for (int k = 0; k < G.rows; ++k) {
+                int nk = 0;
+                for (size_t l = g0; l < g1; ++l) nk += (int)chains[l].vox.size() > k ? 1 : 0;
+                G.nk[k] = (uint8_t)nk;
+                for (int l = 0; l < nk; ++l) {
+                    const int32_t v = chains[g0 + l].vox[k];
+                    P.pos_of[v] = seg + l;
+                    P.lpos.push_back(v);
+                }
+                seg += nk;
+            }
+            P.grp.push_back(G);
+            for (size_t l = g0; l < g0 + 64; ++l) P.slot.push_back(l < g1 ? chains[l].slot : kNoSlot);
+        }
+        ch.n_grp = (int32_t)P.grp.size() - ch.grp_base;
+        ch.gen = -1;
+        if (len != kLungChunk) {
+            LGeneric q{};
+            q.n_leaf = nl;
+            lt.n_leaf = nl;
+            int next = 0;
+            const int res = lt.tree(len, next);
+            const int nops = (int)lt.opa.size();
+            std::vector<int> ord(nops), remap(nops);
+            for (int o = 0; o < nops; ++o) ord[o] = o;
+            std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return lt.lvl[x] < lt.lvl[y]; });
+            for (int o = 0; o < nops; ++o) remap[ord[o]] = o;
+            auto slot = [&](int s) { return s < nl ? s : nl + remap[s - nl]; };
+            q.op_base = (int32_t)P.ops.size();
+            q.lvl_base = (int32_t)P.lvl_end.size();
+            for (int o = 0; o < nops; ++o) {
+                const int src = ord[o];
+                P.ops.push_back((uint32_t)slot(lt.opa[src]) | ((uint32_t)slot(lt.opb[src]) << 16));
+                if (o + 1 == nops || lt.lvl[ord[o + 1]] != lt.lvl[src]) {
+                    P.lvl_end.push_back(o + 1);
+                    ++q.nlev;
+                }
+            }
+            q.result = slot(res);
+            q.tail_base = (int32_t)P.tail_off.size();
+            for (int li = 0; li < nl; ++li) {
+                P.tail_off.push_back((int32_t)P.tail_pos.size());
+                for (int32_t v : tails[li]) P.tail_pos.push_back(P.pos_of[v]);
+            }
+            P.tail_off.push_back((int32_t)P.tail_pos.size());
+            ch.gen = (int32_t)P.gen.size();
+            P.gen.push_back(q);
+        }
+        P.chunk.push_back(ch);
+    }
+    P.n_seg = seg;
+    // the persistent item order: chunks by size, largest first
+    const int nc = (int)P.chunk.size();
+    auto csize = [&](int j) { return (j + 1 < nc ? P.chunk[j + 1].seg_base : seg) - P.chunk[j].seg_base; };
+    P.order.resize(nc);
+    for (int j = 0; j < nc; ++j) P.order[j] = j;
+    std::stable_sort(P.order.begin(), P.order.end(), [&](int a, int b) { return csize(a) > csize(b); });
+    return RT_OK;
+}
+
+// The plan evaluated on the host exactly as k_dense + k_finish evaluate it
+// (chains, LDS slots, leaf formula, butterfly or level plan, chunk fold):
+// np.sum(dose * lungs) of a C-order f32 volume (parity hook).
+float eval_lung_plan(const LungPlanHost& P, const float* dose) {
+    float acc = 0.0f;
+    for (size_t j = 0; j < P.chunk.size(); ++j) {
+        const LChunk& c = P.chunk[j];
+        float slots[kLungSlotFloats] = {};
+        for (int g = c.grp_base; g < c.grp_base + c.n_grp; ++g) {
+            const LGroup& G = P.grp[g];
+            float chain[64] = {};
+            int pos = c.seg_base + G.seg_off;
+            for (int k = 0; k < G.rows; ++k) {
+                for (int l = 0; l < G.nk[k]; ++l) chain[l] = chain[l] + dose[P.lpos[pos + l]];
+                pos += G.nk[k];
+            }
+            for (int l = 0; l < 64; ++l)
+                if (P.slot[(size_t)g * 64 + l] != kNoSlot) slots[P.slot[(size_t)g * 64 + l]] = chain[l];
+        }
+        auto leaf = [&](int L) {
+            const float* r = slots + 8 * L;
+            return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        };
+        float v;
+        if (c.gen < 0) {
+            float lv[64];
+            for (int L = 0; L < 64; ++L) lv[L] = leaf(L);
+            for (int off = 1; off < 64; off <<= 1) {
+                float nx[64];
+                for (int L = 0; L < 64; ++L) nx[L] = lv[L] + lv[L ^ off];
+                std::copy(nx, nx + 64, lv);
+            }
+            v = lv[0];
+        } else {
+            const LGeneric& q = P.gen[c.gen];
+            std::vector<float> tv((size_t)2 * q.n_leaf);
+            for (int L = 0; L < q.n_leaf; ++L) {
+                float t = leaf(L);
+                for (int i = P.tail_off[q.tail_base + L]; i < P.tail_off[q.tail_base + L + 1]; ++i)
+                    t = t + dose[P.lpos[P.tail_pos[i]]];
+                tv[L] = t;
+            }
+            int lo = 0;
+            for (int l = 0; l < q.nlev; ++l) {
+                const int hi = P.lvl_end[q.lvl_base + l];
+                for (int o = lo; o < hi; ++o) {
+                    const uint32_t ab = P.ops[q.op_base + o];
+                    tv[q.n_leaf + o] = tv[ab & 0xffffu] + tv[ab >> 16];
+                }
+                lo = hi;
+            }
+            v = tv[q.result];
+        }
+        acc = acc + v;
+    }
+    return acc;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1802,6 +2120,8 @@ struct rt_env {
     int vec_per_slice = 0;   // float4 per slice
     int lung_first = 0;      // dose rows lung-first (dense visionless), else C order
     int lung_n = 0;          // lung voxels (the lung-first segment)
+    int n_chunk = 0;         // numpy buffers holding lung voxels (k_dense items per env)
+    LungParams lplan{};      // the lung sum plan (device copies)
     int32_t* dose_pos_d = nullptr;  // voxel -> row position (lung_first)
     size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
     int finish_wave_lds = 0; // bytes per wave
@@ -1820,7 +2140,7 @@ struct rt_env {
     float* gscratch = nullptr;  // [N][2 * max_tvox] plan slots of tumours above a kernel's LDS capacity
     uint32_t view_hash_mask = 0;
     int32_t* part_cnt = nullptr;
-    double* part_sum = nullptr;
+    float* part_sum = nullptr;
     // optional live kernel timing: 4 events per step (before k_beam, k_dense,
     // k_finish, after k_finish) in a ring of `timing_cap` steps
     std::vector<hipEvent_t> tev;
@@ -1849,6 +2169,31 @@ int dev_alloc(rt_env* env, T** p, size_t count) {
     if (e != hipSuccess) return fail(RT_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
     env->allocs.push_back(q);
     *p = static_cast<T*>(q);
+    return RT_OK;
+}
+
+template <typename T>
+int dev_upload(rt_env* env, const T** p, const std::vector<T>& h) {
+    T* d = nullptr;
+    if (int rc = dev_alloc(env, &d, h.size())) return rc;
+    if (!h.empty() && hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(RT_EDEVICE, "lung sum plan upload failed");
+    *p = d;
+    return RT_OK;
+}
+
+int upload_lung_plan(rt_env* env, const LungPlanHost& lp) {
+    LungParams& L = env->lplan;
+    int rc;
+    if ((rc = dev_upload(env, &L.chunk, lp.chunk)) || (rc = dev_upload(env, &L.grp, lp.grp)) ||
+        (rc = dev_upload(env, &L.slot, lp.slot)) || (rc = dev_upload(env, &L.gen, lp.gen)) ||
+        (rc = dev_upload(env, &L.ops, lp.ops)) || (rc = dev_upload(env, &L.lvl_end, lp.lvl_end)) ||
+        (rc = dev_upload(env, &L.tail_off, lp.tail_off)) || (rc = dev_upload(env, &L.tail_pos, lp.tail_pos)) ||
+        (rc = dev_upload(env, &L.order, lp.order)))
+        return rc;
+    L.lpos = nullptr;
+    if (!env->lung_first && (rc = dev_upload(env, &L.lpos, lp.lpos))) return rc;
+    L.n_chunk = (int32_t)lp.chunk.size();
     return RT_OK;
 }
 
@@ -1937,6 +2282,16 @@ int rt_host_tumour_sum(int64_t V, int32_t n, const int32_t* idx_h, const float* 
         slot[(size_t)n + src] = slot[pb.opa[src]] + slot[pb.opb[src]];
     }
     *out_h = res < 0 ? 0.0f : slot[res];
+    return RT_OK;
+}
+
+int rt_host_lung_sum(const int32_t grid[3], const uint8_t* lungs_h, const float* dose_h, float* out_h) {
+    if (!grid || !lungs_h || !dose_h || !out_h) return fail(RT_EINVAL, "NULL argument");
+    Geom G{};
+    if (int rc = fill_geom(grid, G)) return rc;
+    LungPlanHost lp;
+    if (int rc = build_lung_plan(lungs_h, G.V, lp)) return rc;
+    *out_h = eval_lung_plan(lp, dose_h);
     return RT_OK;
 }
 
@@ -2029,15 +2384,24 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
             ++lung_count;
         }
     }
-    // dense visionless: lung-first dose rows (k_dense streams the lung segment)
+    // dense handles: the lung sum plan (k_dense); dense visionless handles keep
+    // their rows lung-first in the plan's segment order (k_dense streams the
+    // lung segment), vision handles C order (k_dense<true> gathers)
     env->lung_first = env->visionless && !env->incremental;
     env->lung_n = (int)lung_count;
+    LungPlanHost lp;
+    if (!env->incremental)
+        if (int rc_plan = build_lung_plan(cfg->lungs_h, G.V, lp)) {
+            free_env(env);
+            return rc_plan;
+        }
     std::vector<int32_t> dpos;
     if (env->lung_first) {
         dpos.resize(G.V);
-        int64_t a = 0, b = lung_count;
-        for (int64_t v = 0; v < G.V; ++v) dpos[v] = (int32_t)(cfg->lungs_h[v] ? a++ : b++);
+        int64_t b = lung_count;
+        for (int64_t v = 0; v < G.V; ++v) dpos[v] = lp.pos_of[v] >= 0 ? lp.pos_of[v] : (int32_t)b++;
     }
+    env->n_chunk = (int)lp.chunk.size();
     std::vector<TumourMeta> meta(K);
     std::vector<int32_t> vox, vpos;
     std::vector<uint32_t> coord;
@@ -2112,10 +2476,9 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
     env->lib.K = K;
     env->max_tvox = max_n;
     const int nvec = G.Vpad / 4;
-    // k_dense streams the lung segment (lung-first rows); k_dense_vis whole rows
-    const int svec = env->lung_first ? std::max(1, (env->lung_n + 3) / 4) : nvec;
-    env->vec_per_slice = std::min(svec, kSliceVec);
-    env->slices = (svec + env->vec_per_slice - 1) / env->vec_per_slice;
+    // k_dense_vis: whole rows in slices
+    env->vec_per_slice = std::min(nvec, kSliceVec);
+    env->slices = (nvec + env->vec_per_slice - 1) / env->vec_per_slice;
     const int maxdim = std::max(G.g[0], std::max(G.g[1], G.g[2]));
     env->view_hash_mask = env->visionless ? 0u : next_pow2((uint32_t)(8 * (maxdim + 2))) - 1;
     // per wave: plan slots (2 n floats), then either the plan's operands and
@@ -2181,8 +2544,9 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         (rc = dev_alloc(env, &st.ep_return, N)) || (rc = dev_alloc(env, &st.ep_len, N)) ||
         (rc = dev_alloc(env, &st.next_tumour, N)) || (rc = dev_alloc(env, &st.setup, N)) ||
         (rc = dev_alloc(env, &st.mode_b, N)) ||
-        (rc = dev_alloc(env, &env->part_cnt, (size_t)N * env->slices)) ||
-        (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->slices)) ||
+        (rc = dev_alloc(env, &env->part_cnt, (size_t)N * env->n_chunk)) ||
+        (rc = dev_alloc(env, &env->part_sum, (size_t)N * env->n_chunk)) ||
+        (!env->incremental && (rc = upload_lung_plan(env, lp))) ||
         (rc = dev_alloc(env, &st.lung_cnt, N)) || (rc = dev_alloc(env, &st.lung_sum, N)) ||
         // the persistent rollout's plan slots for tumours above its LDS share
         (env->incremental && env->rollout_wpb && env->rollout_cap < max_n &&
@@ -2280,7 +2644,7 @@ FinishParams finish_params(const rt_env* env, float* obs, float* reward, uint8_t
     fp.info = info;
     fp.part_cnt = env->part_cnt;
     fp.part_sum = env->part_sum;
-    fp.slices = env->slices;
+    fp.n_chunk = env->n_chunk;
     fp.max_tvox = env->max_tvox;
     fp.gscratch = nullptr;
     fp.gscratch_stride = 0;
@@ -2290,7 +2654,6 @@ FinishParams finish_params(const rt_env* env, float* obs, float* reward, uint8_t
     fp.hash_mask = env->view_hash_mask;
     fp.wave_lds = env->finish_wave_lds;
     fp.wpb = env->finish_wpb;
-    fp.lung_n = env->lung_n;
     return fp;
 }
 
@@ -2329,9 +2692,9 @@ DenseParams dense_params(const rt_env* env, int e0) {
     dp.lung_bits = env->lib.lung_bits;
     dp.part_cnt = env->part_cnt;
     dp.part_sum = env->part_sum;
+    dp.L = env->lplan;
     dp.slices = env->slices;
     dp.vec_per_slice = env->vec_per_slice;
-    dp.lung_n = env->lung_n;
     dp.e_begin = e0;
     return dp;
 }
@@ -2347,14 +2710,24 @@ int launch_dense(rt_env* env, int e0, int n, float* obs, int persist_bpc, hipStr
             hipLaunchKernelGGL(k_dense_persist, dim3(persist_bpc * env->num_cu), dim3(kStepThreads), 0, stream, dp,
                                n);
         } else {
-            const int zrows = (kZeroBlocks + env->slices - 1) / env->slices;
-            hipLaunchKernelGGL(k_dense, dim3(env->slices, n + zrows), dim3(kStepThreads), 0, stream, dp, n, zrows);
+            // one wave per (env, chunk) item, 4 per block, after kZeroBlocks zeroing blocks
+            const int64_t blocks = ((int64_t)n * env->n_chunk + 3) / 4;
+            const int gx = kZeroBlocks;
+            const int rows = (int)((blocks + gx - 1) / gx);
+            hipLaunchKernelGGL(k_dense<false>, dim3(gx, rows + 1), dim3(kStepThreads), 0, stream, dp, n, 1);
         }
         RT_LAUNCH_CHECK("k_dense");
     } else {
         DenseVisParams dv{dp, obs, env->render_src, env->render_rows, env->render_stride, env->render_n};
         hipLaunchKernelGGL(k_dense_vis, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dv);
         RT_LAUNCH_CHECK("k_dense_vis");
+        const int64_t blocks = ((int64_t)n * env->n_chunk + 3) / 4;
+        if (blocks > 0) {
+            const int gx = (int)std::min<int64_t>(blocks, kZeroBlocks);
+            const int rows = (int)((blocks + gx - 1) / gx);
+            hipLaunchKernelGGL(k_dense<true>, dim3(gx, rows), dim3(kStepThreads), 0, stream, dp, n, 0);
+            RT_LAUNCH_CHECK("k_dense<gather>");
+        }
     }
     return RT_OK;
 }

@@ -47,6 +47,8 @@ def test_reference_binding_steps_match_oracle():
             assert abs(got[t][1][e] - info[0]) <= 1e-5
             assert bool(got[t][2][e]) == bool(done)
             np.testing.assert_allclose(got[t][3][e][:4], info[:4], rtol=0, atol=1e-5)
+            # doses.tumour / doses.lung: numpy's f32 sums, bit-exact (dense mode)
+            assert got[t][3][e][4] == np.float32(info[4]) and got[t][3][e][5] == np.float32(info[5])
             if done:
                 break
     env.close()

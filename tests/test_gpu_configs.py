@@ -82,6 +82,7 @@ def test_config4_vision_env_128_vs_oracle():
         obs, rew, term, _, infos = env.step(a)
         a_h, r_h, term_h = a.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy()
         rc = {k: infos["reward_components"][k].cpu().numpy() for k in ("tumour", "lung", "distance_to_tumour")}
+        dz = {k: infos["doses"][k].cpu().numpy() for k in ("tumour", "lung")}
         stepped = infos["_reward_components"].cpu().numpy()
         for e in sample:
             if pending[e]:
@@ -95,6 +96,9 @@ def test_config4_vision_env_128_vs_oracle():
             assert abs(r_h[e] - oi[0]) <= 1e-5, (e, t, r_h[e], oi[0])
             assert abs(rc["tumour"][e] - oi[1]) <= 1e-5 and abs(rc["lung"][e] - oi[2]) <= 1e-5
             assert abs(rc["distance_to_tumour"][e] - oi[3]) <= 1e-5
+            # doses (environment.py:233-236): bit-exact -- doses.lung through the
+            # lung sum plan gathered from the C-order rows (k_dense<true>)
+            assert dz["tumour"][e] == np.float32(oi[4]) and dz["lung"][e] == np.float32(oi[5]), (e, t)
             assert bool(term_h[e]) == done, (e, t)
             pending[e] = done
     assert all(draws[e] >= 2 for e in sample)  # every sampled env crossed an autoreset

@@ -39,6 +39,9 @@ def test_facade_replays_reference_trajectory(golden):
             np.testing.assert_array_equal(np.array(info["beam_position"]["translation"]), z["step_pos"][k])
             assert abs(r - z["step_reward"][k]) <= 1e-5 and trunc is False
             assert abs(info["reward_components"]["tumour"] - z["step_tumour"][k]) <= 1e-5
+            # doses (environment.py:233-236): the reference's f32 np.sum values, bit-exact
+            assert info["doses"]["tumour"] == float(np.float32(z["step_dose_tumour"][k]))
+            assert info["doses"]["lung"] == float(np.float32(z["step_dose_lung"][k]))
             assert done == bool(z["step_done"][k])
         off += int(z["ep_len"][e])
         lo, hi = z["dose_off"][e], z["dose_off"][e + 1]
