@@ -43,6 +43,11 @@ Also reported:
                          128-B line RMWs per env-step) vs a measured random-line
                          RMW ceiling (rt_probe_random_rmw)
   update_allreduce_ms    (n_gpus > 1) the flat-gradient all-reduce alone
+  ppo_update_ms_collective_path
+                         the data-parallel update path (rt_ppo_update_dp:
+                         grad, RCCL all-reduce, clip + Adam per minibatch in
+                         one library call); at n_gpus 1 over a world-1 RCCL
+                         group
   cpu_baseline           op-for-op NumPy port of the reference step on one
                          pinned host core, BASELINE.md §3 config C1 (reference
                          grid and tumours, seed 1, default_rng(0) actions;
@@ -63,7 +68,9 @@ Also reported:
                          events on the kernels' stream)
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N > 1 under torch.distributed.run, one rank per GPU)
+      (N > 1: one rank per GPU under torch.distributed.run -- started by the
+      caller, or by bench.py itself when it runs outside one; add
+      --rehearse-same-device to run the N ranks on cuda:0 over gloo)
 """
 from __future__ import annotations
 
@@ -650,14 +657,78 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
             "timing": "HIP events on the kernels' stream, mean of 5 back-to-back launches"}
 
 
+def needs_spawn(gpus: int, environ) -> bool:
+    """--gpus N > 1 outside a torch.distributed.run rank (no WORLD_SIZE)."""
+    return gpus > 1 and "WORLD_SIZE" not in environ
+
+
+def launcher_cmd(gpus: int, port: int, argv) -> list:
+    """The single-node launcher of the driver's own N-GPU command line."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(REPO, "bench.py"), *argv]
+
+
+def spawn_ranks(gpus: int, argv) -> int:
+    """Run `gpus` ranks of this same command under torch.distributed.run as a
+    child process (one rank per GPU; with --rehearse-same-device all on cuda:0
+    over gloo) and return its exit status.  Rank 0 prints the JSON line.  No
+    exec: the child is a new process, this one has not initialised the GPU."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.call(launcher_cmd(gpus, port, argv), env=env)
+
+
+def collective_update_ms(tr, dist, dev) -> float:
+    """ms per minibatch of the trainer's data-parallel update path over a
+    world-1 RCCL group (the update the 8-GPU run makes, minus the xGMI
+    traffic): rt_ppo_update_dp with the library's own communicator."""
+    import socket
+
+    import torch
+
+    own = not dist.is_initialized()
+    if own:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    keep = tr.collective
+    tr.collective = True
+    try:
+        tr.update()  # warm: the communicator, RCCL's first launch
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = tr.update()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert tr._dp_comm, "the update did not take the library's RCCL path"
+    finally:
+        tr.collective = keep
+        if own:
+            dist.destroy_process_group()
+    return 1000 * dt / n
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world == 1 and a.gpus > 1:
-        print(f"bench.py: --gpus {a.gpus} must be launched with torch.distributed.run "
-              f"--nproc-per-node {a.gpus}", file=sys.stderr)
+    if needs_spawn(a.gpus, os.environ):
+        # started directly with --gpus N > 1: the N ranks run as children of a
+        # torch.distributed.run started HERE, before this process touches the GPU
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
+    if a.gpus != world:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
         sys.exit(2)
 
     import torch
@@ -849,6 +920,16 @@ def main():
             d2 = max_over_ranks(time.perf_counter() - t0)
             tr._update_prec = keep
             upd[f"ppo_update_ms_{other}"] = 1000 * d2 / n2
+            # the data-parallel update path (rt_ppo_update_dp: grad, RCCL all-reduce
+            # of the flat gradient, clip + Adam per minibatch, one library call):
+            # at world > 1 that is what ppo_update_ms timed; at world 1 it runs
+            # through a world-1 RCCL group (the all-reduce an identity)
+            if world > 1:
+                upd["ppo_update_ms_collective_path"] = upd["ppo_update_ms"]
+            elif not a.rehearse_same_device:
+                upd["ppo_update_ms_collective_path"] = collective_update_ms(tr, dist, dev)
+            if "ppo_update_ms_collective_path" in upd:
+                upd["collective_path_vs_fused"] = upd["ppo_update_ms_collective_path"] / upd["ppo_update_ms"]
 
     # ---------------- roofline of the dominant kernel, k_dense
     V = int(np.prod(grid))

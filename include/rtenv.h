@@ -46,7 +46,8 @@ extern "C" {
                                 (rt_ppo_hparams.precision, rt_conv_layer.precision) instead of the
                                 process-wide rt_ppo_/rt_conv_set_precision; 5: RT_ROLLOUT_FLOW and
                                 the dense persistent rollout (groups 0 on dense handles) removed,
-                                rt_ppo_status and rt_host_lung_sum added, dense-mode
+                                rt_ppo_status, rt_host_lung_sum and the RCCL
+                                data-parallel update (rt_dp_*, rt_ppo_update_dp) added, dense-mode
                                 doses.lung in numpy's exact order */
 
 enum {
@@ -393,6 +394,35 @@ int rt_ppo_update(const float* const* params_d, float* const* grads_d, const rt_
                   const rt_ppo_hparams* hp, float* flat_param_d, float* flat_grad_d, float* exp_avg_d,
                   float* exp_avg_sq_d, int64_t n_flat, int64_t step0, double lr, float* workspace_d,
                   int64_t workspace_floats, float* stats_d, float* stats_accum_d, void* stream);
+
+/* ---- data-parallel update (train.py:183-248 at world > 1) -----
+ * One process per GPU.  The library holds its own RCCL communicator: rank 0
+ * draws an id (rt_dp_unique_id), the caller broadcasts the RT_DP_ID_BYTES
+ * bytes (e.g. torch.distributed), every rank calls rt_dp_comm_create with
+ * them (a collective: all ranks at once).  RCCL is loaded on the first call
+ * (the copy already mapped in the process, e.g. torch's, else ROCm's). */
+typedef struct rt_dp_comm rt_dp_comm; /* opaque */
+#define RT_DP_ID_BYTES 128
+#define RT_DP_F32 0
+#define RT_DP_F64 1
+int rt_dp_unique_id(uint8_t* id_h /* [RT_DP_ID_BYTES] */);
+int rt_dp_comm_create(const uint8_t* id_h, int32_t nranks, int32_t rank, int device, rt_dp_comm** out);
+void rt_dp_comm_destroy(rt_dp_comm* comm);
+/* In-place SUM all-reduce of count elements (RT_DP_F32 / RT_DP_F64) on `stream`. */
+int rt_dp_allreduce(rt_dp_comm* comm, void* buf_d, int64_t count, int32_t dtype, void* stream);
+/* rt_ppo_update across the ranks of `comm`: per minibatch rt_ppo_grad, the SUM
+ * all-reduce of flat_grad_d over RCCL, then rt_adam_step with grad_div =
+ * nranks (clip on the global gradient, every replica the same step) -- the
+ * whole update in one call, enqueued on `stream`.  adv_stats_d: the global
+ * per-minibatch statistics (rt_ppo_adv_sums -> all-reduce ->
+ * rt_ppo_adv_finalize).  At nranks 1 the all-reduce is an identity and the
+ * result equals rt_ppo_grad + rt_adam_step. */
+int rt_ppo_update_dp(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
+                     const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches, const float* adv_stats_d,
+                     const rt_ppo_hparams* hp, float* flat_param_d, float* flat_grad_d, float* exp_avg_d,
+                     float* exp_avg_sq_d, int64_t n_flat, int64_t step0, double lr, float* workspace_d,
+                     int64_t workspace_floats, float* stats_d, float* stats_accum_d, rt_dp_comm* comm,
+                     void* stream);
 
 /* RT_OK, or RT_EDEVICE when an rt_ppo_update on the current device lost the
  * grid arrival of its fused reduce + Adam launch (the grid was not

@@ -23,6 +23,7 @@ INFO_NAMES = {
 }
 INFO_W = 20
 STEP_DENSE, STEP_INCREMENTAL = 0, 1
+DP_ID_BYTES, DP_F32, DP_F64 = 128, 0, 1  # RT_DP_ID_BYTES, RT_DP_F32, RT_DP_F64
 PPO_PREC = {"f32": 0, "bf16x3": 1}  # RT_PPO_PREC_* (rt_ppo_hparams.precision)
 CONV_PREC = {"f32": 0, "bf16x3": 1}  # RT_CONV_PREC_* (rt_conv_layer.precision)
 
@@ -38,6 +39,7 @@ EXPORTS = [
     "rt_debug_beam", "rt_debug_pose", "rt_env_beam_list", "rt_probe_random_rmw", "rt_probe_stream", "rt_host_sincos", "rt_host_tumour_sum", "rt_host_lung_sum", "rt_policy_sample", "rt_gae",
     "rt_env_step_policy", "rt_env_rollout_policy", "rt_env_set_rollout_groups",
     "rt_ppo_workspace_floats", "rt_ppo_num_params", "rt_ppo_grad", "rt_adam_step", "rt_ppo_update", "rt_ppo_status",
+    "rt_dp_unique_id", "rt_dp_comm_create", "rt_dp_comm_destroy", "rt_dp_allreduce", "rt_ppo_update_dp",
     "rt_ppo_shuffle", "rt_ppo_shuffle_epochs", "rt_ppo_shuffle_adv", "rt_ppo_adv_stats", "rt_ppo_adv_sums", "rt_ppo_adv_finalize",
     "rt_conv_out_dims", "rt_conv_relu_pool_fwd", "rt_conv_wgrad_workspace_floats", "rt_conv_relu_pool_wgrad", "rt_conv_mfma_count",
     "rt_conv_relu_pool_dgrad",
@@ -184,6 +186,13 @@ def load(build_if_missing: bool = True):
                            ctypes.POINTER(RtPpoHparams), vp, vp, vp, vp, i64, i64, f64, vp, i64, vp, vp, vp],
                           ctypes.c_int),
         "rt_ppo_status": ([], ctypes.c_int),
+        "rt_dp_unique_id": ([vp], ctypes.c_int),
+        "rt_dp_comm_create": ([vp, i32, i32, ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
+        "rt_dp_comm_destroy": ([vp], None),
+        "rt_dp_allreduce": ([vp, vp, i64, i32, vp], ctypes.c_int),
+        "rt_ppo_update_dp": ([ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(RtPpoBatch), vp, i32, i32, vp,
+                              ctypes.POINTER(RtPpoHparams), vp, vp, vp, vp, i64, i64, f64, vp, i64, vp, vp, vp, vp],
+                             ctypes.c_int),
         "rt_ppo_shuffle": ([i64, ctypes.c_uint64, vp, vp], ctypes.c_int),
         "rt_ppo_shuffle_epochs": ([i64, i32, vp, vp, vp], ctypes.c_int),
         "rt_ppo_shuffle_adv": ([i64, i32, vp, vp, vp, i32, vp, vp, vp, i64, vp], ctypes.c_int),

@@ -33,6 +33,9 @@
 
 #include "rtenv.h"
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 extern "C" int rt_internal_fail(int code, const char* msg);
 
 namespace {
@@ -1069,7 +1072,8 @@ struct ReduceAdamParams {
     int32_t flat_off[13];  // flat index of each tensor's first element (params_d[t] - flat_param_d)
     unsigned* counter;
     unsigned target;
-    int* fault;  // host-mapped sticky flag (reduce_adam_fault)
+    int* fault;      // host-mapped sticky flag (reduce_adam_fault)
+    int* dev_fault;  // the same event within this rt_ppo_update call, in device memory
 };
 
 __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
@@ -1144,6 +1148,8 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
     // the partial loads below stay behind the poll (sc1 loads of sc1-stored
     // bytes behind a matched poll: MI355X_MICROARCH.md hand-off table, row 1)
     asm volatile("" ::: "memory");
+    // the call's device fault word, loaded beside the partials (no extra round trip)
+    const int faulted = __hip_atomic_load(Q.dev_fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     float tn = 0.0f;
     if (A.max_norm > 0.0f) {
         // all of a lane's partials in flight at once, summed in k_adam's order
@@ -1163,19 +1169,22 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
     const float coef = A.max_norm > 0.0f ? fminf(A.max_norm / (sqrtf(tn) + 1e-6f), 1.0f) : 1.0f;
     if (!arrived) {
         // a lost arrival (the grid was not co-resident): no parameter, moment or
-        // gradient is written, and the host sees RT_EDEVICE on its next call
-        if (lane == 0) __hip_atomic_store(Q.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // gradient is written; the call's device word stops every block that
+        // arrives later, and the host sees RT_EDEVICE (rt_ppo_status, next call)
+        if (lane == 0) {
+            __hip_atomic_store(Q.dev_fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(Q.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         return;
     }
-    // A block of this launch or of an earlier one that gave up raised the
-    // flag before it left: every block that arrives after it -- late in this
-    // launch, or in the update's later launches, which start after it ended --
-    // reads it here and writes nothing either, so a lost arrival leaves the
-    // whole update's state as the last complete minibatch left it (never a
-    // partly updated parameter set); rt_ppo_status reports it after the sync.
-    int faulted = 0;
-    if (lane == 0) faulted = __hip_atomic_load(Q.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (__shfl(faulted, 0, 64)) return;
+    // A block of this launch or of an earlier one of the call that gave up set
+    // the device word before it left: every block that arrives after it -- late
+    // in this launch, or in the call's later launches, which start after it
+    // ended -- reads it (above, with its partials) and writes nothing either,
+    // so a lost arrival leaves the state as the last complete minibatch left
+    // it (never a partly updated parameter set).  (Round 6: the host-mapped
+    // flag itself read here cost ~26 us per minibatch -- 158 PCIe reads.)
+    if (faulted) return;
     if (!upd) return;
     const float g = a * coef;
     A.grad[i] = g;
@@ -1606,9 +1615,12 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
         }
         return RT_OK;
     }
-    // the arrival counter of k_ppo_reduce_adam: the last norm slot (unused by the partials)
+    // the arrival counter of k_ppo_reduce_adam and the call's device fault word:
+    // the last two norm slots (unused by the partials)
+    static_assert(kReduceBlocks <= kNormSlots - 2, "norm partials vs counter / fault word");
+    int* dev_fault = reinterpret_cast<int*>(norm_part + (kNormSlots - 2));
     unsigned* counter = reinterpret_cast<unsigned*>(norm_part + (kNormSlots - 1));
-    if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess)
+    if (hipMemsetAsync(dev_fault, 0, 2 * sizeof(unsigned), st) != hipSuccess)
         return rt_internal_fail(RT_EDEVICE, "rt_ppo_update: hipMemsetAsync failed");
     ReduceAdamParams Q{};
     for (int t = 0; t < 13; ++t) {
@@ -1620,6 +1632,7 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
     }
     Q.counter = counter;
     Q.fault = fault_d;
+    Q.dev_fault = dev_fault;
     for (int i = 0; i < n_minibatches; ++i) {
         int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
                                  adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,
@@ -1752,3 +1765,146 @@ extern "C" int rt_ppo_adv_finalize(const double* sums_d, int64_t count, int32_t 
 }
 
 RT_TRACE_READ_FN(rt_trace_read_update)
+
+// ---------------------------------------------------------------------------
+// Data-parallel update over RCCL (train.py:183-248 at world > 1).
+// One process per GPU; the library keeps its own RCCL communicator, so the
+// per-minibatch sequence -- k_ppo_grad_mfma + k_ppo_reduce, the SUM
+// all-reduce of the flat gradient (40 KB for the MLP, in place), k_gnorm +
+// k_adam with grad_div = world -- is issued by ONE C call for the whole
+// update, with no Python, ctypes or torch.distributed call per minibatch.
+// RCCL is loaded at the first communicator (dlopen): the copy torch already
+// mapped when there is one (same SONAME), otherwise ROCm's; hosts that never
+// build a communicator never load it.
+// ---------------------------------------------------------------------------
+struct rt_dp_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0, device = 0;
+};
+
+namespace {
+
+struct RcclApi {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string error;
+};
+
+const RcclApi& rccl() {
+    static RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // torch's copy, when mapped
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            a.error = std::string("librccl.so.1: ") + dlerror();
+            return a;
+        }
+        a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        a.comm_init_rank = reinterpret_cast<decltype(a.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        a.all_reduce = reinterpret_cast<decltype(a.all_reduce)>(dlsym(h, "ncclAllReduce"));
+        a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
+        if (!a.get_unique_id || !a.comm_init_rank || !a.all_reduce || !a.comm_destroy || !a.error_string)
+            a.error = "librccl.so.1: missing symbols";
+        return a;
+    }();
+    return api;
+}
+
+int rccl_fail(const char* what, ncclResult_t r) {
+    const RcclApi& A = rccl();
+    return rt_internal_fail(RT_EDEVICE, (std::string(what) + ": " + (A.error_string ? A.error_string(r) : "RCCL error")).c_str());
+}
+
+}  // namespace
+
+extern "C" int rt_dp_unique_id(uint8_t* id_h) {
+    if (!id_h) return rt_internal_fail(RT_EINVAL, "rt_dp_unique_id: NULL argument");
+    static_assert(sizeof(ncclUniqueId) == RT_DP_ID_BYTES, "RT_DP_ID_BYTES");
+    const RcclApi& A = rccl();
+    if (!A.error.empty()) return rt_internal_fail(RT_EDEVICE, A.error.c_str());
+    ncclUniqueId id;
+    const ncclResult_t r = A.get_unique_id(&id);
+    if (r != ncclSuccess) return rccl_fail("ncclGetUniqueId", r);
+    std::memcpy(id_h, &id, sizeof(id));
+    return RT_OK;
+}
+
+extern "C" int rt_dp_comm_create(const uint8_t* id_h, int32_t nranks, int32_t rank, int device, rt_dp_comm** out) {
+    if (!id_h || !out || nranks < 1 || rank < 0 || rank >= nranks)
+        return rt_internal_fail(RT_EINVAL, "rt_dp_comm_create: bad argument");
+    *out = nullptr;
+    const RcclApi& A = rccl();
+    if (!A.error.empty()) return rt_internal_fail(RT_EDEVICE, A.error.c_str());
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (hipSetDevice(device) != hipSuccess) return rt_internal_fail(RT_EDEVICE, "rt_dp_comm_create: bad device");
+    ncclUniqueId id;
+    std::memcpy(&id, id_h, sizeof(id));
+    rt_dp_comm* c = new rt_dp_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    const ncclResult_t r = A.comm_init_rank(&c->comm, nranks, id, rank);
+    (void)hipSetDevice(cur);
+    if (r != ncclSuccess) {
+        delete c;
+        return rccl_fail("ncclCommInitRank", r);
+    }
+    *out = c;
+    return RT_OK;
+}
+
+extern "C" void rt_dp_comm_destroy(rt_dp_comm* comm) {
+    if (!comm) return;
+    if (comm->comm && rccl().comm_destroy) (void)rccl().comm_destroy(comm->comm);
+    delete comm;
+}
+
+extern "C" int rt_dp_allreduce(rt_dp_comm* comm, void* buf_d, int64_t count, int32_t dtype, void* stream) {
+    if (!comm || !buf_d || count < 0 || (dtype != RT_DP_F32 && dtype != RT_DP_F64))
+        return rt_internal_fail(RT_EINVAL, "rt_dp_allreduce: bad argument");
+    const ncclResult_t r = rccl().all_reduce(buf_d, buf_d, (size_t)count, dtype == RT_DP_F32 ? ncclFloat32 : ncclFloat64,
+                                             ncclSum, comm->comm, reinterpret_cast<hipStream_t>(stream));
+    return r == ncclSuccess ? RT_OK : rccl_fail("ncclAllReduce", r);
+}
+
+extern "C" int rt_ppo_update_dp(const float* const* params_d, float* const* grads_d, const rt_ppo_batch* batch,
+                                const int64_t* perm_d, int32_t mb_size, int32_t n_minibatches,
+                                const float* adv_stats_d, const rt_ppo_hparams* hp, float* flat_param_d,
+                                float* flat_grad_d, float* exp_avg_d, float* exp_avg_sq_d, int64_t n_flat,
+                                int64_t step0, double lr, float* workspace_d, int64_t workspace_floats,
+                                float* stats_d, float* stats_accum_d, rt_dp_comm* comm, void* stream) {
+    if (bad13(reinterpret_cast<const void* const*>(params_d)) || bad13(reinterpret_cast<const void* const*>(grads_d)) ||
+        bad_batch(batch) || !perm_d || mb_size < 1 || n_minibatches < 1 || !hp || !flat_param_d || !flat_grad_d ||
+        !exp_avg_d || !exp_avg_sq_d || n_flat != NP || step0 < 1 || !workspace_d || !stats_d || !comm ||
+        (hp->norm_adv && !adv_stats_d) || mb_size > batch->batch_size || bad_prec(hp))
+        return rt_internal_fail(RT_EINVAL, "rt_ppo_update_dp: bad argument");
+    if (reduce_adam_faulted())
+        return rt_internal_fail(RT_EDEVICE, "rt_ppo_update_dp: an earlier rt_ppo_update lost its grid arrival");
+    for (int t = 0; t < 13; ++t)
+        if (grads_d[t] - flat_grad_d != params_d[t] - flat_param_d || params_d[t] < flat_param_d ||
+            params_d[t] - flat_param_d + (kTensorOff[t + 1] - kTensorOff[t]) > n_flat)
+            return rt_internal_fail(RT_EINVAL, "rt_ppo_update_dp: params_d / grads_d must be views of the flat buffers");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    float* norm_part = workspace_d + (workspace_floats - kNormSlots);
+    const RcclApi& A = rccl();
+    for (int i = 0; i < n_minibatches; ++i) {
+        int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
+                                 adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,
+                                 stats_d, stats_accum_d, st, true);
+        if (rc) return rc;
+        // SUM over the ranks, in place; the Adam step divides by the world size
+        const ncclResult_t r = A.all_reduce(flat_grad_d, flat_grad_d, (size_t)n_flat, ncclFloat32, ncclSum,
+                                            comm->comm, st);
+        if (r != ncclSuccess) return rccl_fail("ncclAllReduce", r);
+        rc = adam_launch(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part,
+                         false, (float)comm->nranks, st);
+        if (rc) return rc;
+    }
+    return RT_OK;
+}

@@ -733,9 +733,8 @@ struct LChunk {          // one numpy buffer holding lung voxels
     int32_t gen;         // -1: a whole 8192-element buffer (butterfly); else its LGeneric record
 };
 struct LGroup {          // 64 chains (lane l = chain l), sorted by length
-    int32_t seg_off;     // first element, relative to the chunk's seg_base
-    int32_t rows;        // length of its longest chain (lane 0)
-    uint8_t nk[16];      // lanes active in row k (non-increasing; 0 past `rows`)
+    uint32_t row[16];    // row k: its first element relative to the chunk's seg_base | lanes
+                         // active in it (non-increasing in k; 0 past the longest chain) << 16
 };
 struct LGeneric {        // a partial buffer's leaf tree
     int32_t n_leaf, op_base, lvl_base, nlev, result, tail_base;
@@ -795,29 +794,52 @@ __device__ __forceinline__ float lung_load(const DenseParams& P, const float* ro
 
 // One chain group: element k of lane l's chain (k < rows, l < nk[k]) -> x[k];
 // 0 elsewhere (an exact no-op for the chain sum and the count).
+// The plan is read-only while k_dense runs: read through the constant address
+// space so the compiler issues scalar loads (one s_load_dwordx16 per group)
+// instead of per-lane byte loads whose results gate the row addresses.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* cst(const T* p) {
+    return (const __attribute__((address_space(4))) T*)p;
+}
+#else  // the host pass of the device functions (never executed)
+template <typename T>
+__device__ __forceinline__ const T* cst(const T* p) {
+    return p;
+}
+#endif
+
 template <bool GATHER>
 __device__ __forceinline__ void lung_fetch(const DenseParams& P, const float* row, int seg_base, int g, int lane,
                                            float (&x)[16], int& slot) {
-    const LGroup& G = P.L.grp[g];
-    int pos = seg_base + G.seg_off;
-    const int rows = G.rows;
+    const auto G = cst(P.L.grp) + g;
+    uint32_t ri[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ri[k] = G->row[k];  // one s_load_dwordx16, one wait
+    slot = P.L.slot[(size_t)g * 64 + lane];
+    // All 16 loads are issued, unconditionally: lanes past nk load the row's last
+    // element and rows past the group's longest chain its first element (lines
+    // the group fetches anyway) and drop the value.  A fixed load count lets the
+    // compiler wait for THIS group's loads only (vmcnt(16)) while the next
+    // group's are in flight; data-dependent branches made it wait for all.
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const int nk = k < rows ? (int)G.nk[k] : 0;
-        x[k] = lane < nk ? lung_load<GATHER>(P, row, pos + lane) : 0.0f;
-        pos += nk;
+        const int nk = (int)(ri[k] >> 16);
+        const int off = nk > 0 ? (int)(ri[k] & 0xffffu) + min(lane, nk - 1) : (int)(ri[0] & 0xffffu);
+        const float v = lung_load<GATHER>(P, row, seg_base + off);
+        x[k] = lane < nk ? v : 0.0f;
     }
-    slot = P.L.slot[(size_t)g * 64 + lane];
 }
 
 // the lane's chain in order (numpy's r[j] += a[i] sequence), its over-threshold
 // count, and the chain sum into its LDS slot
-__device__ __forceinline__ void lung_consume(const float (&x)[16], int rows, int slot, float thr, int& cnt,
-                                             float* slots) {
+__device__ __forceinline__ void lung_consume(const DenseParams& P, int g, const float (&x)[16], int slot, float thr,
+                                             int& cnt, float* slots) {
+    const auto G = cst(P.L.grp) + g;
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        if (k < rows) {  // wave-uniform
+        if (G->row[k] >> 16) {  // wave-uniform: a row of this group
             acc = acc + x[k];
             cnt += x[k] > thr ? 1 : 0;
         }
@@ -831,7 +853,7 @@ __device__ __forceinline__ void lung_consume(const float (&x)[16], int rows, int
 // current one is summed.
 template <bool GATHER>
 __device__ void lung_item(const DenseParams& P, int e, int j, int lane, float* wl) {
-    const LChunk c = P.L.chunk[j];
+    const LChunk c = cst(P.L.chunk)[j];
     const float* row = P.st.dose + (size_t)e * P.G.Vpad;
     float* slots = wl;
     // a partial buffer's leaf values and plan slots overwrite the class slots:
@@ -850,9 +872,9 @@ __device__ void lung_item(const DenseParams& P, int e, int j, int lane, float* w
     lung_fetch<GATHER>(P, row, c.seg_base, g0, lane, xa, sa);
     for (int g = g0; g < g1; g += 2) {
         if (g + 1 < g1) lung_fetch<GATHER>(P, row, c.seg_base, g + 1, lane, xb, sb);
-        lung_consume(xa, P.L.grp[g].rows, sa, thr, cnt, slots);
+        lung_consume(P, g, xa, sa, thr, cnt, slots);
         if (g + 2 < g1) lung_fetch<GATHER>(P, row, c.seg_base, g + 2, lane, xa, sa);
-        if (g + 1 < g1) lung_consume(xb, P.L.grp[g + 1].rows, sb, thr, cnt, slots);
+        if (g + 1 < g1) lung_consume(P, g + 1, xb, sb, thr, cnt, slots);
     }
     lds_wave_sync();
     float v;
@@ -865,7 +887,7 @@ __device__ void lung_item(const DenseParams& P, int e, int j, int lane, float* w
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
     } else {
-        const LGeneric q = P.L.gen[c.gen];
+        const LGeneric q = cst(P.L.gen)[c.gen];
         for (int L = lane; L < q.n_leaf; L += 64) {
             const nf4 a = reinterpret_cast<const nf4*>(slots)[2 * L];
             const nf4 b = reinterpret_cast<const nf4*>(slots)[2 * L + 1];
@@ -963,11 +985,13 @@ __global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env, int zer
         return;
     }
     __shared__ __attribute__((aligned(16))) float dsm[4 * kLungWaveFloats];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // wave-uniform (readfirstlane): the item, its chunk and group records then
+    // live in SGPRs and the plan is read by scalar loads
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int it = (int)(((blockIdx.y - (GATHER ? 0 : zero_rows)) * gridDim.x + blockIdx.x) * 4 + w);
     if (it >= n_env * P.L.n_chunk) return;  // wave-uniform
-    const int e = P.e_begin + it % n_env, j = P.L.order[it / n_env];
-    if (P.st.setup[e].mode != MODE_STEP) return;
+    const int e = P.e_begin + it % n_env, j = cst(P.L.order)[it / n_env];
+    if (cst(P.st.mode_b)[e] != MODE_STEP) return;
     lung_item<GATHER>(P, e, j, lane, dsm + w * kLungWaveFloats);
 }
 
@@ -980,11 +1004,13 @@ __global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env, int zer
 // each wave one fixed chunk index: a 250x spread of bytes per wave).
 __global__ __launch_bounds__(256) void k_dense_persist(DenseParams P, int n_env) {
     __shared__ __attribute__((aligned(16))) float dsm[4 * kLungWaveFloats];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // wave-uniform (readfirstlane): the item, its chunk and group records then
+    // live in SGPRs and the plan is read by scalar loads
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int n_items = n_env * P.L.n_chunk;
     for (int it = blockIdx.x * 4 + w; it < n_items; it += gridDim.x * 4) {
-        const int e = P.e_begin + it % n_env, j = P.L.order[it / n_env];
-        if (P.st.setup[e].mode != MODE_STEP) continue;  // wave-uniform
+        const int e = P.e_begin + it % n_env, j = cst(P.L.order)[it / n_env];
+        if (cst(P.st.mode_b)[e] != MODE_STEP) continue;  // wave-uniform
         lung_item<false>(P, e, j, lane, dsm + w * kLungWaveFloats);
     }
     zero_reset_share(P, P.e_begin, n_env, blockIdx.x, gridDim.x);
@@ -1978,13 +2004,12 @@ int build_lung_plan(const uint8_t* lungs, int64_t V, LungPlanHost& P) {
         for (size_t g0 = 0; g0 < chains.size(); g0 += 64) {
             const size_t g1 = std::min(chains.size(), g0 + 64);
             LGroup G{};
-            G.seg_off = seg - ch.seg_base;
-            G.rows = (int32_t)chains[g0].vox.size();
-            if (G.rows > 16) return fail(RT_ELIMIT, "lung sum plan: chain longer than 16");
-            for (int k = 0; k < G.rows; ++k) {
+            const int rows = (int)chains[g0].vox.size();
+            if (rows > 16) return fail(RT_ELIMIT, "lung sum plan: chain longer than 16");
+            for (int k = 0; k < rows; ++k) {
                 int nk = 0;
                 for (size_t l = g0; l < g1; ++l) nk += (int)chains[l].vox.size() > k ? 1 : 0;
-                G.nk[k] = (uint8_t)nk;
+                G.row[k] = (uint32_t)(seg - ch.seg_base) | (uint32_t)nk << 16;
                 for (int l = 0; l < nk; ++l) {
                     const int32_t v = chains[g0 + l].vox[k];
                     P.pos_of[v] = seg + l;
@@ -2052,10 +2077,9 @@ float eval_lung_plan(const LungPlanHost& P, const float* dose) {
         for (int g = c.grp_base; g < c.grp_base + c.n_grp; ++g) {
             const LGroup& G = P.grp[g];
             float chain[64] = {};
-            int pos = c.seg_base + G.seg_off;
-            for (int k = 0; k < G.rows; ++k) {
-                for (int l = 0; l < G.nk[k]; ++l) chain[l] = chain[l] + dose[P.lpos[pos + l]];
-                pos += G.nk[k];
+            for (int k = 0; k < 16; ++k) {
+                const int pos = c.seg_base + (int)(G.row[k] & 0xffffu), nk = (int)(G.row[k] >> 16);
+                for (int l = 0; l < nk; ++l) chain[l] = chain[l] + dose[P.lpos[pos + l]];
             }
             for (int l = 0; l < 64; ++l)
                 if (P.slot[(size_t)g * 64 + l] != kNoSlot) slots[P.slot[(size_t)g * 64 + l]] = chain[l];

@@ -154,6 +154,7 @@ class PPOTrainer:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
             off += p.numel()
         self._last_stats = None
+        self._dp_comm = None  # the library's RCCL communicator (_native_dp), built on first use
         self.optimizer = torch.optim.Adam(self.params, lr=float(cfg.learning_rate), eps=1e-5,
                                           foreach=self.device.type == "cuda")
         self.max_minibatches = 0  # >0: stop the update after this many minibatch steps (benchmarks)
@@ -547,12 +548,37 @@ class PPOTrainer:
             self.record_perms.extend(p.clone() for p in perm)
         return perm, stats
 
+    def _native_dp(self):
+        """The library's own RCCL communicator for the data-parallel fused
+        update (rt_ppo_update_dp), built once over the torch.distributed group:
+        rank 0 draws the id, a broadcast hands it to every rank.  None -- the
+        per-minibatch loop of rt_ppo_grad / torch.distributed.all_reduce /
+        rt_adam_step -- on gloo groups (the CPU and same-device rehearsals) or
+        with cfg.native_dp = False."""
+        if self._dp_comm is None:
+            self._dp_comm = False
+            if (bool(getattr(self.cfg, "native_dp", True)) and self.device.type == "cuda" and dist.is_available()
+                    and dist.is_initialized() and dist.get_backend() == "nccl"):
+                L = _lib.load()
+                ident = (ctypes.c_uint8 * _lib.DP_ID_BYTES)()
+                if dist.get_rank() == 0:
+                    _lib.check(L.rt_dp_unique_id(ident), "rt_dp_unique_id")
+                t = torch.tensor(list(bytes(ident)), dtype=torch.uint8, device=self.device)
+                dist.broadcast(t, 0)
+                ident = (ctypes.c_uint8 * _lib.DP_ID_BYTES)(*t.cpu().tolist())
+                h = ctypes.c_void_p()
+                _lib.check(L.rt_dp_comm_create(ident, dist.get_world_size(), dist.get_rank(),
+                                               self.device.index or 0, ctypes.byref(h)), "rt_dp_comm_create")
+                self._dp_comm = h
+        return self._dp_comm or None
+
     def _update_fused(self):
         """train.py:183-248 through the fused kernels: every epoch's shuffle and
         (all-reduced) minibatch advantage statistics up front, then per
         minibatch rt_ppo_grad + the clip/Adam step (world 1: all of it is ONE
-        rt_ppo_update call; world > 1: RCCL all-reduce of the flat gradient
-        bucket between rt_ppo_grad and rt_adam_step)."""
+        rt_ppo_update call; world > 1 over RCCL: ONE rt_ppo_update_dp call, the
+        library all-reducing the flat gradient bucket between the grad and Adam
+        kernels; over gloo: a Python loop around torch.distributed.all_reduce)."""
         self._bind_batch()
         L = _lib.load()
         self._hp.precision = self._update_prec  # per call (rt_ppo_hparams.precision)
@@ -578,6 +604,16 @@ class PPOTrainer:
                                        self._exp_avg_sq.data_ptr(), n, self._adam_step + 1, lr,
                                        self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
                                        self._ppo_accum.data_ptr(), stream), "rt_ppo_update")
+            self._adam_step += total
+        elif self._native_dp() is not None:
+            # the whole data-parallel update in one call: grad, RCCL SUM all-reduce
+            # of the flat gradient, clip + Adam (grad_div = world) per minibatch
+            _lib.check(L.rt_ppo_update_dp(self._policy_ptrs, self._grad_ptrs, ctypes.byref(batch), perm.data_ptr(),
+                                          mbs, total, _lib.ptr(adv), hp, self.flat_param.data_ptr(),
+                                          self.flat_grad.data_ptr(), self._exp_avg.data_ptr(),
+                                          self._exp_avg_sq.data_ptr(), n, self._adam_step + 1, lr,
+                                          self._ws.data_ptr(), self._ws.numel(), self._ppo_stats.data_ptr(),
+                                          self._ppo_accum.data_ptr(), self._dp_comm, stream), "rt_ppo_update_dp")
             self._adam_step += total
         else:
             for i in range(total):

@@ -13,7 +13,8 @@ autoreset + RecordEpisodeStatistics) on the actions the kernel sampled:
 
 * observations bit-exact (f32), rewards and reward components within 1e-5,
   doses.tumour bit-exact, doses.lung bit-exact in dense mode (numpy's f32
-  order) and within 4 ulp in incremental mode (tests/dose_checks.py);
+  order) and within the f32 summation bound in incremental mode
+  (tests/dose_checks.py);
 * terminated / autoreset / episode r and l identical;
 * the tumour of every autoreset = the restated Philox draw (tests/rt_rng.py);
 * the final dose volumes bit-exact.

@@ -5,8 +5,10 @@ RCCL does not run two ranks on one device, so this is a world-1 process
 group: the all-reduces are identities, but every call the 8-GPU run makes
 goes through RCCL here with the trainer's own buffers and dtypes — the f64
 advantage-sum all-reduce (rt_ppo_adv_sums -> all-reduce ->
-rt_ppo_adv_finalize), the f32 flat-gradient all-reduce between rt_ppo_grad and
-rt_adam_step per minibatch (ppo.py `_update_fused`, collective branch), the
+rt_ppo_adv_finalize), the f32 flat-gradient all-reduce between the grad and
+Adam kernels per minibatch, both as the library's own RCCL communicator
+(rt_ppo_update_dp, the whole update in one call) and as the Python loop
+around torch.distributed.all_reduce (bitwise the same), the
 bench's MAX all-reduce of an f64 scalar and a barrier.  The collective update
 must agree with the single-call rt_ppo_update from the same state (same
 generator draws, same batch): train.py:183-248 either way, the only
@@ -68,13 +70,25 @@ def _worker(port, q):
         tr.compute_gae()
         start = copy.deepcopy(tr.state_dict())
         out = {}
-        for mode in (True, False):  # collective (RCCL) path, then the single-call update
+        # collective paths: the library's own RCCL communicator (rt_ppo_update_dp,
+        # one call per update), the per-minibatch Python loop around
+        # torch.distributed.all_reduce (cfg.native_dp = False); then the single
+        # call rt_ppo_update
+        for mode in ("native", "loop", "single"):
             tr.load_state_dict(copy.deepcopy(start))
-            tr.collective = mode
+            tr.collective = mode != "single"
+            tr.cfg.native_dp = mode == "native"
+            tr._dp_comm = None if mode == "native" else False
             n = tr.update()
             torch.cuda.synchronize()
+            if mode == "native":
+                assert tr._dp_comm, "the native RCCL path did not run"
             out[mode] = (n, tr.flat_param.detach().cpu().numpy().copy(), tr._exp_avg.cpu().numpy().copy(),
                          tr._exp_avg_sq.cpu().numpy().copy(), int(tr._adam_step))
+        # the native update runs the loop's kernels around RCCL's all-reduce: bitwise
+        for a, b in zip(out["native"][1:4], out["loop"][1:4]):
+            assert np.array_equal(a, b)
+        out[True], out[False] = out["native"], out["single"]
         t = torch.tensor([1.5], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py max_over_ranks
         dist.barrier()
