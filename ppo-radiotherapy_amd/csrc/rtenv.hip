@@ -17,10 +17,12 @@
 // written out where OpenBLAS fuses.  See DESIGN.md "Numerics".
 //
 // Data layout in HBM (per handle = one GPU):
-//   dose      f32[N][Vpad]   Vpad = round_up(D*H*W, 1024): rows 4 KiB aligned;
-//                            dense visionless: lung-first rows (the lung voxels in
-//                            C order, then the rest), so k_dense streams only the
-//                            lung segment; otherwise C order
+//   dose      f32[N][Vpad]   rows 4 KiB aligned; dense visionless: lung-first rows
+//                            (the lung segment in the lung sum plan's chain order
+//                            with its zero pad slots, then the other voxels; Vpad =
+//                            round_up(its length, 1024)), so k_dense streams only
+//                            the lung segment; otherwise C order (Vpad =
+//                            round_up(D*H*W, 1024))
 //   pose      f64[N][6]      beam position + direction
 //   lung_bits u32[Vpad/32]   shared lung mask, 1 bit per voxel (L2-resident)
 //   tumour library: sorted C-order voxel lists + per-tumour sum plans
@@ -705,36 +707,40 @@ __device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const 
 //
 // Dense visionless handles keep each dose row lung-first; the host builder
 // (build_lung_plan) orders the lung segment by numpy buffer ("chunk") and, inside
-// a chunk, by chain: the chains sorted by length, in groups of 64 (one per
-// lane), group rows stored ragged -- row k of a group holds element k of its
-// first nk[k] chains, contiguously -- so a wave streams a chunk with
-// coalesced dword loads, each lane summing its own chain in order with no
-// padding bytes.  The chain sums go to LDS slots [leaf][class]; lane = leaf
-// then combines its 8 slots, and a whole 8192-element buffer (64 leaves of
-// 128, a perfect tree) finishes with a 6-step xor butterfly (IEEE addition
-// commutes, so both lanes of a pair form the same sum).  A partial buffer (the
-// last one of a volume whose size is not a multiple of 8192) has an irregular
-// tree: its leaves add their tail voxels and run a level plan (run_plan).  The
-// chunk sums go to part_sum[e][chunk]; k_finish adds them in chunk order from
-// 0.0f -- numpy's outer loop (chunks without lung voxels add +0).
+// a chunk, by chain: the chains sorted by length, 256 per group -- lane l of a
+// wave owns chains 4l..4l+3 -- group rows stored ragged: row k holds element k
+// of the group's first nk[k] chains, contiguously, padded with zero slots to a
+// multiple of 4 (~1.5 % of the segment at 64^3).  A wave streams a chunk with
+// coalesced 16-B loads (element k of its four chains per lane, 16 rows in
+// flight: 16 KiB per wave), each lane summing its chains in order.  The chain
+// sums go to LDS slots [leaf][class]; lane = leaf then combines its 8 slots,
+// and a whole 8192-element buffer (64 leaves of 128, a perfect tree) finishes
+// with a 6-step xor butterfly (IEEE addition commutes, so both lanes of a pair
+// form the same sum).  A partial buffer (the last one of a volume whose size
+// is not a multiple of 8192) has an irregular tree: its leaves add their tail
+// voxels and run a level plan (run_plan).  The chunk sums go to
+// part_sum[e][chunk]; k_finish adds them in chunk order from 0.0f -- numpy's
+// outer loop (chunks without lung voxels add +0).
 // Vision handles keep C-order rows: the same plan, each segment position
-// gathered through lpos (segment position -> voxel).
+// gathered through lpos (segment position -> voxel, -1 for a pad slot).
 // ---------------------------------------------------------------------------
 constexpr int kLungChunk = 8192;        // numpy's reduction buffer
 constexpr int kLungLeafMax = 65;        // leaves of a buffer of <= 8192 elements (65 at 8185..8191)
 constexpr int kLungSlotFloats = 528;    // [leaf][8 classes], 16-B padded
 constexpr int kLungWaveFloats = kLungSlotFloats;  // a partial buffer's plan slots (2 x leaves) alias the slots
+constexpr int kLungGroup = 256;         // chains per group (4 per lane)
 constexpr uint16_t kNoSlot = 0xFFFFu;
 
 struct LChunk {          // one numpy buffer holding lung voxels
-    int32_t seg_base;    // segment position of its first chain element
+    int32_t seg_base;    // segment position of its first chain element (a multiple of 4)
     int32_t grp_base;    // its first chain group
     int32_t n_grp;
     int32_t gen;         // -1: a whole 8192-element buffer (butterfly); else its LGeneric record
 };
-struct LGroup {          // 64 chains (lane l = chain l), sorted by length
-    uint32_t row[16];    // row k: its first element relative to the chunk's seg_base | lanes
-                         // active in it (non-increasing in k; 0 past the longest chain) << 16
+struct LGroup {          // 256 chains (lane l: chains 4l..4l+3), sorted by length
+    uint32_t row[16];    // row k: its first slot relative to the chunk's seg_base | the lanes
+                         // whose float4 holds one of its elements (ceil(nk / 4); non-increasing
+                         // in k; 0 past the longest chain) << 16
 };
 struct LGeneric {        // a partial buffer's leaf tree
     int32_t n_leaf, op_base, lvl_base, nlev, result, tail_base;
@@ -742,13 +748,14 @@ struct LGeneric {        // a partial buffer's leaf tree
 struct LungParams {
     const LChunk* chunk;
     const LGroup* grp;
-    const uint16_t* slot;     // [group][64] leaf * 8 + class, kNoSlot (tail voxel / no chain)
+    const uint64_t* slot;     // [group][64]: lane's 4 chains' slots (leaf * 8 + class; kNoSlot: tail
+                              // voxel / no chain), 16 bits each
     const LGeneric* gen;
     const uint32_t* ops;      // partial buffers' leaf trees: (a | b << 16), dst = n_leaf + op
     const int32_t* lvl_end;
     const int32_t* tail_off;  // per partial buffer: [n_leaf + 1] into tail_pos
     const int32_t* tail_pos;  // segment positions of each leaf's tail voxels, C order
-    const int32_t* lpos;      // C-order rows (vision): segment position -> voxel; null: lung-first
+    const int32_t* lpos;      // C-order rows (vision): segment position -> voxel (-1: pad); null: lung-first
     const int32_t* order;     // chunk indices, largest first (the persistent item order)
     int32_t n_chunk;
 };
@@ -786,17 +793,9 @@ __device__ __forceinline__ float4 load_nt(const float4* p) {
     return make_float4(t.x, t.y, t.z, t.w);
 }
 
-template <bool GATHER>
-__device__ __forceinline__ float lung_load(const DenseParams& P, const float* row, int pos) {
-    if constexpr (GATHER) return row[P.L.lpos[pos]];  // C-order row (vision): L2-resident map
-    else return __builtin_nontemporal_load(row + pos);
-}
-
-// One chain group: element k of lane l's chain (k < rows, l < nk[k]) -> x[k];
-// 0 elsewhere (an exact no-op for the chain sum and the count).
 // The plan is read-only while k_dense runs: read through the constant address
 // space so the compiler issues scalar loads (one s_load_dwordx16 per group)
-// instead of per-lane byte loads whose results gate the row addresses.
+// instead of per-lane loads whose results gate the row addresses.
 #if defined(__HIP_DEVICE_COMPILE__)
 template <typename T>
 __device__ __forceinline__ const __attribute__((address_space(4))) T* cst(const T* p) {
@@ -809,91 +808,111 @@ __device__ __forceinline__ const T* cst(const T* p) {
 }
 #endif
 
+typedef float lf4 __attribute__((ext_vector_type(4)));
+
+// One chain group: element k of the lane's 4 chains -> x[k] (zero where the
+// lane holds no element of row k: an exact no-op for the sums and the count;
+// pad slots are zeros in memory).  All 16 loads are issued unconditionally
+// (rows past the group's longest chain reload its first row; buffer loads with
+// the row offset in an SGPR), so their count is fixed.
 template <bool GATHER>
-__device__ __forceinline__ void lung_fetch(const DenseParams& P, const float* row, int seg_base, int g, int lane,
-                                           float (&x)[16], int& slot) {
+__device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer_rsrc_t rsrc, const float* row,
+                                           int seg_base, int g, int lane, lf4 (&x)[16], uint64_t& slot) {
     const auto G = cst(P.L.grp) + g;
     uint32_t ri[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) ri[k] = G->row[k];  // one s_load_dwordx16, one wait
     slot = P.L.slot[(size_t)g * 64 + lane];
-    // All 16 loads are issued, unconditionally: lanes past nk load the row's last
-    // element and rows past the group's longest chain its first element (lines
-    // the group fetches anyway) and drop the value.  A fixed load count lets the
-    // compiler wait for THIS group's loads only (vmcnt(16)) while the next
-    // group's are in flight; data-dependent branches made it wait for all.
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const int nk = (int)(ri[k] >> 16);
-        const int off = nk > 0 ? (int)(ri[k] & 0xffffu) + min(lane, nk - 1) : (int)(ri[0] & 0xffffu);
-        const float v = lung_load<GATHER>(P, row, seg_base + off);
-        x[k] = lane < nk ? v : 0.0f;
+        const int nl = (int)(ri[k] >> 16);
+        const int r0 = seg_base + (int)((nl > 0 ? ri[k] : ri[0]) & 0xffffu);
+        lf4 v;
+        if constexpr (GATHER) {
+            const int4 lp = *reinterpret_cast<const int4*>(P.L.lpos + r0 + 4 * lane);
+            v = lf4{lp.x >= 0 ? row[lp.x] : 0.0f, lp.y >= 0 ? row[lp.y] : 0.0f, lp.z >= 0 ? row[lp.z] : 0.0f,
+                    lp.w >= 0 ? row[lp.w] : 0.0f};
+        } else {
+            // aux 2: non-temporal (streamed once)
+            v = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * lane, 4 * r0, 2));
+        }
+        x[k] = lane < nl ? v : lf4{0.0f, 0.0f, 0.0f, 0.0f};
     }
 }
 
-// the lane's chain in order (numpy's r[j] += a[i] sequence), its over-threshold
-// count, and the chain sum into its LDS slot
-__device__ __forceinline__ void lung_consume(const DenseParams& P, int g, const float (&x)[16], int slot, float thr,
-                                             int& cnt, float* slots) {
+// the lane's 4 chains in order (numpy's r[j] += a[i] sequences), their
+// over-threshold count, and the chain sums into their LDS slots
+__device__ __forceinline__ void lung_consume(const DenseParams& P, int g, const lf4 (&x)[16], uint64_t slot,
+                                             float thr, int& cnt, float* slots) {
     const auto G = cst(P.L.grp) + g;
-    float acc = 0.0f;
+    lf4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         if (G->row[k] >> 16) {  // wave-uniform: a row of this group
-            acc = acc + x[k];
-            cnt += x[k] > thr ? 1 : 0;
+            acc.x = acc.x + x[k].x;
+            acc.y = acc.y + x[k].y;
+            acc.z = acc.z + x[k].z;
+            acc.w = acc.w + x[k].w;
+            cnt += (x[k].x > thr ? 1 : 0) + (x[k].y > thr ? 1 : 0) + (x[k].z > thr ? 1 : 0) + (x[k].w > thr ? 1 : 0);
         }
     }
-    if (slot != kNoSlot) slots[slot] = acc;
+    const uint32_t s0 = (uint32_t)slot & 0xffffu, s1 = (uint32_t)(slot >> 16) & 0xffffu;
+    const uint32_t s2 = (uint32_t)(slot >> 32) & 0xffffu, s3 = (uint32_t)(slot >> 48);
+    if (s0 != kNoSlot) slots[s0] = acc.x;
+    if (s1 != kNoSlot) slots[s1] = acc.y;
+    if (s2 != kNoSlot) slots[s2] = acc.z;
+    if (s3 != kNoSlot) slots[s3] = acc.w;
 }
 
 // Work item (env e, lung chunk j) of one wave: count and exact-order sum of
 // the chunk's lung voxels -> part_cnt / part_sum[e][j].  `wl`: the wave's
-// kLungWaveFloats of LDS.  The next group's loads are in flight while the
-// current one is summed.
+// kLungWaveFloats of LDS.  The first group's loads are issued before the
+// slots are cleared; later groups one at a time (16 KiB in flight per wave).
 template <bool GATHER>
 __device__ void lung_item(const DenseParams& P, int e, int j, int lane, float* wl) {
     const LChunk c = cst(P.L.chunk)[j];
     const float* row = P.st.dose + (size_t)e * P.G.Vpad;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), 0, P.G.Vpad * 4, 0x00020000);
     float* slots = wl;
     // a partial buffer's leaf values and plan slots overwrite the class slots:
     // lane L reads leaf L's 8 slots (all lanes in one instruction) before it
     // writes leafv[L], and leaf L + 64 (lane 0's second pass) lies above 64
     float* leafv = wl;
-    lds_wave_sync();  // the previous item's combine has read the slots
-    typedef float nf4 __attribute__((ext_vector_type(4)));
-    for (int i = lane; i < kLungSlotFloats / 4; i += 64) reinterpret_cast<nf4*>(slots)[i] = nf4{0.f, 0.f, 0.f, 0.f};
-    lds_wave_sync();
     const float thr = P.lung_thr;
     int cnt = 0;
-    float xa[16], xb[16];
-    int sa = kNoSlot, sb = kNoSlot;
+    lf4 x[16];
+    uint64_t sl;
     const int g0 = c.grp_base, g1 = c.grp_base + c.n_grp;
-    lung_fetch<GATHER>(P, row, c.seg_base, g0, lane, xa, sa);
-    for (int g = g0; g < g1; g += 2) {
-        if (g + 1 < g1) lung_fetch<GATHER>(P, row, c.seg_base, g + 1, lane, xb, sb);
-        lung_consume(P, g, xa, sa, thr, cnt, slots);
-        if (g + 2 < g1) lung_fetch<GATHER>(P, row, c.seg_base, g + 2, lane, xa, sa);
-        if (g + 1 < g1) lung_consume(P, g + 1, xb, sb, thr, cnt, slots);
+    lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g0, lane, x, sl);
+    lds_wave_sync();  // the previous item's combine has read the slots
+    for (int i = lane; i < kLungSlotFloats / 4; i += 64) reinterpret_cast<lf4*>(slots)[i] = lf4{0.f, 0.f, 0.f, 0.f};
+    lds_wave_sync();
+    for (int g = g0; g < g1; ++g) {
+        if (g > g0) lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g, lane, x, sl);
+        lung_consume(P, g, x, sl, thr, cnt, slots);
     }
     lds_wave_sync();
     float v;
     if (c.gen < 0) {
         // a whole buffer: lane = leaf (64 x 128 elements), leaf formula, then the
         // perfect tree over the 64 leaves as an xor butterfly
-        const nf4 a = reinterpret_cast<const nf4*>(slots)[2 * lane];
-        const nf4 b = reinterpret_cast<const nf4*>(slots)[2 * lane + 1];
+        const lf4 a = reinterpret_cast<const lf4*>(slots)[2 * lane];
+        const lf4 b = reinterpret_cast<const lf4*>(slots)[2 * lane + 1];
         v = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
     } else {
         const LGeneric q = cst(P.L.gen)[c.gen];
         for (int L = lane; L < q.n_leaf; L += 64) {
-            const nf4 a = reinterpret_cast<const nf4*>(slots)[2 * L];
-            const nf4 b = reinterpret_cast<const nf4*>(slots)[2 * L + 1];
+            const lf4 a = reinterpret_cast<const lf4*>(slots)[2 * L];
+            const lf4 b = reinterpret_cast<const lf4*>(slots)[2 * L + 1];
             float t = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
             const int t0 = P.L.tail_off[q.tail_base + L], t1 = P.L.tail_off[q.tail_base + L + 1];
-            for (int i = t0; i < t1; ++i) t = t + lung_load<GATHER>(P, row, P.L.tail_pos[i]);
+            for (int i = t0; i < t1; ++i) {
+                const int p = P.L.tail_pos[i];
+                t = t + (GATHER ? row[P.L.lpos[p]] : row[p]);
+            }
             leafv[L] = t;
         }
         v = run_plan(leafv, P.L.ops + q.op_base, P.L.lvl_end + q.lvl_base, q.n_leaf, q.nlev, q.result, lane);
@@ -1947,12 +1966,12 @@ struct LeafTree {
 
 struct LungPlanHost {
     int64_t V = 0;
-    int32_t n_seg = 0;            // lung voxels
+    int32_t n_seg = 0;            // segment slots: the lung voxels and the rows' pad slots
     std::vector<int32_t> pos_of;  // [V] voxel -> segment position (-1: not lung)
-    std::vector<int32_t> lpos;    // [n_seg] segment position -> voxel
+    std::vector<int32_t> lpos;    // [n_seg + 256] segment position -> voxel (-1: pad)
     std::vector<LChunk> chunk;
     std::vector<LGroup> grp;
-    std::vector<uint16_t> slot;
+    std::vector<uint64_t> slot;
     std::vector<LGeneric> gen;
     std::vector<uint32_t> ops;
     std::vector<int32_t> lvl_end, tail_off, tail_pos, order;
@@ -1960,7 +1979,9 @@ struct LungPlanHost {
 
 // Lays out the lung segment by numpy buffer, then by chain (LChunk comment):
 // chains of a buffer sorted by length (longest first, ties in slot order),
-// 64 per group, ragged rows.
+// 256 per group (4 per lane), ragged rows padded to a multiple of 4 slots.
+// lpos: segment position -> voxel, -1 for a pad slot, plus 4 * 64 trailing
+// -1 entries (the gather reads a whole wave's float4 of a row's last lanes).
 int build_lung_plan(const uint8_t* lungs, int64_t V, LungPlanHost& P) {
     P.V = V;
     P.pos_of.assign((size_t)V, -1);
@@ -2001,24 +2022,31 @@ int build_lung_plan(const uint8_t* lungs, int64_t V, LungPlanHost& P) {
         LChunk ch{};
         ch.seg_base = seg;
         ch.grp_base = (int32_t)P.grp.size();
-        for (size_t g0 = 0; g0 < chains.size(); g0 += 64) {
-            const size_t g1 = std::min(chains.size(), g0 + 64);
+        for (size_t g0 = 0; g0 < chains.size(); g0 += kLungGroup) {
+            const size_t g1 = std::min(chains.size(), g0 + kLungGroup);
             LGroup G{};
             const int rows = (int)chains[g0].vox.size();
             if (rows > 16) return fail(RT_ELIMIT, "lung sum plan: chain longer than 16");
             for (int k = 0; k < rows; ++k) {
                 int nk = 0;
                 for (size_t l = g0; l < g1; ++l) nk += (int)chains[l].vox.size() > k ? 1 : 0;
-                G.row[k] = (uint32_t)(seg - ch.seg_base) | (uint32_t)nk << 16;
-                for (int l = 0; l < nk; ++l) {
-                    const int32_t v = chains[g0 + l].vox[k];
-                    P.pos_of[v] = seg + l;
+                const int nk4 = (nk + 3) / 4 * 4;
+                if (seg - ch.seg_base + nk4 > 0xffff) return fail(RT_ELIMIT, "lung sum plan: chunk too large");
+                G.row[k] = (uint32_t)(seg - ch.seg_base) | (uint32_t)(nk4 / 4) << 16;
+                for (int l = 0; l < nk4; ++l) {
+                    const int32_t v = l < nk ? chains[g0 + l].vox[k] : -1;
+                    if (v >= 0) P.pos_of[v] = seg + l;
                     P.lpos.push_back(v);
                 }
-                seg += nk;
+                seg += nk4;
             }
             P.grp.push_back(G);
-            for (size_t l = g0; l < g0 + 64; ++l) P.slot.push_back(l < g1 ? chains[l].slot : kNoSlot);
+            for (size_t l = g0; l < g0 + kLungGroup; l += 4) {
+                uint64_t w = 0;
+                for (int i = 0; i < 4; ++i)
+                    w |= (uint64_t)(l + i < g1 ? chains[l + i].slot : kNoSlot) << (16 * i);
+                P.slot.push_back(w);
+            }
         }
         ch.n_grp = (int32_t)P.grp.size() - ch.grp_base;
         ch.gen = -1;
@@ -2057,6 +2085,7 @@ int build_lung_plan(const uint8_t* lungs, int64_t V, LungPlanHost& P) {
         P.chunk.push_back(ch);
     }
     P.n_seg = seg;
+    P.lpos.insert(P.lpos.end(), 4 * 64, -1);
     // the persistent item order: chunks by size, largest first
     const int nc = (int)P.chunk.size();
     auto csize = [&](int j) { return (j + 1 < nc ? P.chunk[j + 1].seg_base : seg) - P.chunk[j].seg_base; };
@@ -2076,13 +2105,18 @@ float eval_lung_plan(const LungPlanHost& P, const float* dose) {
         float slots[kLungSlotFloats] = {};
         for (int g = c.grp_base; g < c.grp_base + c.n_grp; ++g) {
             const LGroup& G = P.grp[g];
-            float chain[64] = {};
+            float chain[kLungGroup] = {};
             for (int k = 0; k < 16; ++k) {
-                const int pos = c.seg_base + (int)(G.row[k] & 0xffffu), nk = (int)(G.row[k] >> 16);
-                for (int l = 0; l < nk; ++l) chain[l] = chain[l] + dose[P.lpos[pos + l]];
+                const int pos = c.seg_base + (int)(G.row[k] & 0xffffu), n4 = 4 * (int)(G.row[k] >> 16);
+                for (int l = 0; l < n4; ++l) {
+                    const int32_t v = P.lpos[pos + l];
+                    chain[l] = chain[l] + (v >= 0 ? dose[v] : 0.0f);
+                }
             }
-            for (int l = 0; l < 64; ++l)
-                if (P.slot[(size_t)g * 64 + l] != kNoSlot) slots[P.slot[(size_t)g * 64 + l]] = chain[l];
+            for (int l = 0; l < kLungGroup; ++l) {
+                const uint32_t sl = (uint32_t)(P.slot[(size_t)g * 64 + l / 4] >> (16 * (l % 4))) & 0xffffu;
+                if (sl != kNoSlot) slots[sl] = chain[l];
+            }
         }
         auto leaf = [&](int L) {
             const float* r = slots + 8 * L;
@@ -2421,8 +2455,11 @@ int rt_env_create(const rt_env_config* cfg, int device, rt_env** out) {
         }
     std::vector<int32_t> dpos;
     if (env->lung_first) {
+        // rows: the lung segment (chains + pad slots), then the other voxels
+        const int64_t need = (int64_t)lp.n_seg + (G.V - lung_count);
+        env->G.Vpad = std::max<int32_t>(G.Vpad, (int32_t)((need + 1023) / 1024 * 1024));
         dpos.resize(G.V);
-        int64_t b = lung_count;
+        int64_t b = lp.n_seg;
         for (int64_t v = 0; v < G.V; ++v) dpos[v] = lp.pos_of[v] >= 0 ? lp.pos_of[v] : (int32_t)b++;
     }
     env->n_chunk = (int)lp.chunk.size();
