@@ -864,63 +864,108 @@ __device__ __forceinline__ void lung_consume(const DenseParams& P, int g, const 
     if (s3 != kNoSlot) slots[s3] = acc.w;
 }
 
-// Work item (env e, lung chunk j) of one wave: count and exact-order sum of
-// the chunk's lung voxels -> part_cnt / part_sum[e][j].  `wl`: the wave's
-// kLungWaveFloats of LDS.  The first group's loads are issued before the
-// slots are cleared; later groups one at a time (16 KiB in flight per wave).
+// LDS order inside one wave: its DS instructions execute in issue order, so a
+// lane reads what another lane of the same wave wrote earlier with no wait on
+// memory -- only the compiler must keep the order (the workgroup fence of
+// lds_wave_sync would also wait for every vector load in flight).
+__device__ __forceinline__ void lds_wave_order() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// The (env, chunk) items of envs [e_begin, e_begin + n_env) a wave takes:
+// first, first + stride, ...  Item i -> chunk order[i / n_env] (chunk-major,
+// largest chunks first), env e_begin + i % n_env.  Per item: its groups'
+// loads and chain sums, then -- with the NEXT item's first group already in
+// flight -- the combine (leaf formula, butterfly or level plan) and the
+// partials, written for STEP envs only (a RESET env's row may be zeroed by
+// zero_reset_share meanwhile; its values are dropped).  `wl`: the wave's
+// kLungWaveFloats of LDS.
 template <bool GATHER>
-__device__ void lung_item(const DenseParams& P, int e, int j, int lane, float* wl) {
-    const LChunk c = cst(P.L.chunk)[j];
-    const float* row = P.st.dose + (size_t)e * P.G.Vpad;
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), 0, P.G.Vpad * 4, 0x00020000);
+__device__ void lung_stream(const DenseParams& P, int n_env, int first, int stride, int lane, float* wl) {
+    const int n_items = n_env * P.L.n_chunk;
+    if (first >= n_items) return;
     float* slots = wl;
     // a partial buffer's leaf values and plan slots overwrite the class slots:
     // lane L reads leaf L's 8 slots (all lanes in one instruction) before it
     // writes leafv[L], and leaf L + 64 (lane 0's second pass) lies above 64
     float* leafv = wl;
     const float thr = P.lung_thr;
-    int cnt = 0;
+    auto row_of = [&](int e) { return P.st.dose + (size_t)e * P.G.Vpad; };
+    auto rsrc_of = [&](const float* r) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(r), 0, P.G.Vpad * 4, 0x00020000);
+    };
+    int it = first;
+    int e = P.e_begin + it % n_env, j = cst(P.L.order)[it / n_env];
+    LChunk c = cst(P.L.chunk)[j];
+    const float* row = row_of(e);
+    __amdgpu_buffer_rsrc_t rsrc = rsrc_of(row);
     lf4 x[16];
     uint64_t sl;
-    const int g0 = c.grp_base, g1 = c.grp_base + c.n_grp;
-    lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g0, lane, x, sl);
-    lds_wave_sync();  // the previous item's combine has read the slots
+    lung_fetch<GATHER>(P, rsrc, row, c.seg_base, c.grp_base, lane, x, sl);
     for (int i = lane; i < kLungSlotFloats / 4; i += 64) reinterpret_cast<lf4*>(slots)[i] = lf4{0.f, 0.f, 0.f, 0.f};
-    lds_wave_sync();
-    for (int g = g0; g < g1; ++g) {
-        if (g > g0) lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g, lane, x, sl);
-        lung_consume(P, g, x, sl, thr, cnt, slots);
-    }
-    lds_wave_sync();
-    float v;
-    if (c.gen < 0) {
-        // a whole buffer: lane = leaf (64 x 128 elements), leaf formula, then the
-        // perfect tree over the 64 leaves as an xor butterfly
-        const lf4 a = reinterpret_cast<const lf4*>(slots)[2 * lane];
-        const lf4 b = reinterpret_cast<const lf4*>(slots)[2 * lane + 1];
-        v = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
-    } else {
-        const LGeneric q = cst(P.L.gen)[c.gen];
-        for (int L = lane; L < q.n_leaf; L += 64) {
-            const lf4 a = reinterpret_cast<const lf4*>(slots)[2 * L];
-            const lf4 b = reinterpret_cast<const lf4*>(slots)[2 * L + 1];
-            float t = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
-            const int t0 = P.L.tail_off[q.tail_base + L], t1 = P.L.tail_off[q.tail_base + L + 1];
-            for (int i = t0; i < t1; ++i) {
-                const int p = P.L.tail_pos[i];
-                t = t + (GATHER ? row[P.L.lpos[p]] : row[p]);
-            }
-            leafv[L] = t;
+    lds_wave_order();
+    for (;;) {
+        int cnt = 0;
+        for (int g = c.grp_base; g < c.grp_base + c.n_grp; ++g) {
+            if (g > c.grp_base) lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g, lane, x, sl);
+            lung_consume(P, g, x, sl, thr, cnt, slots);
         }
-        v = run_plan(leafv, P.L.ops + q.op_base, P.L.lvl_end + q.lvl_base, q.n_leaf, q.nlev, q.result, lane);
-    }
-    cnt = wave_sum_i(cnt);
-    if (lane == 0) {
-        P.part_cnt[(size_t)e * P.L.n_chunk + j] = cnt;
-        P.part_sum[(size_t)e * P.L.n_chunk + j] = v;
+        lds_wave_order();
+        // the next item's first group in flight during this item's combine
+        const int nit = it + stride;
+        int ne = e, nj = j;
+        LChunk nc = c;
+        const float* nrow = row;
+        __amdgpu_buffer_rsrc_t nrsrc = rsrc;
+        if (nit < n_items) {
+            ne = P.e_begin + nit % n_env;
+            nj = cst(P.L.order)[nit / n_env];
+            nc = cst(P.L.chunk)[nj];
+            nrow = row_of(ne);
+            nrsrc = rsrc_of(nrow);
+            lung_fetch<GATHER>(P, nrsrc, nrow, nc.seg_base, nc.grp_base, lane, x, sl);
+        }
+        float v;
+        if (c.gen < 0) {
+            // a whole buffer: lane = leaf (64 x 128 elements), leaf formula, then
+            // the perfect tree over the 64 leaves as an xor butterfly
+            const lf4 a = reinterpret_cast<const lf4*>(slots)[2 * lane];
+            const lf4 b = reinterpret_cast<const lf4*>(slots)[2 * lane + 1];
+            v = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
+        } else {
+            const LGeneric q = cst(P.L.gen)[c.gen];
+            for (int L = lane; L < q.n_leaf; L += 64) {
+                const lf4 a = reinterpret_cast<const lf4*>(slots)[2 * L];
+                const lf4 b = reinterpret_cast<const lf4*>(slots)[2 * L + 1];
+                float t = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+                const int t0 = P.L.tail_off[q.tail_base + L], t1 = P.L.tail_off[q.tail_base + L + 1];
+                for (int i = t0; i < t1; ++i) {
+                    const int p = P.L.tail_pos[i];
+                    t = t + (GATHER ? row[P.L.lpos[p]] : row[p]);
+                }
+                leafv[L] = t;
+            }
+            v = run_plan(leafv, P.L.ops + q.op_base, P.L.lvl_end + q.lvl_base, q.n_leaf, q.nlev, q.result, lane);
+        }
+        cnt = wave_sum_i(cnt);
+        if (lane == 0 && cst(P.st.mode_b)[e] == MODE_STEP) {
+            P.part_cnt[(size_t)e * P.L.n_chunk + j] = cnt;
+            P.part_sum[(size_t)e * P.L.n_chunk + j] = v;
+        }
+        if (nit >= n_items) break;
+        lds_wave_order();  // the combine has read the slots
+        for (int i = lane; i < kLungSlotFloats / 4; i += 64)
+            reinterpret_cast<lf4*>(slots)[i] = lf4{0.f, 0.f, 0.f, 0.f};
+        lds_wave_order();
+        it = nit;
+        e = ne;
+        j = nj;
+        c = nc;
+        row = nrow;
+        rsrc = nrsrc;
     }
 }
 
@@ -993,46 +1038,23 @@ __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, i
     }
 }
 
-// Grid k_dense: the first zero_rows rows of blocks (dispatched first) zero
-// the RESET envs' rows in equal shares; the other blocks run 4 (env, chunk)
-// items, one per wave, largest chunks first so the launch's tail is made of
-// small items.  GATHER: C-order rows (vision handles, after k_dense_vis).
+// k_dense: waves stride over the (env, chunk) items of envs [e_begin,
+// e_begin + n_env) (lung_stream), then every block zeroes its share of the
+// RESET envs' rows.  A fixed grid of a few blocks per CU: the pipelined dense
+// rollout's dose stream leaves CU slots free for the other env group's
+// latency-bound kernels; the stepwise / one-group launches fill the chip.
+// Items are ordered chunk-major, largest chunks first, env-minor, so a wave's
+// strided items sample every chunk size (an env-major order would give each
+// wave one fixed chunk index: a 250x spread of bytes per wave).
+// GATHER: C-order rows (vision handles, after k_dense_vis; no zeroing).
 template <bool GATHER>
-__global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env, int zero_rows) {
-    if (!GATHER && (int)blockIdx.y < zero_rows) {
-        zero_reset_share(P, P.e_begin, n_env, blockIdx.y * gridDim.x + blockIdx.x, zero_rows * gridDim.x);
-        return;
-    }
+__global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env) {
     __shared__ __attribute__((aligned(16))) float dsm[4 * kLungWaveFloats];
     // wave-uniform (readfirstlane): the item, its chunk and group records then
     // live in SGPRs and the plan is read by scalar loads
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int it = (int)(((blockIdx.y - (GATHER ? 0 : zero_rows)) * gridDim.x + blockIdx.x) * 4 + w);
-    if (it >= n_env * P.L.n_chunk) return;  // wave-uniform
-    const int e = P.e_begin + it % n_env, j = cst(P.L.order)[it / n_env];
-    if (cst(P.st.mode_b)[e] != MODE_STEP) return;
-    lung_item<GATHER>(P, e, j, lane, dsm + w * kLungWaveFloats);
-}
-
-// k_dense with a fixed grid (a few blocks per CU) whose waves stride over the
-// (env, chunk) items of envs [e_begin, e_begin + n_env): the pipelined dense
-// rollout's dose stream.  It leaves CU slots free for the other env group's
-// latency-bound kernels (the grid version fills every slot and has a launch
-// tail).  Items are ordered chunk-major, largest chunks first, env-minor, so a
-// wave's strided items sample every chunk size (an env-major order would give
-// each wave one fixed chunk index: a 250x spread of bytes per wave).
-__global__ __launch_bounds__(256) void k_dense_persist(DenseParams P, int n_env) {
-    __shared__ __attribute__((aligned(16))) float dsm[4 * kLungWaveFloats];
-    // wave-uniform (readfirstlane): the item, its chunk and group records then
-    // live in SGPRs and the plan is read by scalar loads
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int n_items = n_env * P.L.n_chunk;
-    for (int it = blockIdx.x * 4 + w; it < n_items; it += gridDim.x * 4) {
-        const int e = P.e_begin + it % n_env, j = cst(P.L.order)[it / n_env];
-        if (cst(P.st.mode_b)[e] != MODE_STEP) continue;  // wave-uniform
-        lung_item<false>(P, e, j, lane, dsm + w * kLungWaveFloats);
-    }
-    zero_reset_share(P, P.e_begin, n_env, blockIdx.x, gridDim.x);
+    lung_stream<GATHER>(P, n_env, blockIdx.x * 4 + w, gridDim.x * 4, lane, dsm + w * kLungWaveFloats);
+    if (!GATHER) zero_reset_share(P, P.e_begin, n_env, blockIdx.x, gridDim.x);
 }
 
 constexpr int kMaxRolloutGroups = 4;
@@ -2179,6 +2201,7 @@ struct rt_env {
     int lung_first = 0;      // dose rows lung-first (dense visionless), else C order
     int lung_n = 0;          // lung voxels (the lung-first segment)
     int n_chunk = 0;         // numpy buffers holding lung voxels (k_dense items per env)
+    int dense_bpc = 0;       // k_dense blocks resident per CU (occupancy query, first launch)
     LungParams lplan{};      // the lung sum plan (device copies)
     int32_t* dose_pos_d = nullptr;  // voxel -> row position (lung_first)
     size_t finish_smem = 0;  // k_finish dynamic LDS (4 waves)
@@ -2766,27 +2789,31 @@ int launch_dense(rt_env* env, int e0, int n, float* obs, int persist_bpc, hipStr
     const DenseParams dp = dense_params(env, e0);
     if (env->incremental) {
         // no dense pass: k_beam maintains the lung count and sum
-    } else if (env->visionless) {
-        if (persist_bpc > 0) {
-            hipLaunchKernelGGL(k_dense_persist, dim3(persist_bpc * env->num_cu), dim3(kStepThreads), 0, stream, dp,
-                               n);
-        } else {
-            // one wave per (env, chunk) item, 4 per block, after kZeroBlocks zeroing blocks
-            const int64_t blocks = ((int64_t)n * env->n_chunk + 3) / 4;
-            const int gx = kZeroBlocks;
-            const int rows = (int)((blocks + gx - 1) / gx);
-            hipLaunchKernelGGL(k_dense<false>, dim3(gx, rows + 1), dim3(kStepThreads), 0, stream, dp, n, 1);
-        }
-        RT_LAUNCH_CHECK("k_dense");
     } else {
-        DenseVisParams dv{dp, obs, env->render_src, env->render_rows, env->render_stride, env->render_n};
-        hipLaunchKernelGGL(k_dense_vis, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dv);
-        RT_LAUNCH_CHECK("k_dense_vis");
-        const int64_t blocks = ((int64_t)n * env->n_chunk + 3) / 4;
-        if (blocks > 0) {
-            const int gx = (int)std::min<int64_t>(blocks, kZeroBlocks);
-            const int rows = (int)((blocks + gx - 1) / gx);
-            hipLaunchKernelGGL(k_dense<true>, dim3(gx, rows), dim3(kStepThreads), 0, stream, dp, n, 0);
+        if (!env->visionless) {
+            DenseVisParams dv{dp, obs, env->render_src, env->render_rows, env->render_stride, env->render_n};
+            hipLaunchKernelGGL(k_dense_vis, dim3(env->slices, n), dim3(kStepThreads), 0, stream, dv);
+            RT_LAUNCH_CHECK("k_dense_vis");
+        }
+        // persist_bpc blocks per CU (the pipelined rollout), else as many as are
+        // resident at once (a strided wave's items all run in one round)
+        if (env->dense_bpc == 0) {
+            int bpc = 0;
+            const void* kf = env->visionless ? reinterpret_cast<const void*>(&k_dense<false>)
+                                             : reinterpret_cast<const void*>(&k_dense<true>);
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kf, kStepThreads, 0) != hipSuccess || bpc < 1)
+                bpc = 4;
+            env->dense_bpc = bpc;
+        }
+        const int bpc = persist_bpc > 0 ? persist_bpc : env->dense_bpc;
+        const int64_t items = (int64_t)n * env->n_chunk;
+        const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)bpc * env->num_cu, (items + 3) / 4));
+        if (env->visionless) {
+            hipLaunchKernelGGL(k_dense<false>, dim3(std::max(blocks, persist_bpc > 0 ? blocks : kZeroBlocks)),
+                               dim3(kStepThreads), 0, stream, dp, n);
+            RT_LAUNCH_CHECK("k_dense");
+        } else if (items > 0) {
+            hipLaunchKernelGGL(k_dense<true>, dim3(blocks), dim3(kStepThreads), 0, stream, dp, n);
             RT_LAUNCH_CHECK("k_dense<gather>");
         }
     }
