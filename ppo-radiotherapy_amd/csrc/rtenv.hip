@@ -710,9 +710,10 @@ __device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const 
 // a chunk, by chain: the chains sorted by length, 256 per group -- lane l of a
 // wave owns chains 4l..4l+3 -- group rows stored ragged: row k holds element k
 // of the group's first nk[k] chains, contiguously, padded with zero slots to a
-// multiple of 4 (~1.5 % of the segment at 64^3).  A wave streams a chunk with
-// coalesced 16-B loads (element k of its four chains per lane, 16 rows in
-// flight: 16 KiB per wave), each lane summing its chains in order.  The chain
+// whole number of 128-B lines (no line holds two rows).  A wave streams a chunk
+// with coalesced 16-B loads (element k of its four chains per lane, a group's
+// rows in flight: up to 16 KiB per wave), each lane summing its chains in
+// order.  The chain
 // sums go to LDS slots [leaf][class]; lane = leaf then combines its 8 slots,
 // and a whole 8192-element buffer (64 leaves of 128, a perfect tree) finishes
 // with a 6-step xor butterfly (IEEE addition commutes, so both lanes of a pair
@@ -732,7 +733,7 @@ constexpr int kLungGroup = 256;         // chains per group (4 per lane)
 constexpr uint16_t kNoSlot = 0xFFFFu;
 
 struct LChunk {          // one numpy buffer holding lung voxels
-    int32_t seg_base;    // segment position of its first chain element (a multiple of 4)
+    int32_t seg_base;    // segment position of its first chain element (a multiple of 32)
     int32_t grp_base;    // its first chain group
     int32_t n_grp;
     int32_t gen;         // -1: a whole 8192-element buffer (butterfly); else its LGeneric record
@@ -812,9 +813,10 @@ typedef float lf4 __attribute__((ext_vector_type(4)));
 
 // One chain group: element k of the lane's 4 chains -> x[k] (zero where the
 // lane holds no element of row k: an exact no-op for the sums and the count;
-// pad slots are zeros in memory).  All 16 loads are issued unconditionally
-// (rows past the group's longest chain reload its first row; buffer loads with
-// the row offset in an SGPR), so their count is fixed.
+// pad slots are zeros in memory).  Only the group's rows are loaded (a uniform
+// branch per row: the profile of round 6 had the texture-address unit 73 %
+// busy when every group issued all 16 rows); buffer loads, the row offset in
+// an SGPR.
 template <bool GATHER>
 __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer_rsrc_t rsrc, const float* row,
                                            int seg_base, int g, int lane, lf4 (&x)[16], uint64_t& slot) {
@@ -826,7 +828,11 @@ __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int nl = (int)(ri[k] >> 16);
-        const int r0 = seg_base + (int)((nl > 0 ? ri[k] : ri[0]) & 0xffffu);
+        if (nl == 0) {  // wave-uniform: past the group's longest chain
+            x[k] = lf4{0.0f, 0.0f, 0.0f, 0.0f};
+            continue;
+        }
+        const int r0 = seg_base + (int)(ri[k] & 0xffffu);
         lf4 v;
         if constexpr (GATHER) {
             const int4 lp = *reinterpret_cast<const int4*>(P.L.lpos + r0 + 4 * lane);
@@ -2052,15 +2058,18 @@ int build_lung_plan(const uint8_t* lungs, int64_t V, LungPlanHost& P) {
             for (int k = 0; k < rows; ++k) {
                 int nk = 0;
                 for (size_t l = g0; l < g1; ++l) nk += (int)chains[l].vox.size() > k ? 1 : 0;
-                const int nk4 = (nk + 3) / 4 * 4;
-                if (seg - ch.seg_base + nk4 > 0xffff) return fail(RT_ELIMIT, "lung sum plan: chunk too large");
+                // a row: its float4 (ceil(nk / 4) lanes), padded to a whole number of
+                // 128-B lines, so no line holds two rows (a non-temporal load
+                // would fetch a shared line twice: +15 % HBM bytes, round 6)
+                const int nk4 = (nk + 3) / 4 * 4, span = (nk + 31) / 32 * 32;
+                if (seg - ch.seg_base + span > 0xffff) return fail(RT_ELIMIT, "lung sum plan: chunk too large");
                 G.row[k] = (uint32_t)(seg - ch.seg_base) | (uint32_t)(nk4 / 4) << 16;
-                for (int l = 0; l < nk4; ++l) {
+                for (int l = 0; l < span; ++l) {
                     const int32_t v = l < nk ? chains[g0 + l].vox[k] : -1;
                     if (v >= 0) P.pos_of[v] = seg + l;
                     P.lpos.push_back(v);
                 }
-                seg += nk4;
+                seg += span;
             }
             P.grp.push_back(G);
             for (size_t l = g0; l < g0 + kLungGroup; l += 4) {
