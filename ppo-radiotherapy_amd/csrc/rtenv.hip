@@ -838,11 +838,15 @@ __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer
             const int4 lp = *reinterpret_cast<const int4*>(P.L.lpos + r0 + 4 * lane);
             v = lf4{lp.x >= 0 ? row[lp.x] : 0.0f, lp.y >= 0 ? row[lp.y] : 0.0f, lp.z >= 0 ? row[lp.z] : 0.0f,
                     lp.w >= 0 ? row[lp.w] : 0.0f};
+            x[k] = lane < nl ? v : lf4{0.0f, 0.0f, 0.0f, 0.0f};
         } else {
-            // aux 2: non-temporal (streamed once)
-            v = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * lane, 4 * r0, 2));
+            // a buffer resource of exactly the row's nl float4: the lanes past it
+            // read zeros without a memory access (no line of the next row fetched
+            // twice); aux 2: non-temporal (streamed once)
+            const __amdgpu_buffer_rsrc_t rk =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row) + r0, 0, 16 * nl, 0x00020000);
+            x[k] = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(rk, 16 * lane, 0, 2));
         }
-        x[k] = lane < nl ? v : lf4{0.0f, 0.0f, 0.0f, 0.0f};
     }
 }
 
