@@ -883,9 +883,21 @@ __device__ __forceinline__ void lds_wave_order() {
     asm volatile("" ::: "memory");
 }
 
+// Item i of a launch -> env e_begin + i / n_chunk, chunk (i + e) % n_chunk:
+// env-major, so the waves in flight at once read neighbouring chunks of the
+// same few dose rows (an env-minor order put them 1 MiB apart: every wave on
+// the same offset of its row -- 4.3 vs 5.1 TB/s alone, round 6), the chunk
+// index rotated by the env so a wave's strided items visit every chunk size
+// (without it a stride that is a multiple of n_chunk pins each wave to one
+// chunk index: a 250x spread of bytes per wave).
+__device__ __forceinline__ void lung_item_of(int n_chunk, int e_begin, int i, int& e, int& j) {
+    const int r = i / n_chunk;
+    e = e_begin + r;
+    j = (i - r * n_chunk + r) % n_chunk;
+}
+
 // The (env, chunk) items of envs [e_begin, e_begin + n_env) a wave takes:
-// first, first + stride, ...  Item i -> chunk order[i / n_env] (chunk-major,
-// largest chunks first), env e_begin + i % n_env.  Per item: its groups'
+// first, first + stride, ... (lung_item_of).  Per item: its groups'
 // loads and chain sums, then -- with the NEXT item's first group already in
 // flight -- the combine (leaf formula, butterfly or level plan) and the
 // partials, written for STEP envs only (a RESET env's row may be zeroed by
@@ -906,7 +918,8 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
         return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(r), 0, P.G.Vpad * 4, 0x00020000);
     };
     int it = first;
-    int e = P.e_begin + it % n_env, j = cst(P.L.order)[it / n_env];
+    int e, j;
+    lung_item_of(P.L.n_chunk, P.e_begin, it, e, j);
     LChunk c = cst(P.L.chunk)[j];
     const float* row = row_of(e);
     __amdgpu_buffer_rsrc_t rsrc = rsrc_of(row);
@@ -929,8 +942,7 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
         const float* nrow = row;
         __amdgpu_buffer_rsrc_t nrsrc = rsrc;
         if (nit < n_items) {
-            ne = P.e_begin + nit % n_env;
-            nj = cst(P.L.order)[nit / n_env];
+            lung_item_of(P.L.n_chunk, P.e_begin, nit, ne, nj);
             nc = cst(P.L.chunk)[nj];
             nrow = row_of(ne);
             nrsrc = rsrc_of(nrow);
@@ -1053,9 +1065,7 @@ __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, i
 // RESET envs' rows.  A fixed grid of a few blocks per CU: the pipelined dense
 // rollout's dose stream leaves CU slots free for the other env group's
 // latency-bound kernels; the stepwise / one-group launches fill the chip.
-// Items are ordered chunk-major, largest chunks first, env-minor, so a wave's
-// strided items sample every chunk size (an env-major order would give each
-// wave one fixed chunk index: a 250x spread of bytes per wave).
+// Items: lung_item_of.
 // GATHER: C-order rows (vision handles, after k_dense_vis; no zeroing).
 template <bool GATHER>
 __global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env) {
