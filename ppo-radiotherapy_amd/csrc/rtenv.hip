@@ -840,12 +840,12 @@ __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer
                     lp.w >= 0 ? row[lp.w] : 0.0f};
             x[k] = lane < nl ? v : lf4{0.0f, 0.0f, 0.0f, 0.0f};
         } else {
-            // a buffer resource of exactly the row's nl float4: the lanes past it
-            // read zeros without a memory access (no line of the next row fetched
-            // twice); aux 2: non-temporal (streamed once)
-            const __amdgpu_buffer_rsrc_t rk =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row) + r0, 0, 16 * nl, 0x00020000);
-            x[k] = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(rk, 16 * lane, 0, 2));
+            // only the row's nl lanes load (exec-masked: the lanes past it take no
+            // texture-address cycles and fetch no line of the next row); aux 2:
+            // non-temporal (streamed once)
+            lf4 v = lf4{0.0f, 0.0f, 0.0f, 0.0f};
+            if (lane < nl) v = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * lane, 4 * r0, 2));
+            x[k] = v;
         }
     }
 }
@@ -883,17 +883,15 @@ __device__ __forceinline__ void lds_wave_order() {
     asm volatile("" ::: "memory");
 }
 
-// Item i of a launch -> env e_begin + i / n_chunk, chunk (i + e) % n_chunk:
-// env-major, so the waves in flight at once read neighbouring chunks of the
-// same few dose rows (an env-minor order put them 1 MiB apart: every wave on
-// the same offset of its row -- 4.3 vs 5.1 TB/s alone, round 6), the chunk
-// index rotated by the env so a wave's strided items visit every chunk size
-// (without it a stride that is a multiple of n_chunk pins each wave to one
-// chunk index: a 250x spread of bytes per wave).
-__device__ __forceinline__ void lung_item_of(int n_chunk, int e_begin, int i, int& e, int& j) {
-    const int r = i / n_chunk;
-    e = e_begin + r;
-    j = (i - r * n_chunk + r) % n_chunk;
+// Item i of a launch -> chunk order[i / n_env] (chunk-major, largest chunks
+// first), env e_begin + i % n_env: the waves in flight at once read the same
+// chunk of many dose rows (1 MiB apart; an env-major order -- neighbouring
+// chunks of a few rows -- streamed 4.1 vs 5.1 TB/s alone, round 6), and a
+// wave's strided items visit every chunk size (an env-major order without a
+// rotation pins each wave to one chunk index: a 250x spread of bytes).
+__device__ __forceinline__ void lung_item_of(const LungParams& L, int n_env, int e_begin, int i, int& e, int& j) {
+    e = e_begin + i % n_env;
+    j = cst(L.order)[i / n_env];
 }
 
 // The (env, chunk) items of envs [e_begin, e_begin + n_env) a wave takes:
@@ -919,7 +917,7 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
     };
     int it = first;
     int e, j;
-    lung_item_of(P.L.n_chunk, P.e_begin, it, e, j);
+    lung_item_of(P.L, n_env, P.e_begin, it, e, j);
     LChunk c = cst(P.L.chunk)[j];
     const float* row = row_of(e);
     __amdgpu_buffer_rsrc_t rsrc = rsrc_of(row);
@@ -942,7 +940,7 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
         const float* nrow = row;
         __amdgpu_buffer_rsrc_t nrsrc = rsrc;
         if (nit < n_items) {
-            lung_item_of(P.L.n_chunk, P.e_begin, nit, ne, nj);
+            lung_item_of(P.L, n_env, P.e_begin, nit, ne, nj);
             nc = cst(P.L.chunk)[nj];
             nrow = row_of(ne);
             nrsrc = rsrc_of(nrow);
