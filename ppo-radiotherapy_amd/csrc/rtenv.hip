@@ -817,16 +817,17 @@ typedef float lf4 __attribute__((ext_vector_type(4)));
 // branch per row: the profile of round 6 had the texture-address unit 73 %
 // busy when every group issued all 16 rows); buffer loads, the row offset in
 // an SGPR.
+constexpr int kLungHalf = 8;  // rows per fetch: a group's 16 rows in two halves
+
 template <bool GATHER>
 __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer_rsrc_t rsrc, const float* row,
-                                           int seg_base, int g, int lane, lf4 (&x)[16], uint64_t& slot) {
+                                           int seg_base, int g, int h, int lane, lf4 (&x)[kLungHalf]) {
     const auto G = cst(P.L.grp) + g;
-    uint32_t ri[16];
+    uint32_t ri[kLungHalf];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) ri[k] = G->row[k];  // one s_load_dwordx16, one wait
-    slot = P.L.slot[(size_t)g * 64 + lane];
+    for (int k = 0; k < kLungHalf; ++k) ri[k] = G->row[h * kLungHalf + k];  // one s_load_dwordx8, one wait
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < kLungHalf; ++k) {
         const int nl = (int)(ri[k] >> 16);
         if (nl == 0) {  // wave-uniform: past the group's longest chain
             x[k] = lf4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -850,15 +851,14 @@ __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer
     }
 }
 
-// the lane's 4 chains in order (numpy's r[j] += a[i] sequences), their
-// over-threshold count, and the chain sums into their LDS slots
-__device__ __forceinline__ void lung_consume(const DenseParams& P, int g, const lf4 (&x)[16], uint64_t slot,
-                                             float thr, int& cnt, float* slots) {
+// rows h*8 .. h*8+7 of the lane's 4 chains in order (numpy's r[j] += a[i]
+// sequences) onto acc, and their over-threshold count
+__device__ __forceinline__ void lung_consume(const DenseParams& P, int g, int h, const lf4 (&x)[kLungHalf], lf4& acc,
+                                             float thr, int& cnt) {
     const auto G = cst(P.L.grp) + g;
-    lf4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (G->row[k] >> 16) {  // wave-uniform: a row of this group
+    for (int k = 0; k < kLungHalf; ++k) {
+        if (G->row[h * kLungHalf + k] >> 16) {  // wave-uniform: a row of this group
             acc.x = acc.x + x[k].x;
             acc.y = acc.y + x[k].y;
             acc.z = acc.z + x[k].z;
@@ -866,6 +866,10 @@ __device__ __forceinline__ void lung_consume(const DenseParams& P, int g, const 
             cnt += (x[k].x > thr ? 1 : 0) + (x[k].y > thr ? 1 : 0) + (x[k].z > thr ? 1 : 0) + (x[k].w > thr ? 1 : 0);
         }
     }
+}
+
+// the group's 4 chain sums of the lane into their LDS slots
+__device__ __forceinline__ void lung_emit(uint64_t slot, const lf4& acc, float* slots) {
     const uint32_t s0 = (uint32_t)slot & 0xffffu, s1 = (uint32_t)(slot >> 16) & 0xffffu;
     const uint32_t s2 = (uint32_t)(slot >> 32) & 0xffffu, s3 = (uint32_t)(slot >> 48);
     if (s0 != kNoSlot) slots[s0] = acc.x;
@@ -921,16 +925,22 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
     LChunk c = cst(P.L.chunk)[j];
     const float* row = row_of(e);
     __amdgpu_buffer_rsrc_t rsrc = rsrc_of(row);
-    lf4 x[16];
-    uint64_t sl;
-    lung_fetch<GATHER>(P, rsrc, row, c.seg_base, c.grp_base, lane, x, sl);
+    lf4 x[kLungHalf];
+    lung_fetch<GATHER>(P, rsrc, row, c.seg_base, c.grp_base, 0, lane, x);
     for (int i = lane; i < kLungSlotFloats / 4; i += 64) reinterpret_cast<lf4*>(slots)[i] = lf4{0.f, 0.f, 0.f, 0.f};
     lds_wave_order();
     for (;;) {
         int cnt = 0;
         for (int g = c.grp_base; g < c.grp_base + c.n_grp; ++g) {
-            if (g > c.grp_base) lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g, lane, x, sl);
-            lung_consume(P, g, x, sl, thr, cnt, slots);
+            const uint64_t sl = P.L.slot[(size_t)g * 64 + lane];
+            lf4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (g > c.grp_base) lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g, 0, lane, x);
+            lung_consume(P, g, 0, x, acc, thr, cnt);
+            if (cst(P.L.grp)[g].row[kLungHalf] >> 16) {  // wave-uniform: the group has a second half
+                lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g, 1, lane, x);
+                lung_consume(P, g, 1, x, acc, thr, cnt);
+            }
+            lung_emit(sl, acc, slots);
         }
         lds_wave_order();
         // the next item's first group in flight during this item's combine
@@ -944,7 +954,7 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
             nc = cst(P.L.chunk)[nj];
             nrow = row_of(ne);
             nrsrc = rsrc_of(nrow);
-            lung_fetch<GATHER>(P, nrsrc, nrow, nc.seg_base, nc.grp_base, lane, x, sl);
+            lung_fetch<GATHER>(P, nrsrc, nrow, nc.seg_base, nc.grp_base, 0, lane, x);
         }
         float v;
         if (c.gen < 0) {
@@ -1066,7 +1076,7 @@ __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, i
 // Items: lung_item_of.
 // GATHER: C-order rows (vision handles, after k_dense_vis; no zeroing).
 template <bool GATHER>
-__global__ __launch_bounds__(256) void k_dense(DenseParams P, int n_env) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_dense(DenseParams P, int n_env) {
     __shared__ __attribute__((aligned(16))) float dsm[4 * kLungWaveFloats];
     // wave-uniform (readfirstlane): the item, its chunk and group records then
     // live in SGPRs and the plan is read by scalar loads

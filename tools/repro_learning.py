@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--scratch", default="/tmp/repro_learning")
     ap.add_argument("--step-mode", default=None)
     ap.add_argument("--seed", type=int, default=None, help="override the config's seed (seed spread)")
+    ap.add_argument("--fused-update", type=int, default=None,
+                    help="0: the torch autograd update (train.py's own arithmetic path) instead of rt_ppo_update")
     a = ap.parse_args()
     cfg = config_mod.load(a.config)
     cfg.total_timesteps = a.total
@@ -70,6 +72,8 @@ def main():
         cfg.seed = a.seed
     if a.step_mode:
         cfg.step_mode = a.step_mode
+    if a.fused_update is not None:
+        cfg.fused_update = bool(a.fused_update)
     cfg = config_mod.derive(cfg)
     torch.manual_seed(cfg.seed)
     np.random.seed(cfg.seed)
@@ -99,6 +103,7 @@ def main():
     out = {"config": {k: cfg[k] for k in ("exp_name", "seed", "num_envs", "num_steps", "num_minibatches",
                                           "update_epochs", "learning_rate", "anneal_lr", "total_timesteps",
                                           "num_iterations", "visionless", "grid", "tumour_library", "step_mode")},
+           "fused_update": bool(cfg.get("fused_update", True)),
            "wall_s": wall, "env_steps": int(cfg.num_iterations * cfg.batch_size),
            "logged_rows": len(s_tot), "bin_env_steps": bin_w,
            "reference": "README.md:44 / notebooks/figures/reward_curves.png: episodic total reward plateau ~4.6 "
