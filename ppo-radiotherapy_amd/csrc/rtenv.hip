@@ -47,7 +47,7 @@ namespace {
 constexpr int kStepThreads = 256;
 // variant builds (tools/build_variant.py) override this for sweeps
 #ifndef RT_PIPE_DENSE_BPC
-#define RT_PIPE_DENSE_BPC 5
+#define RT_PIPE_DENSE_BPC 8
 #endif
 
 // Library events order work between the library's own streams on one device
