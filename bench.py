@@ -101,6 +101,7 @@ def c3d_fwd_flop(grid) -> int:
         pads = [(d - 2) % 2 for d in dims] if pad is None else [0, 0, 0]
         dims = [(c + 2 * p - 2) // 2 + 1 for c, p in zip(conv, pads)]
     return total
+WINO_USEFUL = 64 / 216  # F(2x2x2, 3x3x3): products per window and channel pair / direct MACs
 UPDATE_MACS_PER_SAMPLE = (9 * 64 + 64 * 64 + 64 * 6) + (9 * 64 + 64 * 64 + 64) \
     + (2 * 64 * 6 + 2 * 64 * 64 + 9 * 64) + (2 * 64 + 2 * 64 * 64 + 9 * 64)
 
@@ -540,7 +541,7 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
             ams.append(torch.empty((batch, 16, *od), dtype=torch.uint8, device=dev))
             grads.append(torch.randn((batch, 16, *od), device=dev) * 1e-3)
         stages, tot = {}, {"fwd_ms": 0.0, "train_ms": 0.0, "fwd_exec": 0, "train_mfma": 0, "train_valu": 0,
-                           "fwd_eff": 0, "train_eff": 0}
+                           "fwd_eff": 0, "train_eff": 0, "train_useful": 0}
         dims = list(grid)
         for k, (layer, od) in enumerate(plan):
             cpg = cins[k] // int(layer.groups)
@@ -591,6 +592,9 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
             tot["train_valu"] += f_wg
             tot["fwd_eff"] += direct
             tot["train_eff"] += 2 * direct + (direct if k > 0 else 0)
+            # useful Winograd work: 64 products per 2x2x2 window and channel pair against
+            # the direct form's 8 x 27 = 216 (no zero-padded rows or channel lanes)
+            tot["train_useful"] += direct * WINO_USEFUL * (2 if k > 0 else 1) + f_wg
         return stages, tot, [a for a in acts[1:]]
 
     stages, tot, y32 = run_stages("f32")
@@ -635,12 +639,14 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
                   "(conv1, the grouped stages' forward and data gradient); weight gradients f32; "
                   "effective = direct-conv FLOP / time (not a utilisation)"}
     fwd_frac = tot["fwd_exec"] / (tot["fwd_ms"] * 1e-3) / F32_MFMA_PEAK
+    fwd_useful = tot["fwd_eff"] * WINO_USEFUL
     exec_train = tot["train_mfma"] + tot["train_valu"]
     return {"bound": "mfma", "workload": f"C3D extractor stages, {batch} observations at {grid[0]}^3 "
                                          "(BASELINE configs[3] rollout step), f32",
             "peak": F32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
             "forward": {"ms": tot["fwd_ms"], "executed_flop": tot["fwd_exec"],
-                        "achieved": tot["fwd_exec"] / tot["fwd_ms"] / 1e9, "frac": fwd_frac,
+                        "achieved": tot["fwd_exec"] / tot["fwd_ms"] / 1e9, "frac": fwd_frac, "executed_frac": fwd_frac,
+                        "useful_flop": fwd_useful, "useful_frac": fwd_useful / (tot["fwd_ms"] * 1e-3) / F32_MFMA_PEAK,
                         "effective_flop": tot["fwd_eff"],
                         "effective_tflops": tot["fwd_eff"] / tot["fwd_ms"] / 1e9,
                         "work": "Winograd MFMA wave-instructions x 2,048 FLOP (rt_conv_mfma_count = SQ_INSTS_MFMA)"},
@@ -648,12 +654,18 @@ def c3d_roofline(dev, lib, grid, batch: int = 512, reps: int = 5):
                            "executed_mfma_flop": tot["train_mfma"], "executed_valu_flop": tot["train_valu"],
                            "achieved": exec_train / tot["train_ms"] / 1e9,
                            "frac": exec_train / (tot["train_ms"] * 1e-3) / F32_MFMA_PEAK,
+                           "executed_frac": exec_train / (tot["train_ms"] * 1e-3) / F32_MFMA_PEAK,
+                           "useful_flop": tot["train_useful"],
+                           "useful_frac": tot["train_useful"] / (tot["train_ms"] * 1e-3) / F32_MFMA_PEAK,
                            "effective_flop": tot["train_eff"],
                            "effective_tflops": tot["train_eff"] / tot["train_ms"] / 1e9,
                            "work": "MFMA: training forward + grouped data gradients (Winograd); VALU: the sparse "
                                    "weight gradients (one 27-tap argmax patch per channel pair and pooled window)"},
             "stages": stages, "bf16x3": bf,
             "pmc_source": pmc["source"] if pmc else None,
+            "frac_note": "frac = executed_frac: the MFMA wave-instructions the kernels issue (zero-padded rows and "
+                         "channel lanes included, since round 5); useful_frac: the Winograd products the "
+                         "convolution needs (direct FLOP x 64/216) plus the sparse weight gradients' FMAs",
             "timing": "HIP events on the kernels' stream, mean of 5 back-to-back launches"}
 
 

@@ -844,9 +844,14 @@ __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer
             // only the row's nl lanes load (exec-masked: the lanes past it take no
             // texture-address cycles and fetch no line of the next row); aux 2:
             // non-temporal (streamed once)
+#ifdef RT_LUNG_PROBE  // timing-only variant build: whole 1-KiB rows, contiguous (wrong sums)
+            x[k] = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rsrc, 16 * lane, 4 * (seg_base + 256 * (h * kLungHalf + k)), 2));
+#else
             lf4 v = lf4{0.0f, 0.0f, 0.0f, 0.0f};
             if (lane < nl) v = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * lane, 4 * r0, 2));
             x[k] = v;
+#endif
         }
     }
 }
@@ -894,8 +899,14 @@ __device__ __forceinline__ void lds_wave_order() {
 // wave's strided items visit every chunk size (an env-major order without a
 // rotation pins each wave to one chunk index: a 250x spread of bytes).
 __device__ __forceinline__ void lung_item_of(const LungParams& L, int n_env, int e_begin, int i, int& e, int& j) {
+#ifdef RT_LUNG_ENVMAJOR  // variant: env-major, chunk index rotated by a hash of the env
+    const int r = i / L.n_chunk;
+    e = e_begin + r;
+    j = (int)(((uint32_t)(i - r * L.n_chunk) + (((uint32_t)r * 2654435761u) >> 16)) % (uint32_t)L.n_chunk);
+#else
     e = e_begin + i % n_env;
     j = cst(L.order)[i / n_env];
+#endif
 }
 
 // The (env, chunk) items of envs [e_begin, e_begin + n_env) a wave takes:
@@ -957,7 +968,12 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
             lung_fetch<GATHER>(P, nrsrc, nrow, nc.seg_base, nc.grp_base, 0, lane, x);
         }
         float v;
+#ifdef RT_LUNG_PROBE2  // timing-only variant build: no combine (wrong sums)
+        v = slots[lane];
+        if (0) {
+#else
         if (c.gen < 0) {
+#endif
             // a whole buffer: lane = leaf (64 x 128 elements), leaf formula, then
             // the perfect tree over the 64 leaves as an xor butterfly
             const lf4 a = reinterpret_cast<const lf4*>(slots)[2 * lane];
