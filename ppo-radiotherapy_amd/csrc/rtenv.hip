@@ -757,7 +757,6 @@ struct LungParams {
     const int32_t* tail_off;  // per partial buffer: [n_leaf + 1] into tail_pos
     const int32_t* tail_pos;  // segment positions of each leaf's tail voxels, C order
     const int32_t* lpos;      // C-order rows (vision): segment position -> voxel (-1: pad); null: lung-first
-    const int32_t* order;     // chunk indices, largest first (the persistent item order)
     int32_t n_chunk;
 };
 
@@ -844,14 +843,9 @@ __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer
             // only the row's nl lanes load (exec-masked: the lanes past it take no
             // texture-address cycles and fetch no line of the next row); aux 2:
             // non-temporal (streamed once)
-#ifdef RT_LUNG_PROBE  // timing-only variant build: whole 1-KiB rows, contiguous (wrong sums)
-            x[k] = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               rsrc, 16 * lane, 4 * (seg_base + 256 * (h * kLungHalf + k)), 2));
-#else
             lf4 v = lf4{0.0f, 0.0f, 0.0f, 0.0f};
             if (lane < nl) v = __builtin_bit_cast(lf4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * lane, 4 * r0, 2));
             x[k] = v;
-#endif
         }
     }
 }
@@ -892,21 +886,18 @@ __device__ __forceinline__ void lds_wave_order() {
     asm volatile("" ::: "memory");
 }
 
-// Item i of a launch -> chunk order[i / n_env] (chunk-major, largest chunks
-// first), env e_begin + i % n_env: the waves in flight at once read the same
-// chunk of many dose rows (1 MiB apart; an env-major order -- neighbouring
-// chunks of a few rows -- streamed 4.1 vs 5.1 TB/s alone, round 6), and a
-// wave's strided items visit every chunk size (an env-major order without a
-// rotation pins each wave to one chunk index: a 250x spread of bytes).
-__device__ __forceinline__ void lung_item_of(const LungParams& L, int n_env, int e_begin, int i, int& e, int& j) {
-#ifdef RT_LUNG_ENVMAJOR  // variant: env-major, chunk index rotated by a hash of the env
+// Item i of a launch -> env e_begin + i / n_chunk, chunk (i + h(env)) mod
+// n_chunk with h a multiplicative hash: env-major, so the waves in flight at
+// once read neighbouring buffers of a few hundred dose rows, and the rotation
+// makes a wave's strided items (stride = the grid's waves, a multiple of the
+// chunk count) visit every chunk size -- without it each wave keeps one chunk
+// index: a 250x spread of bytes per wave (4.1 TB/s alone), and the chunk-major
+// order (the waves on the same buffer of every row) streamed 5.5 against 5.7
+// TB/s alone (rocprofv3, round 6).
+__device__ __forceinline__ void lung_item_of(const LungParams& L, int e_begin, int i, int& e, int& j) {
     const int r = i / L.n_chunk;
     e = e_begin + r;
     j = (int)(((uint32_t)(i - r * L.n_chunk) + (((uint32_t)r * 2654435761u) >> 16)) % (uint32_t)L.n_chunk);
-#else
-    e = e_begin + i % n_env;
-    j = cst(L.order)[i / n_env];
-#endif
 }
 
 // The (env, chunk) items of envs [e_begin, e_begin + n_env) a wave takes:
@@ -932,7 +923,7 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
     };
     int it = first;
     int e, j;
-    lung_item_of(P.L, n_env, P.e_begin, it, e, j);
+    lung_item_of(P.L, P.e_begin, it, e, j);
     LChunk c = cst(P.L.chunk)[j];
     const float* row = row_of(e);
     __amdgpu_buffer_rsrc_t rsrc = rsrc_of(row);
@@ -961,19 +952,14 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
         const float* nrow = row;
         __amdgpu_buffer_rsrc_t nrsrc = rsrc;
         if (nit < n_items) {
-            lung_item_of(P.L, n_env, P.e_begin, nit, ne, nj);
+            lung_item_of(P.L, P.e_begin, nit, ne, nj);
             nc = cst(P.L.chunk)[nj];
             nrow = row_of(ne);
             nrsrc = rsrc_of(nrow);
             lung_fetch<GATHER>(P, nrsrc, nrow, nc.seg_base, nc.grp_base, 0, lane, x);
         }
         float v;
-#ifdef RT_LUNG_PROBE2  // timing-only variant build: no combine (wrong sums)
-        v = slots[lane];
-        if (0) {
-#else
         if (c.gen < 0) {
-#endif
             // a whole buffer: lane = leaf (64 x 128 elements), leaf formula, then
             // the perfect tree over the 64 leaves as an xor butterfly
             const lf4 a = reinterpret_cast<const lf4*>(slots)[2 * lane];
@@ -2040,7 +2026,7 @@ struct LungPlanHost {
     std::vector<uint64_t> slot;
     std::vector<LGeneric> gen;
     std::vector<uint32_t> ops;
-    std::vector<int32_t> lvl_end, tail_off, tail_pos, order;
+    std::vector<int32_t> lvl_end, tail_off, tail_pos;
 };
 
 // Lays out the lung segment by numpy buffer, then by chain (LChunk comment):
@@ -2155,12 +2141,6 @@ int build_lung_plan(const uint8_t* lungs, int64_t V, LungPlanHost& P) {
     }
     P.n_seg = seg;
     P.lpos.insert(P.lpos.end(), 4 * 64, -1);
-    // the persistent item order: chunks by size, largest first
-    const int nc = (int)P.chunk.size();
-    auto csize = [&](int j) { return (j + 1 < nc ? P.chunk[j + 1].seg_base : seg) - P.chunk[j].seg_base; };
-    P.order.resize(nc);
-    for (int j = 0; j < nc; ++j) P.order[j] = j;
-    std::stable_sort(P.order.begin(), P.order.end(), [&](int a, int b) { return csize(a) > csize(b); });
     return RT_OK;
 }
 
@@ -2316,8 +2296,7 @@ int upload_lung_plan(rt_env* env, const LungPlanHost& lp) {
     if ((rc = dev_upload(env, &L.chunk, lp.chunk)) || (rc = dev_upload(env, &L.grp, lp.grp)) ||
         (rc = dev_upload(env, &L.slot, lp.slot)) || (rc = dev_upload(env, &L.gen, lp.gen)) ||
         (rc = dev_upload(env, &L.ops, lp.ops)) || (rc = dev_upload(env, &L.lvl_end, lp.lvl_end)) ||
-        (rc = dev_upload(env, &L.tail_off, lp.tail_off)) || (rc = dev_upload(env, &L.tail_pos, lp.tail_pos)) ||
-        (rc = dev_upload(env, &L.order, lp.order)))
+        (rc = dev_upload(env, &L.tail_off, lp.tail_off)) || (rc = dev_upload(env, &L.tail_pos, lp.tail_pos)))
         return rc;
     L.lpos = nullptr;
     if (!env->lung_first && (rc = dev_upload(env, &L.lpos, lp.lpos))) return rc;
