@@ -385,12 +385,14 @@ def stream_ceilings(dev, lib_obj, gib: float = 4.0, reps: int = 8) -> dict:
     return out
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r05", "r05_s23_k_dense_persist_pmc.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r06", "r06_final_k_dense_pmc.json")
 # rocprofv3 --kernel-trace --stats of this bench's default command, committed
 # with a sidecar <csv>.meta.json naming the commit of the tree it was measured
 # on; used (labelled "historical") when --rocprof-stats does not name the
 # stats of the current run
-ROCPROF_FILE = os.path.join(REPO, "profiles", "r05", "r05_s23_kernel_stats.csv")
+ROCPROF_FILE = os.path.join(REPO, "profiles", "r06", "r06_final_kernel_stats.csv")
+# the lung-first stream kernel (k_dense<true> gathers from C-order rows)
+DENSE_KERNEL = "k_dense<false>"
 
 
 def load_rocprof(kernel: str, path: str | None = None):
@@ -424,14 +426,14 @@ def load_rocprof(kernel: str, path: str | None = None):
     return None
 
 
-def load_pmc(grid, envs, kernel="k_dense"):
+def load_pmc(grid, envs, pipelined=False, kernel="k_dense"):
     """Per-launch HBM traffic (bytes) of the dense stream from the committed
-    rocprofv3 PMC runs, gfx950 FETCH_SIZE x2 correction applied there:
-    k_dense_persist (the pipelined rollout, 2048 envs per launch) from
+    rocprofv3 PMC runs, gfx950 FETCH_SIZE x2 correction applied there: the
+    pipelined rollout (k_dense over 2048 envs per launch) from
     tools/probe_dense_pmc.py + tools/dense_pmc_segments.py on the current
     kernel -> {"value_window": B, "steady_window": B}; the older single-run
     files (profiles/{kernel}_pmc.json) otherwise.  None when no run matches."""
-    if kernel == "k_dense_persist":
+    if pipelined:
         try:
             with open(PMC_FILE) as f:
                 d = json.load(f)
@@ -957,8 +959,8 @@ def main():
     launches = max(kcalls, 1) / K  # launches per step (2: pipelined env groups)
     dense_ms = kms["k_dense"]  # per step: the launches of all env groups
     kernel_name = "k_dense"
-    if launches > 1.5:  # pipelined: k_dense_persist over half the envs (tools/archive/gpu_dense_persist_pmc.sh)
-        traffic = load_pmc(grid, a.envs // 2, "k_dense_persist")
+    if launches > 1.5:  # pipelined: k_dense over half the envs per launch (tools/r06/gpu_final.sh)
+        traffic = load_pmc(grid, a.envs // 2, pipelined=True)
     else:  # whole-handle grid launches (tools/archive/gpu_dense_pmc.sh, bench.py --env-only)
         traffic = load_pmc(grid, a.envs)
     achieved = bytes_launch / (dense_ms * 1e-3)  # = per-launch bytes / per-launch duration (per step)
@@ -979,7 +981,7 @@ def main():
         # the same kernel in the committed rocprofv3 stats of this command: the
         # HIP-event interval above also spans the dispatch after the turn
         # hand-off (~9 us), rocprofv3 times the kernel alone
-        rp = load_rocprof("k_dense_persist", a.rocprof_stats)
+        rp = load_rocprof(DENSE_KERNEL, a.rocprof_stats)
         if rp is not None:
             rp["achieved"] = bytes_launch / launches / (rp["avg_ms"] * 1e-3) / 1e9
             rp["frac"] = rp["achieved"] * 1e9 / HBM_PEAK

@@ -2774,7 +2774,10 @@ FinishParams finish_params(const rt_env* env, float* obs, float* reward, uint8_t
 // actual request.
 int allow_lds(const void* kernel, bool& raised) {
     if (raised) return RT_OK;
-    const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncAttributes fa{};  // the kernel's static LDS counts against the same 160 KiB
+    if (hipFuncGetAttributes(&fa, kernel) != hipSuccess) return fail(RT_EDEVICE, "hipFuncGetAttributes");
+    const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024 - (int)fa.sharedSizeBytes);
     if (e != hipSuccess) return fail(RT_EDEVICE, std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(e));
     raised = true;
     return RT_OK;

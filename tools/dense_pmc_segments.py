@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
-"""FETCH_SIZE / WRITE_SIZE per k_dense_persist dispatch (two rocprofv3 --pmc
+"""FETCH_SIZE / WRITE_SIZE per k_dense dispatch (two rocprofv3 --pmc
 runs of tools/probe_dense_pmc.py), split into its segments, with the gfx950
 corrections of MI355X_MICROARCH.md's HBM section (FETCH_SIZE x2 for wide
 coalesced 16-B reads; both counters in KiB).
 
-usage: dense_pmc_segments.py FETCH_DIR WRITE_DIR OUT.json
+usage: dense_pmc_segments.py FETCH_DIR WRITE_DIR OUT.json [KERNEL]
+
+KERNEL: a substring of the dispatch's kernel name (default "k_dense<false>",
+the lung-first stream; "k_dense_persist" for the round-5 runs)
 """
 import csv
 import glob
@@ -17,11 +20,11 @@ SEGMENTS = [("stagger_preroll", 200), ("warm", 10), ("value_window_20_steps", 40
 ENVS, LUNG_VOXELS = 2048, 96160  # per launch; lung voxels of the 64^3 resampled reference mask
 
 
-def per_dispatch(d, counter):
+def per_dispatch(d, counter, kernel):
     rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_dense_persist" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+            if kernel in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
                 rows.append((int(r.get("Dispatch_Id") or r.get("Correlation_Id")), float(r["Counter_Value"])))
     agg = {}
     for k, v in rows:  # one row per (dispatch, dimension instance) in some versions: sum them
@@ -29,10 +32,10 @@ def per_dispatch(d, counter):
     return [agg[k] for k in sorted(agg)]
 
 
-def main(fd, wd, out):
-    f, w = per_dispatch(fd, "FETCH_SIZE"), per_dispatch(wd, "WRITE_SIZE")
+def main(fd, wd, out, kernel="k_dense<false>"):
+    f, w = per_dispatch(fd, "FETCH_SIZE", kernel), per_dispatch(wd, "WRITE_SIZE", kernel)
     alg = 4 * LUNG_VOXELS * ENVS
-    res = {"kernel": "k_dense_persist", "envs_per_launch": ENVS, "grid": [64, 64, 64], "lung_voxels": LUNG_VOXELS,
+    res = {"kernel": kernel, "envs_per_launch": ENVS, "grid": [64, 64, 64], "lung_voxels": LUNG_VOXELS,
            "dispatches": [len(f), len(w)], "algorithmic_bytes_per_launch": alg,
            "correction": "FETCH_SIZE x2 (gfx950 wide coalesced reads), KiB->B", "segments": {}}
     i = 0
@@ -50,4 +53,4 @@ def main(fd, wd, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

@@ -1,10 +1,10 @@
 """PMC companion of bench.py's dense pipelined rollout (4096 envs x 64^3, two
-env groups, k_dense_persist over 2048 envs per launch), in bench.py's order:
+env groups, k_dense over 2048 envs per launch), in bench.py's order:
 200 launches of the stagger pre-roll (100 one-step calls; every env's episode
 clock offset by e % 100), 10 (5 warm steps), 40 (a 20-step window, the
 `value` shape) and 128 (a 64-step window, the steady-state shape).  With the
 phases staggered ~1 % of the envs reset every step in both windows, each
-reset zeroing its dose row inside k_dense_persist.
+reset zeroing its dose row inside k_dense.
 tools/dense_pmc_segments.py splits the counter rows by that order."""
 import os
 import sys
