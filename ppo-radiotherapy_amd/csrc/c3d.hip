@@ -921,6 +921,10 @@ int launch_ring(const RingGeom& rg, int32_t B, const float* x, const int64_t* ro
 constexpr int kWinoC1Nth = RT_WINO_C1_NTH;
   // threads per block of conv1's Winograd forward
 
+#ifndef RT_WINO_PATCH_BATCH
+#define RT_WINO_PATCH_BATCH 1
+#endif
+
 template <int CPG>
 constexpr int wino_u_floats() {  // U in LDS: 16 columns x 64 lanes x 4 xi_z x CPG / 4 quads
     return 16 * 64 * 4 * (CPG / 4);
@@ -957,6 +961,7 @@ void k_conv_wino(WinoParams P) {
     constexpr int NW = NTH / 64;
     constexpr int NS = CPG / 4;  // channel quads (MFMA k-steps) per xi
     constexpr bool kWinoPrio = CPG == 4 && COG == 16;  // conv1
+    constexpr bool kPatchBatch = RT_WINO_PATCH_BATCH && COG != 4;  // (conv3: spills at 3 waves per SIMD)
     const Geom& g = P.rg.g;
     const int SLOT = P.rg.SLOT;
     const int b = blockIdx.z / P.G, grp = blockIdx.z - b * P.G;
@@ -1061,6 +1066,10 @@ void k_conv_wino(WinoParams P) {
                 if constexpr (kWinoPrio) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
+                    // the whole half's patch reads issued before its transform
+                    // (one exposed LDS latency instead of one per 2 dy rows)
+                    float2 pa[4][4], pc[4][4];
+                    if constexpr (kPatchBatch) {
 #pragma unroll
                     for (int dz = 0; dz < 4; ++dz) {
                         int sl = sb + dz;
@@ -1068,8 +1077,28 @@ void k_conv_wino(WinoParams P) {
                         const float* p = xs + sl * SLOT + 4 * s * g.CS + xo;
 #pragma unroll
                         for (int dy = 0; dy < 4; ++dy) {
-                            const float2 a = *reinterpret_cast<const float2*>(p + dy * g.YS);
-                            const float2 c = *reinterpret_cast<const float2*>(p + dy * g.YS + 2);
+                            pa[dz][dy] = *reinterpret_cast<const float2*>(p + dy * g.YS);
+                            pc[dz][dy] = *reinterpret_cast<const float2*>(p + dy * g.YS + 2);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    }
+#pragma unroll
+                    for (int dz = 0; dz < 4; ++dz) {
+                        int sl = sb + dz;
+                        sl = sl >= kRing ? sl - kRing : sl;
+                        const float* p = xs + sl * SLOT + 4 * s * g.CS + xo;
+                        (void)p;
+#pragma unroll
+                        for (int dy = 0; dy < 4; ++dy) {
+                            float2 a, c;
+                            if constexpr (kPatchBatch) {
+                                a = pa[dz][dy];
+                                c = pc[dz][dy];
+                            } else {
+                                a = *reinterpret_cast<const float2*>(p + dy * g.YS);
+                                c = *reinterpret_cast<const float2*>(p + dy * g.YS + 2);
+                            }
                             float* q = v[s] + (dz * 4 + dy) * 2;
                             if (h == 0) {  // B^T along x, rows 0, 1
                                 q[0] = a.x - c.x;
