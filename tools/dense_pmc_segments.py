@@ -16,7 +16,11 @@ import os
 import statistics
 import sys
 
-SEGMENTS = [("stagger_preroll", 200), ("warm", 10), ("value_window_20_steps", 40), ("steady_window_64_steps", 128)]
+# tools/probe_dense_pmc.py's dispatch order: reset() (1), the stagger pre-roll
+# (100 x a masked reset + one two-group step: 300), 5 warm steps, the 20-step
+# and 64-step windows (two launches per step)
+SEGMENTS = [("reset_and_stagger_preroll", 301), ("warm", 10), ("value_window_20_steps", 40),
+            ("steady_window_64_steps", 128)]
 ENVS, LUNG_VOXELS = 2048, 96160  # per launch; lung voxels of the 64^3 resampled reference mask
 
 
