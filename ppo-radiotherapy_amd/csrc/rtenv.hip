@@ -45,9 +45,11 @@
 namespace {
 
 constexpr int kStepThreads = 256;
-// variant builds (tools/build_variant.py) override this for sweeps
+// k_dense blocks per CU in the pipelined dense rollout: all its 5 resident
+// blocks (16-row fetches; blocks per CU 4 / 5 at 16 rows: 11.3 / 12.25 M env
+// steps/s; variant builds override this for sweeps)
 #ifndef RT_PIPE_DENSE_BPC
-#define RT_PIPE_DENSE_BPC 8
+#define RT_PIPE_DENSE_BPC 5
 #endif
 
 // Library events order work between the library's own streams on one device
@@ -816,7 +818,14 @@ typedef float lf4 __attribute__((ext_vector_type(4)));
 // branch per row: the profile of round 6 had the texture-address unit 73 %
 // busy when every group issued all 16 rows); buffer loads, the row offset in
 // an SGPR.
-constexpr int kLungHalf = 8;  // rows per fetch: a group's 16 rows in two halves
+// Rows per fetch: a group's 16 rows at once, at 88 VGPRs = 5 waves per SIMD.
+// (8-row halves at 57 VGPRs and 8 waves per SIMD: 11.4 M env steps/s in the
+// pipelined rollout, the stream holding every wave slot of the CU; 10 rows at
+// 8 waves, 12 at 7: no better; 16 rows at 5 waves: 12.25 M, the other group's
+// chain finds its slots again -- profiles/r06/r06_s18_fetch_rows_sweep.txt.)
+// The half index h stays for a fetch size below 16.
+constexpr int kLungHalf = 16;
+constexpr int kDenseWavesPerSimd = 5;
 
 template <bool GATHER>
 __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer_rsrc_t rsrc, const float* row,
@@ -824,7 +833,7 @@ __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer
     const auto G = cst(P.L.grp) + g;
     uint32_t ri[kLungHalf];
 #pragma unroll
-    for (int k = 0; k < kLungHalf; ++k) ri[k] = G->row[h * kLungHalf + k];  // one s_load_dwordx8, one wait
+    for (int k = 0; k < kLungHalf; ++k) ri[k] = h * kLungHalf + k < 16 ? G->row[h * kLungHalf + k] : 0u;  // one s_load_dwordx16, one wait
 #pragma unroll
     for (int k = 0; k < kLungHalf; ++k) {
         const int nl = (int)(ri[k] >> 16);
@@ -850,14 +859,14 @@ __device__ __forceinline__ void lung_fetch(const DenseParams& P, __amdgpu_buffer
     }
 }
 
-// rows h*8 .. h*8+7 of the lane's 4 chains in order (numpy's r[j] += a[i]
+// the fetched rows of the lane's 4 chains in order (numpy's r[j] += a[i]
 // sequences) onto acc, and their over-threshold count
 __device__ __forceinline__ void lung_consume(const DenseParams& P, int g, int h, const lf4 (&x)[kLungHalf], lf4& acc,
                                              float thr, int& cnt) {
     const auto G = cst(P.L.grp) + g;
 #pragma unroll
     for (int k = 0; k < kLungHalf; ++k) {
-        if (G->row[h * kLungHalf + k] >> 16) {  // wave-uniform: a row of this group
+        if (h * kLungHalf + k < 16 && (G->row[h * kLungHalf + k] >> 16)) {  // wave-uniform: a row of this group
             acc.x = acc.x + x[k].x;
             acc.y = acc.y + x[k].y;
             acc.z = acc.z + x[k].z;
@@ -938,7 +947,7 @@ __device__ void lung_stream(const DenseParams& P, int n_env, int first, int stri
             lf4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
             if (g > c.grp_base) lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g, 0, lane, x);
             lung_consume(P, g, 0, x, acc, thr, cnt);
-            if (cst(P.L.grp)[g].row[kLungHalf] >> 16) {  // wave-uniform: the group has a second half
+            if (kLungHalf < 16 && (cst(P.L.grp)[g].row[kLungHalf % 16] >> 16)) {  // wave-uniform: the group has a second half
                 lung_fetch<GATHER>(P, rsrc, row, c.seg_base, g, 1, lane, x);
                 lung_consume(P, g, 1, x, acc, thr, cnt);
             }
@@ -1078,7 +1087,8 @@ __device__ void zero_reset_share(const DenseParams& P, int e_begin, int n_env, i
 // Items: lung_item_of.
 // GATHER: C-order rows (vision handles, after k_dense_vis; no zeroing).
 template <bool GATHER>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_dense(DenseParams P, int n_env) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kDenseWavesPerSimd))) void k_dense(DenseParams P,
+                                                                                                    int n_env) {
     __shared__ __attribute__((aligned(16))) float dsm[4 * kLungWaveFloats];
     // wave-uniform (readfirstlane): the item, its chunk and group records then
     // live in SGPRs and the plan is read by scalar loads
