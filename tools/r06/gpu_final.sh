@@ -46,7 +46,7 @@ python3 - "$O" <<'PY'
 import json, sys
 O = sys.argv[1]
 for i in (1, 2):
-    d = json.load(open(f"{O}/bench{i}.json")); r = d["roofline"]; s = d["steady_state"]
+    d = json.loads([l for l in open(f"{O}/bench{i}.json") if l.startswith("{")][-1]); r = d["roofline"]; s = d["steady_state"]
     rp = r.get("rocprof") or {}
     print("bench", i, round(d["value"] / 1e6, 3), "M", round(d["ms_per_step"], 4), "steady", round(s["ms_per_step"], 4),
           "frac", round(r["frac"], 3), "rocprof_ms", rp.get("avg_ms"), "rocprof_frac", rp.get("frac"),
@@ -54,11 +54,11 @@ for i in (1, 2):
           "coll", d.get("ppo_update_ms_collective_path"), "train", round(d["train_env_steps_per_s"] / 1e6, 2),
           "incr", round(d["other_step_mode"]["env_steps_per_s"] / 1e6, 2), "cpu", d["cpu_baseline"].get("value"))
 for g in (1, 3):
-    d = json.load(open(f"{O}/groups{g}.json")); s = d.get("steady_state", {})
+    d = json.loads([l for l in open(f"{O}/groups{g}.json") if l.startswith("{")][-1]); s = d.get("steady_state", {})
     print("groups", g, round(d["value"] / 1e6, 3), "M", round(d["ms_per_step"], 4), "steady", s.get("ms_per_step"),
           "kms", d["roofline"].get("kernel_ms_all"))
 for n in ("vision_f32", "vision128_f32"):
-    d = json.load(open(f"{O}/{n}.json"))
+    d = json.loads([l for l in open(f"{O}/{n}.json") if l.startswith("{")][-1])
     print(n, "rollout", round(d["value"]), "minibatch ms", round(d["ppo_update_ms"], 2), "iteration", round(d["train_env_steps_per_s"]))
 PY
 echo ALLDONE
