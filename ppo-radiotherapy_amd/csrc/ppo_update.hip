@@ -1072,6 +1072,7 @@ struct ReduceAdamParams {
     int32_t flat_off[13];  // flat index of each tensor's first element (params_d[t] - flat_param_d)
     unsigned* counter;
     unsigned target;
+    unsigned max_polls;  // the bounded wait (1 << 24; RT_PPO_FORCE_LOST_ARRIVAL: 16 and an unreachable target)
     int* fault;      // host-mapped sticky flag (reduce_adam_fault)
     int* dev_fault;  // the same event within this rt_ppo_update call, in device memory
 };
@@ -1138,7 +1139,7 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce_adam(ReduceAdamParams Q) {
         int spins = 0;
         while (__hip_atomic_load(Q.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < Q.target) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1 << 24)) {
+            if ((unsigned)++spins > Q.max_polls) {
                 arrived = 0;
                 break;
             }
@@ -1515,6 +1516,16 @@ bool force_split_update() {
     return v && v[0] == '1';
 }
 
+// Debug knob (tests): RT_PPO_FORCE_LOST_ARRIVAL=1 makes every block of the
+// fused reduce + Adam wait for an arrival count that never comes, with a
+// 16-poll budget: the lost-arrival path (no write, device word, sticky
+// host flag, RT_EDEVICE from then on) runs as it would on a grid that was
+// not co-resident.  The flag is per process: tests run it in a child.
+bool force_lost_arrival() {
+    const char* v = std::getenv("RT_PPO_FORCE_LOST_ARRIVAL");
+    return v && v[0] == '1';
+}
+
 // k_ppo_reduce_adam's grid arrival needs all kReduceBlocks blocks resident at
 // once: checked per device against the occupancy query (cached)
 bool reduce_adam_coresident() {
@@ -1633,6 +1644,7 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
     Q.counter = counter;
     Q.fault = fault_d;
     Q.dev_fault = dev_fault;
+    const bool lost = force_lost_arrival();
     for (int i = 0; i < n_minibatches; ++i) {
         int rc = ppo_grad_launch(params_d, grads_d, batch, perm_d + (int64_t)i * mb_size, mb_size,
                                  adv_stats_d ? adv_stats_d + 2 * i : nullptr, hp, workspace_d, workspace_floats,
@@ -1641,7 +1653,8 @@ extern "C" int rt_ppo_update(const float* const* params_d, float* const* grads_d
         Q.R = reduce_params(grads_d, mb_size, hp, workspace_d, workspace_floats, stats_d, stats_accum_d);
         Q.A = adam_params(n_flat, flat_param_d, flat_grad_d, exp_avg_d, exp_avg_sq_d, step0 + i, lr, hp, norm_part,
                           1.0f);
-        Q.target = (unsigned)((i + 1) * kReduceBlocks);
+        Q.target = lost ? 0xFFFFFFFFu : (unsigned)((i + 1) * kReduceBlocks);
+        Q.max_polls = lost ? 16u : (1u << 24);
         hipLaunchKernelGGL(k_ppo_reduce_adam, dim3(kReduceBlocks), dim3(1024), 0, st, Q);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return rt_internal_fail(RT_ELAUNCH, hipGetErrorString(e));

@@ -493,3 +493,47 @@ def test_shuffle_adv_equals_separate_calls(n, mb, epochs):
     assert torch.equal(p1[0].sort().values, torch.arange(n, device=dev))  # a permutation
     assert L.rt_ppo_shuffle_adv(n, epochs, keys, p2.data_ptr(), adv.data_ptr(), mb, q2.data_ptr(), s2.data_ptr(),
                                 ws.data_ptr(), ws.numel(), None) == -1  # exactly one output form
+
+
+def test_lost_arrival_writes_nothing_and_reports():
+    """The fused reduce + Adam's lost-arrival path, forced
+    by the debug knob RT_PPO_FORCE_LOST_ARRIVAL (an arrival count that never
+    comes, a 16-poll budget): the update leaves parameters and Adam moments
+    bitwise untouched, rt_ppo_status and the trainer's check_device_status
+    report RT_EDEVICE after the sync, and the next update call refuses.  The
+    fault flag is sticky per process, so the case runs in a child process."""
+    import subprocess
+    import sys
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = f"""
+import os, sys
+sys.path[:0] = [{os.path.dirname(here)!r}, {here!r}]
+import _rtpkg
+import torch
+import test_gpu_trainer as T
+from ppo_radiotherapy_amd import _lib
+tr = T._make(fused=True)
+p0, m0, v0 = tr.flat_param.clone(), tr._exp_avg.clone(), tr._exp_avg_sq.clone()
+os.environ["RT_PPO_FORCE_LOST_ARRIVAL"] = "1"
+tr.update()
+torch.cuda.synchronize()
+assert _lib.load().rt_ppo_status() == -3, "rt_ppo_status"
+assert torch.equal(tr.flat_param, p0) and torch.equal(tr._exp_avg, m0) and torch.equal(tr._exp_avg_sq, v0)
+try:
+    tr.check_device_status()
+    raise SystemExit("check_device_status did not raise")
+except _lib.RtError as e:
+    assert "RT_EDEVICE" in str(e), e
+del os.environ["RT_PPO_FORCE_LOST_ARRIVAL"]
+try:
+    tr.update()
+    raise SystemExit("the next update ran")
+except _lib.RtError as e:
+    assert "RT_EDEVICE" in str(e), e
+print("lost-arrival ok")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "lost-arrival ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
