@@ -142,7 +142,7 @@ struct EnvState {
     int32_t* ep_len;
     int32_t* next_tumour;
     BeamSetup* setup;
-    uint8_t* mode_b;      // [N] setup[e].mode as a byte (k_dense_persist scans a group's modes)
+    uint8_t* mode_b;      // [N] setup[e].mode as a byte (k_dense scans a group's modes)
     int32_t* lung_cnt;    // incremental mode: # lung voxels with dose > threshold
     double* lung_sum;     // incremental mode: sum of dose over lung voxels
 };

@@ -2,7 +2,7 @@
 
 bench.py times `rt_env_rollout_policy` at BASELINE configs[1] (4096 envs,
 64^3): in dense step mode two env groups pipelined over two library streams
-around the persistent `k_dense_persist`, in incremental mode the persistent
+taking turns on the persistent lung stream `k_dense`, in incremental mode the persistent
 `k_rollout_policy`.  Here that exact call runs 2 x 64 = 128 rollout steps
 (crossing the t = 100 truncation of every env's first episode, irradiation
 terminations and the NEXT_STEP autoresets with their Philox tumour redraws)
