@@ -712,7 +712,7 @@ __device__ __forceinline__ float run_plan(float* tv, const uint32_t* ops, const 
 // a chunk, by chain: the chains sorted by length, 256 per group -- lane l of a
 // wave owns chains 4l..4l+3 -- group rows stored ragged: row k holds element k
 // of the group's first nk[k] chains, contiguously, padded with zero slots to a
-// whole number of 128-B lines (no line holds two rows).  A wave streams a chunk
+// whole number of 64-B sectors (no sector holds two rows).  A wave streams a chunk
 // with coalesced 16-B loads (element k of its four chains per lane, a group's
 // rows in flight: up to 16 KiB per wave), each lane summing its chains in
 // order.  The chain
@@ -732,10 +732,14 @@ constexpr int kLungLeafMax = 65;        // leaves of a buffer of <= 8192 element
 constexpr int kLungSlotFloats = 528;    // [leaf][8 classes], 16-B padded
 constexpr int kLungWaveFloats = kLungSlotFloats;  // a partial buffer's plan slots (2 x leaves) alias the slots
 constexpr int kLungGroup = 256;         // chains per group (4 per lane)
+#ifndef RT_LUNG_ROW_ALIGN
+#define RT_LUNG_ROW_ALIGN 16
+#endif
+constexpr int kLungRowAlign = RT_LUNG_ROW_ALIGN;  // floats a lung row is padded to (16: one 64-B sector)
 constexpr uint16_t kNoSlot = 0xFFFFu;
 
 struct LChunk {          // one numpy buffer holding lung voxels
-    int32_t seg_base;    // segment position of its first chain element (a multiple of 32)
+    int32_t seg_base;    // segment position of its first chain element (a multiple of kLungRowAlign)
     int32_t grp_base;    // its first chain group
     int32_t n_grp;
     int32_t gen;         // -1: a whole 8192-element buffer (butterfly); else its LGeneric record
@@ -2093,9 +2097,11 @@ int build_lung_plan(const uint8_t* lungs, int64_t V, LungPlanHost& P) {
                 int nk = 0;
                 for (size_t l = g0; l < g1; ++l) nk += (int)chains[l].vox.size() > k ? 1 : 0;
                 // a row: its float4 (ceil(nk / 4) lanes), padded to a whole number of
-                // 128-B lines, so no line holds two rows (a non-temporal load
-                // would fetch a shared line twice: +15 % HBM bytes, round 6)
-                const int nk4 = (nk + 3) / 4 * 4, span = (nk + 31) / 32 * 32;
+                // 64-B sectors (rows meeting inside a sector made the non-temporal
+                // loads fetch it twice: +15 % HBM bytes; padded to 128-B lines the
+                // pads cost 6 %, to 64-B sectors 3.5 %, and the 16-row stream ran
+                // 2.6 % faster: profiles/r06/r06_s27_row_pad_64.txt)
+                const int nk4 = (nk + 3) / 4 * 4, span = (nk + kLungRowAlign - 1) / kLungRowAlign * kLungRowAlign;
                 if (seg - ch.seg_base + span > 0xffff) return fail(RT_ELIMIT, "lung sum plan: chunk too large");
                 G.row[k] = (uint32_t)(seg - ch.seg_base) | (uint32_t)(nk4 / 4) << 16;
                 for (int l = 0; l < span; ++l) {
