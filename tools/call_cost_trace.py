@@ -5,7 +5,7 @@ launched just before the value window's opening synchronise).  The window is
 host-timed from the end of that synchronise (t0) to the end of the closing
 one (t1); this splits it into
   launch   t0 -> the first k_step_policy starts (host enqueue + dispatch)
-  fill     first k_step_policy start -> first k_dense_persist start
+  fill     first k_step_policy start -> first k_dense start
   steps    first k_dense start -> last k_dense end (the dose turns + hand-offs)
   drain    last k_dense end -> last kernel end (the last k_finish)
   return   last kernel end -> t1 (the synchronise returning)
@@ -27,9 +27,9 @@ ks = sorted(csv.DictReader(open(kt)), key=lambda r: int(r["Start_Timestamp"]))
 hs = sorted(csv.DictReader(open(ht)), key=lambda r: int(r["Start_Timestamp"]))
 short = lambda n: n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
 mark = next(i for i, r in enumerate(ks) if "k_probe_stream" in r["Kernel_Name"])
-win = ks[mark + 1: mark + 1 + 6 * K]  # 2 groups x (k_step_policy, k_dense_persist, k_finish) per step
+win = ks[mark + 1: mark + 1 + 6 * K]  # 2 groups x (k_step_policy, k_dense, k_finish) per step
 names = [short(r["Kernel_Name"]) for r in win]
-assert names.count("k_dense_persist") == 2 * K, names[:12]
+assert names.count("k_dense") == 2 * K, names[:12]
 m_end = int(ks[mark]["End_Timestamp"])
 syncs = [h for h in hs if "Synchronize" in h["Function"] and int(h["End_Timestamp"]) >= m_end - 10 ** 6]
 # the opening synchronise: the first one that ends after the marker kernel ran;
@@ -38,7 +38,7 @@ last_end = max(int(r["End_Timestamp"]) for r in win)
 t0 = int(next(h for h in syncs if int(h["End_Timestamp"]) >= m_end)["End_Timestamp"])
 t1 = int(next(h for h in syncs if int(h["End_Timestamp"]) >= last_end)["End_Timestamp"])
 first = int(win[0]["Start_Timestamp"])
-dense = [r for r in win if short(r["Kernel_Name"]) == "k_dense_persist"]
+dense = [r for r in win if short(r["Kernel_Name"]) == "k_dense"]
 d0, d1 = int(dense[0]["Start_Timestamp"]), int(dense[-1]["End_Timestamp"])
 gaps = [(int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 for a, b in zip(dense, dense[1:])]
 durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in dense]
